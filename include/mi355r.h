@@ -1,0 +1,145 @@
+/*
+ * mi355r — MI355X-native differentiable mesh rasterizer: public C ABI.
+ *
+ * Plain pointers + sizes, no torch types. All device pointers live in HBM of
+ * the current HIP device; every call is asynchronous on `stream` (a
+ * hipStream_t passed as void*) and performs no host synchronisation and no
+ * device allocation: callers own outputs and workspace (sized with the
+ * *_workspace() queries). Returns MR_OK (0) or an error code; the message is
+ * in mr_last_error() (thread-local).
+ *
+ * Boundary being replaced (reference path: torch_renderer.py:97-159,
+ * renderer.py:87-101 -> PyTorch3D MeshRasterizer/MeshRenderer ->
+ * pybind11 module pytorch3d._C, upstream csrc/ext.cpp):
+ *   _C.rasterize_meshes           -> mr_rasterize_meshes
+ *   _C.rasterize_meshes_backward  -> mr_rasterize_meshes_backward
+ *   MeshRasterizer.transform (torch bmm) -> mr_project_faces(+_backward)
+ *   SoftPhongShader + SoftSilhouetteShader + zbuf relu over ONE raster pass
+ *     (torch_renderer.py:110-121 rasterizes twice; :155-159 once more)
+ *                                -> mr_render_forward / mr_render_backward
+ */
+#ifndef MI355R_H
+#define MI355R_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { MR_OK = 0, MR_EINVAL = 1, MR_ELAUNCH = 2, MR_EUNSUPPORTED = 3, MR_EWORKSPACE = 4 };
+
+/* Per-view camera: X_view = X_world @ R + T (PyTorch3D row-vector
+ * convention, R row-major), ndc = (ax * x/z + bx, ay * y/z + by, z).
+ * PerspectiveCameras(in_ndc=False): ax = fx/s, bx = (W/2 - px)/s, s = min(H,W)/2
+ * (torch_renderer.py:61-71); FoVPerspectiveCameras: ax = 1/(tan(fov/2)*aspect).
+ * 64 bytes. */
+typedef struct mr_view {
+  float R[9];
+  float T[3];
+  float ax, bx, ay, by;
+} mr_view_t;
+
+/* RasterizationSettings (upstream rasterizer.py) — blur/K/clip/cull as there. */
+typedef struct mr_raster_settings {
+  int32_t H, W;
+  int32_t faces_per_pixel;   /* only 1 is implemented on the GPU path */
+  float blur_radius;
+  int32_t perspective_correct;
+  int32_t clip_barycentric_coords;
+  int32_t cull_backfaces;
+  int32_t max_faces_per_bin; /* <= 0: library default; overflow is handled exactly */
+} mr_raster_settings_t;
+
+/* Shading / blending parameters (SoftPhongShader, PointLights, Materials,
+ * BlendParams, SoftSilhouetteShader). */
+typedef struct mr_shade_params {
+  int32_t light_kind;        /* 0 = PointLights, 1 = AmbientLights */
+  float light_location[3];
+  float light_ambient[3], light_diffuse[3], light_specular[3];
+  float mat_ambient[3], mat_diffuse[3], mat_specular[3];
+  float shininess;
+  float sigma_rgb, gamma, background[3], znear, zfar;
+  float sigma_sil;
+  int32_t out_flags;         /* MR_OUT_* */
+  int32_t rgb_channels;      /* 3 (rgb) or 4 (rgba, alpha = 1 - prod(1 - prob)) */
+} mr_shade_params_t;
+
+enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4 };
+
+/* One triangle mesh shared by all N views (Meshes.extend(N)). */
+typedef struct mr_mesh {
+  const float* verts;        /* (V,3) world */
+  int64_t V;
+  const int32_t* faces;      /* (F,3) */
+  int64_t F;
+  const int32_t* vadj_ptr;   /* (V+1) CSR vertex -> (face<<2 | corner), sorted by (corner, face) */
+  const int32_t* vadj;
+  const float* vnormals;     /* (V,3) from mr_vertex_normals (PointLights only) */
+  int32_t tex_kind;          /* 0 white, 1 per-vertex colours, 2 UV map */
+  const float* vcolors;      /* (V,3) */
+  const float* verts_uvs;    /* (Vt,2) */
+  const int32_t* faces_uvs;  /* (F,3) */
+  const float* tex_rgba;     /* (Ht,Wt,4) float, image row 0 first (flip done in-kernel) */
+  int32_t tex_h, tex_w;
+} mr_mesh_t;
+
+const char* mr_last_error(void);
+int32_t mr_version(void);
+
+/* ---------------- PyTorch3D _C.rasterize_meshes boundary ---------------- */
+size_t mr_rasterize_meshes_workspace(int64_t num_meshes, int64_t total_faces, int32_t H, int32_t W,
+                                     int32_t max_faces_per_bin);
+
+/* face_verts (F,3,3) NDC xy + view z; mesh_to_face_first_idx / num_faces_per_mesh (N) int64 on device.
+ * Outputs (N,H,W,K): pix_to_face int64 (packed face id or -1), zbuf, dists f32; bary (N,H,W,K,3). */
+int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* mesh_to_face_first_idx,
+                            const int64_t* num_faces_per_mesh, int64_t num_meshes, int64_t total_faces,
+                            const mr_raster_settings_t* settings, int64_t* pix_to_face, float* zbuf,
+                            float* bary, float* dists, void* workspace, size_t workspace_bytes, void* stream);
+
+/* grad_face_verts (F,3,3) is overwritten (zeroed then accumulated). */
+int32_t mr_rasterize_meshes_backward(const float* face_verts, const int64_t* pix_to_face,
+                                     const float* grad_zbuf, const float* grad_bary, const float* grad_dists,
+                                     int64_t num_meshes, int64_t total_faces, const mr_raster_settings_t* settings,
+                                     float* grad_face_verts, void* stream);
+
+/* ---------------- projection (MeshRasterizer.transform) ---------------- */
+/* face_verts[n*F + f][c] = ndc(view n, verts[faces[f][c]]) for n < N. */
+int32_t mr_project_faces(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                         const mr_view_t* views, int64_t N, float* face_verts, void* stream);
+/* grad_verts (V,3) and grad_views (N,12: dR row-major, dT) are overwritten. */
+int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                  const int32_t* vadj_ptr, const int32_t* vadj, const mr_view_t* views, int64_t N,
+                                  const float* grad_face_verts, float* grad_verts, float* grad_views, void* stream);
+
+/* ---------------- mesh helpers ---------------- */
+/* Meshes.verts_normals_packed: n_f = (v2-v1) x (v0-v1), summed in (corner, face) order, normalized (eps 1e-6).
+ * vnormals_raw (V,3) keeps the unnormalized sums for the backward. */
+int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, int64_t F, const int32_t* vadj_ptr,
+                          const int32_t* vadj, float* vnormals, float* vnormals_raw, void* stream);
+
+/* ---------------- fused render (one raster pass -> depth, silhouette, rgb) ---------------- */
+size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
+/* Outputs (each optional per out_flags): depth (N,H,W), silhouette (N,H,W), rgb (N,H,W,C);
+ * pix_to_face32 (N,H,W) int32 packed face id n*F+f or -1 (kept for the backward).
+ * cam_centers (Nc,3) world-space specular camera centres, Nc in {1, N}. */
+int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t N, const float* cam_centers,
+                          int64_t num_cam_centers, const mr_raster_settings_t* rs, const mr_shade_params_t* sp,
+                          float* depth, float* silhouette, float* rgb, int32_t* pix_to_face32, void* workspace,
+                          size_t workspace_bytes, void* stream);
+/* Backward from upstream grads (each may be NULL when not requested in out_flags).
+ * Writes grad_verts (V,3), grad_views (N,12), grad_vcolors (V,3; tex_kind 1 only, may be NULL).
+ * `workspace` must be the one passed to the matching mr_render_forward (face records reused). */
+size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W);
+int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, const mr_view_t* views, int64_t N,
+                           const float* cam_centers, int64_t num_cam_centers, const mr_raster_settings_t* rs,
+                           const mr_shade_params_t* sp, const int32_t* pix_to_face32, const float* grad_depth,
+                           const float* grad_silhouette, const float* grad_rgb, const void* fwd_workspace,
+                           void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts, float* grad_views,
+                           float* grad_vcolors, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MI355R_H */

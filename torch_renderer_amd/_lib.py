@@ -1,0 +1,129 @@
+"""ctypes binding of the C ABI in ``include/mi355r.h`` (``libmi355r.so``).
+
+The library is the product: there is no CPU or PyTorch fallback. If the shared
+object is missing or fails to load, importing a GPU entry point raises
+``RuntimeError`` (build it with ``python -m torch_renderer_amd._build`` or
+``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  -- must be imported first: the .so shares torch's HIP runtime
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmi355r.so")
+
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_i64_p = ctypes.POINTER(ctypes.c_int64)
+c_i32_p = ctypes.POINTER(ctypes.c_int32)
+
+MR_OUT_DEPTH = 1
+MR_OUT_SIL = 2
+MR_OUT_RGB = 4
+
+
+class MrView(ctypes.Structure):
+    _fields_ = [("R", ctypes.c_float * 9), ("T", ctypes.c_float * 3), ("ax", ctypes.c_float),
+                ("bx", ctypes.c_float), ("ay", ctypes.c_float), ("by", ctypes.c_float)]
+
+
+class MrRasterSettings(ctypes.Structure):
+    _fields_ = [("H", ctypes.c_int32), ("W", ctypes.c_int32), ("faces_per_pixel", ctypes.c_int32),
+                ("blur_radius", ctypes.c_float), ("perspective_correct", ctypes.c_int32),
+                ("clip_barycentric_coords", ctypes.c_int32), ("cull_backfaces", ctypes.c_int32),
+                ("max_faces_per_bin", ctypes.c_int32)]
+
+
+F3 = ctypes.c_float * 3
+
+
+class MrShadeParams(ctypes.Structure):
+    _fields_ = [("light_kind", ctypes.c_int32), ("light_location", F3), ("light_ambient", F3),
+                ("light_diffuse", F3), ("light_specular", F3), ("mat_ambient", F3), ("mat_diffuse", F3),
+                ("mat_specular", F3), ("shininess", ctypes.c_float), ("sigma_rgb", ctypes.c_float),
+                ("gamma", ctypes.c_float), ("background", F3), ("znear", ctypes.c_float),
+                ("zfar", ctypes.c_float), ("sigma_sil", ctypes.c_float), ("out_flags", ctypes.c_int32),
+                ("rgb_channels", ctypes.c_int32)]
+
+
+class MrMesh(ctypes.Structure):
+    _fields_ = [("verts", ctypes.c_void_p), ("V", ctypes.c_int64), ("faces", ctypes.c_void_p),
+                ("F", ctypes.c_int64), ("vadj_ptr", ctypes.c_void_p), ("vadj", ctypes.c_void_p),
+                ("vnormals", ctypes.c_void_p), ("tex_kind", ctypes.c_int32), ("vcolors", ctypes.c_void_p),
+                ("verts_uvs", ctypes.c_void_p), ("faces_uvs", ctypes.c_void_p), ("tex_rgba", ctypes.c_void_p),
+                ("tex_h", ctypes.c_int32), ("tex_w", ctypes.c_int32)]
+
+
+# (name, restype, argtypes) — mirrors include/mi355r.h
+_VP = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int32
+_SZ = ctypes.c_size_t
+_SIGS = [
+    ("mr_last_error", ctypes.c_char_p, []),
+    ("mr_version", _I32, []),
+    ("mr_rasterize_meshes_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
+    ("mr_rasterize_meshes", _I32, [_VP, _VP, _VP, _I64, _I64, ctypes.POINTER(MrRasterSettings), _VP, _VP, _VP,
+                                   _VP, _VP, _SZ, _VP]),
+    ("mr_rasterize_meshes_backward", _I32, [_VP, _VP, _VP, _VP, _VP, _I64, _I64, ctypes.POINTER(MrRasterSettings),
+                                            _VP, _VP]),
+    ("mr_project_faces", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
+    ("mr_project_faces_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
+    ("mr_vertex_normals", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _VP]),
+    ("mr_render_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
+    ("mr_render_forward", _I32, [ctypes.POINTER(MrMesh), _VP, _I64, _VP, _I64, ctypes.POINTER(MrRasterSettings),
+                                 ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("mr_render_backward_workspace", _SZ, [_I64, _I64, _I64, _I32, _I32]),
+    ("mr_render_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _I64, _VP, _I64,
+                                  ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP, _VP,
+                                  _VP, _VP, _VP, _SZ, _VP, _VP, _VP, _VP]),
+]
+
+EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None) -> ctypes.CDLL:
+    """Load (once) and return the library. Raises RuntimeError if it is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"mi355r: native library not found at {p}. Build it first "
+                "(python -m torch_renderer_amd._build). There is no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        for name, res, args in _SIGS:
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        msg = load().mr_last_error().decode(errors="replace")
+        if rc == 3:
+            raise NotImplementedError(f"mi355r: {msg}")
+        raise RuntimeError(f"mi355r error {rc}: {msg}")
+
+
+def ptr(t):
+    """Device (or host) pointer of a contiguous tensor, or None."""
+    if t is None:
+        return None
+    assert t.is_contiguous(), "mi355r: tensors passed across the C ABI must be contiguous"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

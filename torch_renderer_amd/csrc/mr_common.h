@@ -1,0 +1,145 @@
+// mi355r — MI355X (gfx950) differentiable mesh rasterizer: shared device math.
+//
+// Every function here restates PyTorch3D's rasterization math (the path the
+// reference reaches via torch_renderer.py:97-121 / renderer.py:87-101 ->
+// pytorch3d.renderer.mesh.rasterize_meshes -> pytorch3d._C.rasterize_meshes)
+// with the SAME operand order as the CPU implementation, so that integer
+// outputs (pix_to_face) are bit-identical to the CPU path. The library is built
+// with -ffp-contract=off (no FMA contraction) and HIP's default correctly
+// rounded f32 division; see DESIGN.md "Bit-exactness".
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MR_KEPS_D 1e-8  // geometry_utils.h: `const auto kEpsilon = 1e-8;` (a double)
+#define MR_DEV __device__ __forceinline__
+
+// std::max/std::min semantics (a < b ? b : a) — NaN handling follows the CPU code.
+MR_DEV float smax(float a, float b) { return (a < b) ? b : a; }
+MR_DEV float smin(float a, float b) { return (b < a) ? b : a; }
+
+// rasterization_utils.h PixToNonSquareNdc
+MR_DEV float pix_to_ndc(int i, int S1, int S2) {
+  float range = 2.0f;
+  if (S1 > S2) range = ((float)S1 * range) / (float)S2;
+  const float offset = range / 2.0f;
+  return -offset + (range * (float)i + offset) / (float)S1;
+}
+// NDC of output column xi / row yi (both flipped: +X left, +Y up).
+MR_DEV float col_ndc(int xi, int H, int W) { return pix_to_ndc(W - 1 - xi, W, H); }
+MR_DEV float row_ndc(int yi, int H, int W) { return pix_to_ndc(H - 1 - yi, H, W); }
+
+// geometry_utils.h EdgeFunctionForward: E(p, a, b)
+MR_DEV float edge_fn(float px, float py, float ax, float ay, float bx, float by) {
+  return (px - ax) * (by - ay) - (py - ay) * (bx - ax);
+}
+
+// Face record written by the setup kernel (one per rasterized face instance,
+// index = PyTorch3D packed face id). 64 B, 16-B aligned -> 4 x dwordx4 loads.
+struct __attribute__((aligned(16))) FaceRec {
+  float x0, y0, z0, x1, y1, z1, x2, y2, z2;  // NDC xy, view z
+  float area;                                // float(double(E(v2,v0,v1)) + 1e-8)
+  float xmin, xmax, ymin, ymax;              // NDC bbox (not padded)
+  uint32_t flags;                            // FR_VALID | FR_FAST
+  uint32_t face;                             // mesh face index (into faces array)
+};
+enum : uint32_t { FR_VALID = 1u, FR_FAST = 2u };
+
+// BarycentricPerspectiveCorrectionForward
+MR_DEV void persp_fwd(float w0, float w1, float w2, float z0, float z1, float z2, float& o0, float& o1,
+                      float& o2) {
+  const float t0 = w0 * z1 * z2;
+  const float t1 = w1 * z0 * z2;
+  const float t2 = w2 * z0 * z1;
+  const float d = smax(t0 + t1 + t2, (float)MR_KEPS_D);
+  o0 = t0 / d;
+  o1 = t1 / d;
+  o2 = t2 / d;
+}
+
+// BarycentricClipForward (lower clamp + renormalise)
+MR_DEV void clip_fwd(float b0, float b1, float b2, float& o0, float& o1, float& o2) {
+  const float w0 = smax(b0, 0.0f), w1 = smax(b1, 0.0f), w2 = smax(b2, 0.0f);
+  const float s = smax(w0 + w1 + w2, 1e-5f);
+  o0 = w0 / s;
+  o1 = w1 / s;
+  o2 = w2 / s;
+}
+
+// PointLineDistanceForward (squared)
+MR_DEV float pt_line_dist(float px, float py, float ax, float ay, float bx, float by) {
+  const float dx = bx - ax, dy = by - ay;
+  const float l2 = dx * dx + dy * dy;
+  if ((double)l2 <= MR_KEPS_D) {
+    const float ex = px - bx, ey = py - by;
+    return ex * ex + ey * ey;
+  }
+  const float t = (dx * (px - ax) + dy * (py - ay)) / l2;
+  const float tt = smin(smax(t, 0.0f), 1.0f);
+  const float qx = ax + tt * dx, qy = ay + tt * dy;
+  const float ex = px - qx, ey = py - qy;
+  return ex * ex + ey * ey;
+}
+
+MR_DEV float pt_tri_dist(float px, float py, const FaceRec& r) {
+  const float e01 = pt_line_dist(px, py, r.x0, r.y0, r.x1, r.y1);
+  const float e02 = pt_line_dist(px, py, r.x0, r.y0, r.x2, r.y2);
+  const float e12 = pt_line_dist(px, py, r.x1, r.y1, r.x2, r.y2);
+  return smin(smin(e01, e02), e12);
+}
+
+// Full per-(pixel, face) evaluation, exactly the CPU naive loop body after the
+// face-level skips. Returns true if the face is kept for this pixel.
+struct FragEval {
+  float pz, sdist, b0, b1, b2;  // bary after perspective correction + clip
+  float w0, w1, w2;             // uncorrected barycentrics
+  float c0, c1, c2;             // perspective corrected (pre-clip)
+  bool inside;
+};
+
+MR_DEV bool eval_face(const FaceRec& r, float px, float py, float bbox_pad, float blur, bool persp,
+                      bool clipb, FragEval& o) {
+  if (px > r.xmax + bbox_pad || px < r.xmin - bbox_pad || py > r.ymax + bbox_pad || py < r.ymin - bbox_pad)
+    return false;
+  const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
+  o.w0 = e0 / r.area;
+  o.w1 = e1 / r.area;
+  o.w2 = e2 / r.area;
+  if (persp) persp_fwd(o.w0, o.w1, o.w2, r.z0, r.z1, r.z2, o.c0, o.c1, o.c2);
+  else { o.c0 = o.w0; o.c1 = o.w1; o.c2 = o.w2; }
+  if (clipb) clip_fwd(o.c0, o.c1, o.c2, o.b0, o.b1, o.b2);
+  else { o.b0 = o.c0; o.b1 = o.c1; o.b2 = o.c2; }
+  o.pz = o.b0 * r.z0 + o.b1 * r.z1 + o.b2 * r.z2;
+  if (o.pz < 0.0f) return false;
+  o.inside = o.c0 > 0.0f && o.c1 > 0.0f && o.c2 > 0.0f;
+  if (!o.inside && !(blur > 0.0f)) return false;  // dist >= 0 == blur (finite faces only)
+  const float dist = pt_tri_dist(px, py, r);
+  o.sdist = o.inside ? -dist : dist;
+  if (!o.inside && dist >= blur) return false;
+  return true;
+}
+
+// Cheap exact pre-test (blur == 0): the face can only be kept if the pixel is
+// strictly inside in edge-function sign. Valid when FR_FAST is set (finite,
+// non-zero area; for perspective correction additionally all z > 0).
+MR_DEV bool fast_reject(const FaceRec& r, float px, float py) {
+  const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
+  const bool pos = r.area > 0.0f;
+  const bool in = pos ? (e0 > 0.0f && e1 > 0.0f && e2 > 0.0f) : (e0 < 0.0f && e1 < 0.0f && e2 < 0.0f);
+  return !in;
+}
+
+MR_DEV bool rec_finite(const FaceRec& r) {
+  return __builtin_isfinite(r.x0) && __builtin_isfinite(r.y0) && __builtin_isfinite(r.z0) &&
+         __builtin_isfinite(r.x1) && __builtin_isfinite(r.y1) && __builtin_isfinite(r.z1) &&
+         __builtin_isfinite(r.x2) && __builtin_isfinite(r.y2) && __builtin_isfinite(r.z2);
+}
+
+// Lexicographic (z, face) order == std::sort over (pz, f, ...) tuples.
+MR_DEV bool frag_less(float za, int64_t fa, float zb, int64_t fb) {
+  return za < zb || (!(zb < za) && fa < fb);
+}

@@ -1,0 +1,494 @@
+// mi355r — per-pixel shading (forward + analytic backward) and the rasterizer's
+// per-pixel backward, as device functions fused into the render kernels.
+//
+// Restates (K = faces_per_pixel = 1):
+//  * SoftPhongShader -> phong_shading / _apply_lighting / PointLights.diffuse,
+//    .specular / Materials (upstream pytorch3d/renderer/mesh/shading.py,
+//    lighting.py), used at torch_renderer.py:141-153 and renderer.py:88-98;
+//  * TexturesUV.sample_textures (grid_sample bilinear, align_corners=True,
+//    padding 'border', map flipped vertically) / TexturesVertex;
+//  * softmax_rgb_blend (ColorRender, torch_renderer.py:155-159) and
+//    sigmoid_alpha_blend (DepthRender silhouette, torch_renderer.py:102-121);
+//  * RasterizeMeshesBackwardCpu per (pixel, k) (geometry_utils.h backward fns);
+//  * the projection X_view = X @ R + T, ndc = (ax*x/z+bx, ay*y/z+by, z) and its
+//    derivative w.r.t. X, R and T (MeshRasterizer.transform).
+#pragma once
+#include "mr_common.h"
+
+struct ShadeParams {
+  // geometry
+  const float* verts;     // (V,3) world
+  const int32_t* faces;   // (F,3)
+  const float* vnormals;  // (V,3) normalized vertex normals
+  // texture
+  int tex_kind;             // 0 = white, 1 = per-vertex colours, 2 = UV map
+  const float* vcolors;     // (V,3)
+  const float* verts_uvs;   // (Vt,2)
+  const int32_t* faces_uvs; // (F,3)
+  const float4* tex;        // (Ht,Wt) RGBA-padded, row 0 = first image row (unflipped)
+  int tex_h, tex_w;
+  // lighting / materials
+  int light_kind;  // 0 = point light, 1 = ambient only
+  float light_loc[3], light_amb[3], light_diff[3], light_spec[3];
+  float mat_amb[3], mat_diff[3], mat_spec[3], shininess;
+  const float* cam_centers;  // (Nc,3) world-space camera centre used for specular
+  int cam_center_stride;     // 0 (single camera) or 3
+  // blending
+  float sigma_rgb, gamma, bg[3], znear, zfar;
+  float sigma_sil;
+};
+
+struct ViewRec {  // 16 floats, matches mr_view_t
+  float R[9], T[3], ax, bx, ay, by;
+};
+
+struct ShadeOut {
+  float depth, sil, rgb[3], alpha;
+};
+
+// ---- F.normalize(x, eps=1e-6) forward/backward ----
+MR_DEV void normalize3(const float x[3], float y[3], float& nrm, float& den) {
+  nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  den = smax(nrm, 1e-6f);
+  y[0] = x[0] / den;
+  y[1] = x[1] / den;
+  y[2] = x[2] / den;
+}
+MR_DEV void normalize3_bwd(const float x[3], float nrm, float den, const float g[3], float gx[3]) {
+  const float gd = -((g[0] * x[0] + g[1] * x[1]) + g[2] * x[2]) / (den * den);
+  const float gn = (nrm >= 1e-6f && nrm > 0.0f) ? gd / nrm : 0.0f;
+  gx[0] = g[0] / den + gn * x[0];
+  gx[1] = g[1] / den + gn * x[1];
+  gx[2] = g[2] / den + gn * x[2];
+}
+MR_DEV float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+MR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---- texture: grid_sample(bilinear, align_corners=True, border) on flipped map ----
+struct TexTap {
+  float ix, iy;     // clipped pixel coords in the flipped map
+  bool gx_ok, gy_ok;  // border-clip gradient pass-through
+  int x0, y0;
+};
+MR_DEV float4 tex_fetch(const ShadeParams& S, int xc, int yc) {
+  if (xc < 0 || yc < 0 || xc >= S.tex_w || yc >= S.tex_h) return make_float4(0.f, 0.f, 0.f, 0.f);
+  return S.tex[(int64_t)(S.tex_h - 1 - yc) * S.tex_w + xc];  // torch.flip(maps, [H])
+}
+MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t) {
+  const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
+  float ix = ((gx + 1.0f) / 2.0f) * (float)(S.tex_w - 1);
+  float iy = ((gy + 1.0f) / 2.0f) * (float)(S.tex_h - 1);
+  t.gx_ok = !(ix < 0.0f) && !(ix > (float)(S.tex_w - 1));
+  t.gy_ok = !(iy < 0.0f) && !(iy > (float)(S.tex_h - 1));
+  ix = smin((float)(S.tex_w - 1), smax(ix, 0.0f));
+  iy = smin((float)(S.tex_h - 1), smax(iy, 0.0f));
+  t.ix = ix;
+  t.iy = iy;
+  t.x0 = (int)floorf(ix);
+  t.y0 = (int)floorf(iy);
+  const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
+  const float nw = (x1 - ix) * (y1 - iy), ne = (ix - x0) * (y1 - iy);
+  const float sw = (x1 - ix) * (iy - y0), se = (ix - x0) * (iy - y0);
+  const float4 a = tex_fetch(S, t.x0, t.y0), b = tex_fetch(S, t.x0 + 1, t.y0);
+  const float4 c = tex_fetch(S, t.x0, t.y0 + 1), d = tex_fetch(S, t.x0 + 1, t.y0 + 1);
+  out[0] = ((a.x * nw + b.x * ne) + c.x * sw) + d.x * se;
+  out[1] = ((a.y * nw + b.y * ne) + c.y * sw) + d.y * se;
+  out[2] = ((a.z * nw + b.z * ne) + c.z * sw) + d.z * se;
+}
+// d(texel)/d(u,v) contracted with g (3 channels) -> (gu, gv)
+MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[3], float& gu, float& gv) {
+  const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
+  const float4 a = tex_fetch(S, t.x0, t.y0), b = tex_fetch(S, t.x0 + 1, t.y0);
+  const float4 c = tex_fetch(S, t.x0, t.y0 + 1), d = tex_fetch(S, t.x0 + 1, t.y0 + 1);
+  const float ga = (g[0] * a.x + g[1] * a.y) + g[2] * a.z;
+  const float gb = (g[0] * b.x + g[1] * b.y) + g[2] * b.z;
+  const float gc = (g[0] * c.x + g[1] * c.y) + g[2] * c.z;
+  const float gd = (g[0] * d.x + g[1] * d.y) + g[2] * d.z;
+  float gix = -ga * (y1 - t.iy) + gb * (y1 - t.iy) - gc * (t.iy - y0) + gd * (t.iy - y0);
+  float giy = -ga * (x1 - t.ix) - gb * (t.ix - x0) + gc * (x1 - t.ix) + gd * (t.ix - x0);
+  gix = t.gx_ok ? gix : 0.0f;
+  giy = t.gy_ok ? giy : 0.0f;
+  // ix = ((2u-1+1)/2)*(W-1)  ->  d ix / d u = W-1
+  gu = gix * (float)(S.tex_w - 1);
+  gv = giy * (float)(S.tex_h - 1);
+}
+
+// Per-pixel inputs gathered once for shading
+struct PixGeom {
+  float X[3][3];   // world positions of the 3 corners
+  float Nv[3][3];  // vertex normals
+  float uv[3][2];
+  float col[3][3];
+  int32_t vi[3];
+};
+
+MR_DEV void gather_geom(const ShadeParams& S, uint32_t face, PixGeom& G) {
+  const int32_t* fv = S.faces + 3 * (int64_t)face;
+  for (int c = 0; c < 3; ++c) {
+    const int32_t v = fv[c];
+    G.vi[c] = v;
+    for (int k = 0; k < 3; ++k) {
+      G.X[c][k] = S.verts[3 * (int64_t)v + k];
+      G.Nv[c][k] = S.light_kind == 0 ? S.vnormals[3 * (int64_t)v + k] : 0.0f;
+    }
+  }
+  if (S.tex_kind == 2) {
+    const int32_t* fu = S.faces_uvs + 3 * (int64_t)face;
+    for (int c = 0; c < 3; ++c) {
+      G.uv[c][0] = S.verts_uvs[2 * (int64_t)fu[c]];
+      G.uv[c][1] = S.verts_uvs[2 * (int64_t)fu[c] + 1];
+    }
+  } else if (S.tex_kind == 1) {
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 3; ++k) G.col[c][k] = S.vcolors[3 * (int64_t)G.vi[c] + k];
+  }
+}
+
+// interpolate_face_attributes: sum_i b_i * attr_i
+MR_DEV float interp3(float b0, float b1, float b2, float a0, float a1, float a2) {
+  return (b0 * a0 + b1 * a1) + b2 * a2;
+}
+
+// Intermediate values kept for the backward pass.
+struct ShadeCache {
+  float P[3], Nn[3], nh[3], nlen, nden, l[3], lh[3], llen, lden, v[3], vh[3], vlen, vden;
+  float cosd, r[3], vr, as, spow, texel[3], amb[3], diff[3], spec[3], col[3];
+  float ps, pc, zi, zimax, E, w, ex, delta, den;
+  TexTap tap;
+};
+
+// Forward shading of one pixel (hit = face found). b = bary (after clip), z, sd = signed dist.
+MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, float b0, float b1, float b2,
+                      float z, float sd, ShadeOut& o, ShadeCache& C) {
+  const float m = hit ? 1.0f : 0.0f;
+  const float zb = hit ? z : -1.0f;    // zbuf background = -1
+  const float dd = hit ? sd : -1.0f;   // dists background = -1
+  // DepthRender: relu(zbuf[..., 0])
+  o.depth = zb > 0.0f ? zb : 0.0f;
+  // SoftSilhouetteShader / sigmoid_alpha_blend
+  C.ps = sigmoidf_((-dd) / S.sigma_sil) * m;
+  o.sil = 1.0f - (1.0f - C.ps);
+  // Phong colours (only meaningful for hit pixels; background weight is 0)
+  for (int k = 0; k < 3; ++k) C.col[k] = 0.0f;
+  if (hit) {
+    for (int k = 0; k < 3; ++k) {
+      C.P[k] = interp3(b0, b1, b2, G.X[0][k], G.X[1][k], G.X[2][k]);
+      C.amb[k] = S.mat_amb[k] * S.light_amb[k];
+    }
+    if (S.tex_kind == 2) {
+      const float u = interp3(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
+      const float v = interp3(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
+      tex_sample(S, u, v, C.texel, C.tap);
+    } else if (S.tex_kind == 1) {
+      for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);
+    } else {
+      C.texel[0] = C.texel[1] = C.texel[2] = 1.0f;
+    }
+    if (S.light_kind == 0) {
+      for (int k = 0; k < 3; ++k) C.Nn[k] = interp3(b0, b1, b2, G.Nv[0][k], G.Nv[1][k], G.Nv[2][k]);
+      normalize3(C.Nn, C.nh, C.nlen, C.nden);
+      for (int k = 0; k < 3; ++k) C.l[k] = S.light_loc[k] - C.P[k];
+      normalize3(C.l, C.lh, C.llen, C.lden);
+      C.cosd = dot3(C.nh, C.lh);
+      const float angle = C.cosd > 0.0f ? C.cosd : 0.0f;
+      const float* cc = S.cam_centers + (int64_t)n * S.cam_center_stride;
+      for (int k = 0; k < 3; ++k) C.v[k] = cc[k] - C.P[k];
+      normalize3(C.v, C.vh, C.vlen, C.vden);
+      for (int k = 0; k < 3; ++k) C.r[k] = -C.lh[k] + 2.0f * (C.cosd * C.nh[k]);
+      C.vr = dot3(C.vh, C.r);
+      const float ms = C.cosd > 0.0f ? 1.0f : 0.0f;
+      C.as = (C.vr > 0.0f ? C.vr : 0.0f) * ms;
+      C.spow = powf(C.as, S.shininess);
+      for (int k = 0; k < 3; ++k) {
+        C.diff[k] = S.mat_diff[k] * (S.light_diff[k] * angle);
+        C.spec[k] = S.mat_spec[k] * (S.light_spec[k] * C.spow);
+      }
+    } else {
+      for (int k = 0; k < 3; ++k) C.diff[k] = C.spec[k] = 0.0f;
+    }
+    for (int k = 0; k < 3; ++k) C.col[k] = (C.amb[k] + C.diff[k]) * C.texel[k] + C.spec[k];
+  }
+  // softmax_rgb_blend (K = 1)
+  const float eps = 1e-10f;
+  C.pc = sigmoidf_((-dd) / S.sigma_rgb) * m;
+  const float alpha = 1.0f - C.pc;
+  C.zi = (S.zfar - zb) / (S.zfar - S.znear) * m;
+  C.zimax = smax(C.zi, eps);
+  C.E = expf((C.zi - C.zimax) / S.gamma);
+  C.w = C.pc * C.E;
+  C.ex = expf((eps - C.zimax) / S.gamma);
+  C.delta = smax(C.ex, eps);
+  C.den = C.w + C.delta;
+  for (int k = 0; k < 3; ++k) o.rgb[k] = (C.w * C.col[k] + C.delta * S.bg[k]) / C.den;
+  o.alpha = 1.0f - alpha;
+}
+
+// Backward of shade_fwd for a hit pixel. Produces grads wrt z (zbuf), signed
+// dist, bary (b0..b2), per-corner world positions / normals / vertex colours.
+struct ShadeGrad {
+  float gz, gsd, gb[3];
+  float gX[3][3], gN[3][3], gC[3][3];
+};
+
+MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1, float b2, float z,
+                      const ShadeCache& C, float gD, float gS, const float gRGB[3], float gA, ShadeGrad& R) {
+  const float b[3] = {b0, b1, b2};
+  R.gz = 0.0f;
+  R.gsd = 0.0f;
+  for (int c = 0; c < 3; ++c) {
+    R.gb[c] = 0.0f;
+    for (int k = 0; k < 3; ++k) R.gX[c][k] = R.gN[c][k] = R.gC[c][k] = 0.0f;
+  }
+  // depth = relu(z)
+  if (z > 0.0f) R.gz += gD;
+  // silhouette: sil = 1 - (1 - ps), ps = sigmoid(-sd / sigma_sil)
+  {
+    const float gx = gS * (C.ps * (1.0f - C.ps));
+    R.gsd += -(gx / S.sigma_sil);
+  }
+  // rgb = (w*col + delta*bg) / den
+  float gw = 0.0f, gdelta = 0.0f, gcol[3];
+  {
+    float gden = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      const float num = C.w * C.col[k] + C.delta * S.bg[k];
+      const float gnum = gRGB[k] / C.den;
+      gden += -gRGB[k] * num / (C.den * C.den);
+      gw += gnum * C.col[k];
+      gcol[k] = gnum * C.w;
+      gdelta += gnum * S.bg[k];
+    }
+    gw += gden;
+    gdelta += gden;
+  }
+  float gp = gA;  // A = 1 - (1 - p)
+  float gzimax = 0.0f, gzi = 0.0f;
+  {
+    const float gu = (C.ex >= 1e-10f) ? gdelta * C.ex : 0.0f;  // clamp(min) backward
+    gzimax += -(gu / S.gamma);
+    gp += gw * C.E;
+    const float gE = gw * C.pc;
+    const float gv = gE * C.E;
+    gzi += gv / S.gamma;
+    gzimax += -(gv / S.gamma);
+    gzi += (C.zi >= 1e-10f) ? gzimax : 0.0f;  // max over K=1, then clamp(min=eps)
+    R.gz += -(gzi / (S.zfar - S.znear));
+    const float gx = gp * (C.pc * (1.0f - C.pc));
+    R.gsd += -(gx / S.sigma_rgb);
+  }
+  // colours = (amb + diff) * texel + spec
+  float gtex[3], gP[3] = {0.f, 0.f, 0.f}, gNn[3] = {0.f, 0.f, 0.f};
+  for (int k = 0; k < 3; ++k) gtex[k] = gcol[k] * (C.amb[k] + C.diff[k]);
+  if (S.light_kind == 0) {
+    float gangle = 0.0f, gspow = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      gangle += gcol[k] * C.texel[k] * S.mat_diff[k] * S.light_diff[k];
+      gspow += gcol[k] * S.mat_spec[k] * S.light_spec[k];
+    }
+    const float gas = (C.as > 0.0f) ? gspow * S.shininess * powf(C.as, S.shininess - 1.0f) : 0.0f;
+    const float ms = C.cosd > 0.0f ? 1.0f : 0.0f;
+    const float gvr = (C.vr > 0.0f) ? gas * ms : 0.0f;
+    float gvh[3], gr[3], glh[3], gnh[3];
+    for (int k = 0; k < 3; ++k) {
+      gvh[k] = gvr * C.r[k];
+      gr[k] = gvr * C.vh[k];
+    }
+    // r = -lh + 2 * (cos * nh)
+    float gcos = 2.0f * dot3(gr, C.nh);
+    for (int k = 0; k < 3; ++k) {
+      glh[k] = -gr[k];
+      gnh[k] = 2.0f * C.cosd * gr[k];
+    }
+    gcos += (C.cosd > 0.0f) ? gangle : 0.0f;  // relu(cos) for diffuse
+    for (int k = 0; k < 3; ++k) {
+      gnh[k] += gcos * C.lh[k];
+      glh[k] += gcos * C.nh[k];
+    }
+    float gl[3], gvv[3];
+    normalize3_bwd(C.Nn, C.nlen, C.nden, gnh, gNn);
+    normalize3_bwd(C.l, C.llen, C.lden, glh, gl);
+    normalize3_bwd(C.v, C.vlen, C.vden, gvh, gvv);
+    for (int k = 0; k < 3; ++k) gP[k] = -gl[k] - gvv[k];
+  }
+  for (int c = 0; c < 3; ++c) {
+    R.gb[c] += dot3(G.X[c], gP);
+    if (S.light_kind == 0) R.gb[c] += dot3(G.Nv[c], gNn);
+    for (int k = 0; k < 3; ++k) {
+      R.gX[c][k] = b[c] * gP[k];
+      R.gN[c][k] = b[c] * gNn[k];
+    }
+  }
+  if (S.tex_kind == 2) {
+    float gu, gv;
+    tex_sample_bwd(S, C.tap, gtex, gu, gv);
+    for (int c = 0; c < 3; ++c) R.gb[c] += G.uv[c][0] * gu + G.uv[c][1] * gv;
+  } else if (S.tex_kind == 1) {
+    for (int c = 0; c < 3; ++c) {
+      R.gb[c] += dot3(G.col[c], gtex);
+      for (int k = 0; k < 3; ++k) R.gC[c][k] = b[c] * gtex[k];
+    }
+  }
+}
+
+// ---------------- rasterizer backward (geometry_utils.h) ----------------
+MR_DEV void edge_bwd(float px, float py, float ax, float ay, float bx, float by, float g, float d[6]) {
+  // returns (dp.x, dp.y, da.x, da.y, db.x, db.y)
+  d[0] = (by - ay) * g;
+  d[1] = (ax - bx) * g;
+  d[2] = (py - by) * g;
+  d[3] = (bx - px) * g;
+  d[4] = (ay - py) * g;
+  d[5] = (px - ax) * g;
+}
+
+// BarycentricCoordsBackward -> dv[0..2] (x,y)
+MR_DEV void bary_bwd(float px, float py, const FaceRec& r, const float g[3], float dv[3][2]) {
+  const float area = r.area;
+  const float area2 = area * area;
+  const float area_inv = 1.0f / area;
+  const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
+  float de[6], da[6];
+  // w0: e0 over (p, v1, v2); area over (v2, v0, v1)
+  edge_bwd(px, py, r.x1, r.y1, r.x2, r.y2, g[0] * area_inv, de);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[0] * (-e0 / area2), da);
+  float v0x = da[2], v0y = da[3];
+  float v1x = de[2] + da[4], v1y = de[3] + da[5];
+  float v2x = de[4] + da[0], v2y = de[5] + da[1];
+  // w1: e1 over (p, v2, v0)
+  edge_bwd(px, py, r.x2, r.y2, r.x0, r.y0, g[1] * area_inv, de);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[1] * (-e1 / area2), da);
+  const float w1v0x = de[4] + da[2], w1v0y = de[5] + da[3];
+  const float w1v1x = da[4], w1v1y = da[5];
+  const float w1v2x = de[2] + da[0], w1v2y = de[3] + da[1];
+  // w2: e2 over (p, v0, v1)
+  edge_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g[2] * area_inv, de);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[2] * (-e2 / area2), da);
+  const float w2v0x = de[2] + da[2], w2v0y = de[3] + da[3];
+  const float w2v1x = de[4] + da[4], w2v1y = de[5] + da[5];
+  const float w2v2x = da[0], w2v2y = da[1];
+  dv[0][0] = (v0x + w1v0x) + w2v0x;
+  dv[0][1] = (v0y + w1v0y) + w2v0y;
+  dv[1][0] = (v1x + w1v1x) + w2v1x;
+  dv[1][1] = (v1y + w1v1y) + w2v1y;
+  dv[2][0] = (v2x + w1v2x) + w2v2x;
+  dv[2][1] = (v2y + w1v2y) + w2v2y;
+}
+
+MR_DEV void persp_bwd(float w0, float w1, float w2, float z0, float z1, float z2, const float go[3], float gb[3],
+                      float gzv[3]) {
+  const float t0 = w0 * z1 * z2, t1 = w1 * z0 * z2, t2 = w2 * z0 * z1;
+  const float d = smax(t0 + t1 + t2, (float)MR_KEPS_D);
+  const float gdt = -t0 * go[0] - t1 * go[1] - t2 * go[2];
+  const float gd = gdt / (d * d);
+  const float g0 = gd + go[0] / d, g1 = gd + go[1] / d, g2 = gd + go[2] / d;
+  gb[0] = g0 * z1 * z2;
+  gb[1] = g1 * z0 * z2;
+  gb[2] = g2 * z0 * z1;
+  gzv[0] = g1 * w1 * z2 + g2 * w2 * z1;
+  gzv[1] = g0 * w0 * z2 + g2 * w2 * z0;
+  gzv[2] = g0 * w0 * z1 + g1 * w1 * z0;
+}
+
+MR_DEV void clip_bwd(float c0, float c1, float c2, const float go[3], float gb[3]) {
+  const float w0 = smax(c0, 0.0f), w1 = smax(c1, 0.0f), w2 = smax(c2, 0.0f);
+  const float s = smax(w0 + w1 + w2, 1e-5f);
+  const float num = w0 * go[0] + w1 * go[1] + w2 * go[2];
+  const float gs = -num / (s * s);
+  gb[0] = c0 > 0.0f ? go[0] / s + gs : 0.0f;
+  gb[1] = c1 > 0.0f ? go[1] / s + gs : 0.0f;
+  gb[2] = c2 > 0.0f ? go[2] / s + gs : 0.0f;
+}
+
+MR_DEV void pt_line_bwd(float px, float py, float ax, float ay, float bx, float by, float g, float& gax,
+                        float& gay, float& gbx, float& gby) {
+  const float dx = bx - ax, dy = by - ay;
+  const float t_bot = dx * dx + dy * dy;
+  const float t_top = dx * (px - ax) + dy * (py - ay);
+  const float t = t_top / t_bot;
+  const float tt = smin(smax(t, 0.0f), 1.0f);
+  const float qx = (1.0f - tt) * ax + tt * bx, qy = (1.0f - tt) * ay + tt * by;
+  const float ex = qx - px, ey = qy - py;
+  const float s0 = g * (1.0f - tt) * 2.0f, s1 = g * tt * 2.0f;
+  gax = s0 * ex;
+  gay = s0 * ey;
+  gbx = s1 * ex;
+  gby = s1 * ey;
+}
+
+MR_DEV void pt_tri_bwd(float px, float py, const FaceRec& r, float g, float gv[3][2]) {
+  const float e01 = pt_line_dist(px, py, r.x0, r.y0, r.x1, r.y1);
+  const float e02 = pt_line_dist(px, py, r.x0, r.y0, r.x2, r.y2);
+  const float e12 = pt_line_dist(px, py, r.x1, r.y1, r.x2, r.y2);
+  for (int c = 0; c < 3; ++c) gv[c][0] = gv[c][1] = 0.0f;
+  if (e01 <= e02 && e01 <= e12)
+    pt_line_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g, gv[0][0], gv[0][1], gv[1][0], gv[1][1]);
+  else if (e02 <= e01 && e02 <= e12)
+    pt_line_bwd(px, py, r.x0, r.y0, r.x2, r.y2, g, gv[0][0], gv[0][1], gv[2][0], gv[2][1]);
+  else if (e12 <= e01 && e12 <= e02)
+    pt_line_bwd(px, py, r.x1, r.y1, r.x2, r.y2, g, gv[1][0], gv[1][1], gv[2][0], gv[2][1]);
+}
+
+// RasterizeMeshesBackward for one (pixel, face): grads of (zbuf, bary, dists)
+// -> grad of the face's NDC vertices gfv[corner][x,y,z].
+MR_DEV void raster_bwd_pixel(const FaceRec& r, float px, float py, bool persp, bool clipb, float gz, const float gb_up[3],
+                             float gd, float gfv[3][3]) {
+  const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
+  const float w0 = e0 / r.area, w1 = e1 / r.area, w2 = e2 / r.area;
+  float c0, c1, c2, b0, b1, b2;
+  if (persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
+  else { c0 = w0; c1 = w1; c2 = w2; }
+  if (clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
+  else { b0 = c0; b1 = c1; b2 = c2; }
+  const bool inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
+  const float sign = inside ? -1.0f : 1.0f;
+  float dd[3][2];
+  pt_tri_bwd(px, py, r, sign * gd, dd);
+  float g0[3] = {gb_up[0] + gz * r.z0, gb_up[1] + gz * r.z1, gb_up[2] + gz * r.z2};
+  float dz[3] = {0.0f, 0.0f, 0.0f};
+  if (clipb) {
+    float t[3];
+    clip_bwd(c0, c1, c2, g0, t);
+    g0[0] = t[0]; g0[1] = t[1]; g0[2] = t[2];
+  }
+  if (persp) {
+    float t[3];
+    persp_bwd(w0, w1, w2, r.z0, r.z1, r.z2, g0, t, dz);
+    g0[0] = t[0]; g0[1] = t[1]; g0[2] = t[2];
+  }
+  float db[3][2];
+  bary_bwd(px, py, r, g0, db);
+  const float bc[3] = {b0, b1, b2};
+  for (int c = 0; c < 3; ++c) {
+    gfv[c][0] = db[c][0] + dd[c][0];
+    gfv[c][1] = db[c][1] + dd[c][1];
+    gfv[c][2] = gz * bc[c] + dz[c];
+  }
+}
+
+// ---------------- projection ----------------
+MR_DEV void project_point(const ViewRec& V, const float X[3], float& vx, float& vy, float& vz, float& nx, float& ny) {
+  vx = ((X[0] * V.R[0] + X[1] * V.R[3]) + X[2] * V.R[6]) + V.T[0];
+  vy = ((X[0] * V.R[1] + X[1] * V.R[4]) + X[2] * V.R[7]) + V.T[1];
+  vz = ((X[0] * V.R[2] + X[1] * V.R[5]) + X[2] * V.R[8]) + V.T[2];
+  nx = V.ax * (vx / vz) + V.bx;
+  ny = V.ay * (vy / vz) + V.by;
+}
+
+// g_ndc (x, y, z=view z) at world point X -> g_view; then g_X = R g_view,
+// g_R += X (x) g_view, g_T += g_view.
+MR_DEV void project_bwd(const ViewRec& V, const float X[3], const float gn[3], float gX[3], float gR[9], float gT[3]) {
+  float vx, vy, vz, nx, ny;
+  project_point(V, X, vx, vy, vz, nx, ny);
+  const float qx = vx / vz, qy = vy / vz;
+  const float gqx = gn[0] * V.ax, gqy = gn[1] * V.ay;
+  const float gv[3] = {gqx / vz, gqy / vz, gn[2] - gqx * qx / vz - gqy * qy / vz};
+  for (int a = 0; a < 3; ++a) {
+    gX[a] = (V.R[3 * a] * gv[0] + V.R[3 * a + 1] * gv[1]) + V.R[3 * a + 2] * gv[2];
+    for (int bb = 0; bb < 3; ++bb) gR[3 * a + bb] += X[a] * gv[bb];
+  }
+  for (int bb = 0; bb < 3; ++bb) gT[bb] += gv[bb];
+}

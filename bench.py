@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Headline benchmark: frames/s of fwd+bwd at 512x512, cow mesh (F=5856), 64 views per GPU.
+
+One step = DepthColorRender.render over the rank's 64 views (depth + silhouette +
+Phong RGB from one raster pass, TexturesUV cow texture, PointLights (0,0,-3))
+followed by the backward of sum(gD*depth + gS*sil + gC*rgb) (fixed U(-1,1)
+upstream grads) to the shared vertex positions and every view's OpenCV R, t.
+With N > 1 ranks (one process per GPU, torch.distributed over RCCL) each rank
+renders its own 64 views (weak scaling) and the shared vertex gradient (V x 3
+f32) is all-reduced every step — the only data exchange the path has.
+
+    python bench.py [--gpus N --steps K --warmup W]
+Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md §Measurement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "frames/sec fwd+bwd, 512×512, ~6k-face mesh, batch=64; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+
+
+def canonical_views(verts, n_total, H, W, dist_m=0.5, fov_deg=60.0, seed=0):
+    """OpenCV look-at from 0.5 m to the centroid, azimuth 360*i/n,
+    elevation ~U[-20, 60] deg (seeded), fx = fy for a 60 deg FoV, centred principal point."""
+    from torch_renderer_amd.transforms import opencv_look_at
+
+    g = torch.Generator().manual_seed(seed)
+    c = verts.mean(0).double()
+    az = torch.arange(n_total, dtype=torch.float64) * (2 * math.pi / n_total)
+    el = torch.empty(n_total, dtype=torch.float64).uniform_(math.radians(-20.0), math.radians(60.0), generator=g)
+    C = torch.stack([dist_m * torch.cos(el) * torch.sin(az), dist_m * torch.sin(el),
+                     dist_m * torch.cos(el) * torch.cos(az)], dim=1) + c
+    R_cv, t_cv = opencv_look_at(C, c)
+    f = (W / 2.0) / math.tan(math.radians(fov_deg) / 2.0)
+    K = torch.tensor([[f, 0.0, W / 2.0], [0.0, f, H / 2.0], [0.0, 0.0, 1.0]])
+    return R_cv, t_cv, K
+
+
+def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
+    """Reference CPU path restated (oracle: C naive rasterizer + torch-CPU shading/autograd)
+    on a bounded sample: n_views frames, 1 warm-up + `reps` timed fwd+bwd passes."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from torch_renderer_amd.transforms import opencv_to_pytorch3d
+
+    img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
+    tex = ("uv", torch.from_numpy(d["verts_uvs"]).float(), torch.from_numpy(d["faces_uvs"]).long(), img)
+    s = min(H, W) / 2.0
+    intr = torch.tensor([[K[0, 0] / s, (W / 2.0 - K[0, 2]) / s, K[1, 1] / s, (H / 2.0 - K[1, 2]) / s]]).float()
+    intr = intr.expand(n_views, 4).contiguous()
+    gen = torch.Generator().manual_seed(1)
+    gD = torch.rand(n_views, H, W, generator=gen) * 2 - 1
+    gS = torch.rand(n_views, H, W, generator=gen) * 2 - 1
+    gC = torch.rand(n_views, H, W, 3, generator=gen) * 2 - 1
+    times = []
+    for it in range(reps + 1):
+        t0 = time.perf_counter()
+        v = verts.clone().requires_grad_(True)
+        Rc = R_cv[:n_views].clone().requires_grad_(True)
+        tc = t_cv[:n_views].clone().requires_grad_(True)
+        Rp, Tp = opencv_to_pytorch3d(Rc, tc)
+        out = O.render_ref(v, faces, Rp, Tp, intr, H, W, texture=tex)
+        torch.autograd.backward([out["depth"], out["sil"], out["rgba"][..., :3]], [gD, gS, gC])
+        if it > 0:
+            times.append(time.perf_counter() - t0)
+    sec = sum(times) / len(times)
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
+    return {"value": n_views / sec, "unit": "frames/s", "cores": min(omp, cores), "kind": "port",
+            "sample": f"{n_views} views of the same workload (cow, {H}x{W}, fwd+bwd), 1 warm-up + {reps} timed "
+                      f"passes, {sec:.2f} s/pass; C naive rasterizer (OpenMP {min(omp, cores)} threads) + "
+                      f"torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
+
+
+# algorithmic bytes per frame for each kernel we may find dominant
+def algorithmic_bytes(kernel, H, W, F, views):
+    HW = H * W
+    if kernel == "k_raster<1>":          # fragment pass: 28 B/px/K + 36 B/face
+        return (28 * HW + 36 * F) * views
+    if kernel == "k_render_bwd":         # read fragments 28 + read upstream grads 20 B/px + 72 B/face
+        return (48 * HW + 72 * F) * views
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--views", type=int, default=64, help="views per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--mesh", default="cow")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-views", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from torch_renderer_amd import _lib
+    from torch_renderer_amd.assets import load_asset, load_asset_arrays
+    from torch_renderer_amd.structures import Meshes
+    from torch_renderer_amd.torch_renderer import DepthColorRender
+
+    H = W = args.size
+    d = load_asset_arrays(args.mesh)
+    meshes = load_asset(args.mesh, device=dev)
+    verts0 = meshes.shared_verts().detach().cpu()
+    faces = meshes.shared_faces()
+    Fn = faces.shape[0]
+    nv = args.views
+    R_all, t_all, K = canonical_views(verts0, nv * world, H, W)
+    sl = slice(rank * nv, (rank + 1) * nv)
+    R_cv = R_all[sl].to(dev).requires_grad_(True)
+    t_cv = t_all[sl].to(dev).requires_grad_(True)
+    verts = meshes.shared_verts().clone().requires_grad_(True)
+    bmesh = Meshes([verts], [faces], meshes.textures).extend(nv)
+    renderer = DepthColorRender(K.to(dev), (H, W), device=dev)
+    gen = torch.Generator().manual_seed(1 + rank)
+    gD = (torch.rand(nv, H, W, generator=gen) * 2 - 1).to(dev)
+    gS = (torch.rand(nv, H, W, generator=gen) * 2 - 1).to(dev)
+    gC = (torch.rand(nv, H, W, 3, generator=gen) * 2 - 1).to(dev)
+
+    def step():
+        verts.grad = None
+        R_cv.grad = None
+        t_cv.grad = None
+        depth, sil, rgb = renderer.render(bmesh, R_cv, t_cv)
+        torch.autograd.backward([depth, sil, rgb], [gD, gS, gC])
+        if world > 1:
+            dist.all_reduce(verts.grad)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kt = _lib.timing_read()
+    _lib.timing_enable(False)
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    frames = nv * world * args.steps
+    value = frames / elapsed
+    # dominant kernel (by summed device time) and its roofline point
+    dom = max(kt.items(), key=lambda kv: kv[1][1]) if kt else None
+    roof = None
+    if dom is not None:
+        name, (launches, total_ms) = dom
+        avg_s = total_ms / launches / 1e3
+        b = algorithmic_bytes(name, H, W, Fn, nv)
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as fh:
+                pmc = json.load(fh)
+            ent = pmc.get(name)
+            if ent and ent.get("config") == f"{args.mesh}-{H}x{W}-{nv}":
+                traffic = ent.get("hbm_bytes_per_launch")
+        if b is not None:
+            gbs = b / avg_s / 1e9
+            roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
+                    "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": b}
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2),
+                   "share": round(v[1] / sum(x[1] for x in kt.values()), 3)} for k, v in kt.items()}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(verts0, faces.cpu(), d, R_all, t_all, K, H, W, n_views=args.cpu_views)
+    line = {
+        "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic camera poses on the reference's cow mesh + texture (assets/cow.npz from data/cow_mesh)",
+        "config": {"workload": f"{args.mesh} (F={Fn}, V={verts0.shape[0]}), {H}x{W}, {nv} views/GPU, fwd+bwd: "
+                               "depth+silhouette+Phong RGB from one raster pass, grads to verts and per-view R,t",
+                   "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "global_views": nv * world,
+                   "parallelism": f"view-sharded x{world}"},
+        "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -139,6 +139,15 @@ int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, con
                            void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts, float* grad_views,
                            float* grad_vcolors, void* stream);
 
+/* ---------------- instrumentation ---------------- */
+/* Per-kernel timing with HIP events recorded on each launch's stream (bench.py).
+ * enable=1 clears and starts collection; mr_timing_read synchronizes on the
+ * recorded events and returns, per kernel id, launches and summed ms. */
+int32_t mr_timing_enable(int32_t enable);
+int32_t mr_timing_read(int32_t* launches, double* total_ms, int32_t n);
+const char* mr_timing_kernel_name(int32_t k);
+int32_t mr_timing_kernel_count(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,72 @@
+"""The C ABI library loads and exports every symbol include/mi355r.h declares; host-side
+argument validation runs without a GPU (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from torch_renderer_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "mi355r.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mr_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        from torch_renderer_amd import _build
+
+        _build.build()
+    return _lib.load()
+
+
+def test_all_header_symbols_exported(lib):
+    syms = header_symbols()
+    assert len(syms) >= 14
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(_lib.EXPORTED_SYMBOLS) == syms, "ctypes signature table out of sync with the header"
+
+
+def test_version_and_workspace_queries(lib):
+    assert lib.mr_version() == 1
+    a = lib.mr_render_workspace(64, 5856, 512, 512, 0)
+    b = lib.mr_render_workspace(8, 5856, 512, 512, 0)
+    assert a > b > 0
+    assert lib.mr_rasterize_meshes_workspace(2, 1000, 64, 64, 0) > 0
+    assert lib.mr_render_backward_workspace(64, 2930, 5856, 512, 512) > 0
+
+
+def test_invalid_arguments_fail_loudly_without_touching_the_gpu(lib):
+    s = _lib.MrRasterSettings()
+    s.H, s.W, s.faces_per_pixel, s.blur_radius = 64, 64, 4, 0.0
+    rc = lib.mr_rasterize_meshes(None, None, None, 1, 10, ctypes.byref(s), None, None, None, None, None, 0, None)
+    assert rc == 3 and b"faces_per_pixel" in lib.mr_last_error()
+    with pytest.raises(NotImplementedError):
+        _lib.check(rc)
+    s.faces_per_pixel = 1
+    s.H = 0
+    rc = lib.mr_rasterize_meshes(None, None, None, 1, 10, ctypes.byref(s), None, None, None, None, None, 0, None)
+    assert rc == 1 and b"image size" in lib.mr_last_error()
+    s.H, s.blur_radius = 64, -1.0
+    rc = lib.mr_rasterize_meshes(None, None, None, 1, 10, ctypes.byref(s), None, None, None, None, None, 0, None)
+    assert rc == 1
+    with pytest.raises(RuntimeError):
+        _lib.check(rc)
+
+
+def test_struct_layouts_match_header():
+    assert ctypes.sizeof(_lib.MrView) == 64
+    assert ctypes.sizeof(_lib.MrRasterSettings) == 32
+    assert ctypes.sizeof(_lib.MrShadeParams) == 4 * (1 + 3 * 7 + 1 + 2 + 3 + 2 + 1 + 2)
+
+
+def test_missing_library_raises(tmp_path):
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _lib.load(str(tmp_path / "nope.so"))

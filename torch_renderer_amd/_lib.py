@@ -80,6 +80,10 @@ _SIGS = [
     ("mr_render_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _I64, _VP, _I64,
                                   ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP, _VP,
                                   _VP, _VP, _VP, _SZ, _VP, _VP, _VP, _VP]),
+    ("mr_timing_enable", _I32, [_I32]),
+    ("mr_timing_read", _I32, [_VP, _VP, _I32]),
+    ("mr_timing_kernel_name", ctypes.c_char_p, [_I32]),
+    ("mr_timing_kernel_count", _I32, []),
 ]
 
 EXPORTED_SYMBOLS = [s[0] for s in _SIGS]
@@ -127,3 +131,17 @@ def ptr(t):
 
 def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def timing_enable(on: bool = True) -> None:
+    check(load().mr_timing_enable(1 if on else 0))
+
+
+def timing_read() -> dict:
+    """{kernel name: (launches, total_ms)} for launches recorded since timing_enable(True)."""
+    L = load()
+    n = L.mr_timing_kernel_count()
+    launches = (ctypes.c_int32 * n)()
+    total = (ctypes.c_double * n)()
+    check(L.mr_timing_read(ctypes.cast(launches, ctypes.c_void_p), ctypes.cast(total, ctypes.c_void_p), n))
+    return {L.mr_timing_kernel_name(k).decode(): (launches[k], total[k]) for k in range(n) if launches[k]}

@@ -34,10 +34,10 @@
 #include "mr_common.h"
 #include "mr_shade.h"
 
-#define MR_ST 32      // super-tile edge (pixels)
-#define MR_CH 256     // face records staged in LDS per chunk
-#define MR_HT 512     // LDS hash slots in the backward
-#define MR_DEFAULT_CAP 2048
+#define MR_TS 8         // raster tile edge: one 64-lane wave per 8x8 tile (lane = pixel)
+#define MR_BT 32        // tile edge of the modular (fragments) backward
+#define MR_HT 512       // LDS hash slots in the backward
+#define MR_LDS_HIST 16384  // per-view tiles binned through an LDS histogram (else global atomics)
 
 static thread_local char g_err[512];
 static int set_err(int code, const char* fmt, ...) {
@@ -53,57 +53,126 @@ static int set_err(int code, const char* fmt, ...) {
     if (_e != hipSuccess) return set_err(MR_ELAUNCH, "%s: %s", name, hipGetErrorString(_e)); \
   } while (0)
 
+// ---------------------------------------------------------------------------
+// Optional per-kernel timing: HIP events recorded on the launch stream around
+// every kernel while enabled (bench.py reads them to price the dominant kernel).
+// ---------------------------------------------------------------------------
+enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_RASTER_FRAG, KID_RASTER_RENDER, KID_RASTER_BWD,
+                KID_RENDER_BWD, KID_RT_REDUCE, KID_VGRAD_A, KID_VGRAD_B, KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD,
+                KID_COUNT };
+static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_raster<0>", "k_raster<1>",
+                                              "k_raster_bwd", "k_render_bwd", "k_rt_reduce", "k_vgrad_a",
+                                              "k_vgrad_b", "k_vertex_normals", "k_project_faces",
+                                              "k_project_faces_bwd"};
+#define MR_TPOOL 4096
+static struct {
+  int enabled;
+  int created;
+  hipEvent_t ev[2 * MR_TPOOL];
+  int kid[MR_TPOOL];
+  int used;
+  int dropped;
+} g_t;
+
+static int timing_begin(hipStream_t st) {
+  if (!g_t.enabled || g_t.used >= MR_TPOOL) {
+    if (g_t.enabled) g_t.dropped++;
+    return -1;
+  }
+  const int i = g_t.used++;
+  (void)hipEventRecord(g_t.ev[2 * i], st);
+  return i;
+}
+static void timing_end(int i, int kid, hipStream_t st) {
+  if (i < 0) return;
+  g_t.kid[i] = kid;
+  (void)hipEventRecord(g_t.ev[2 * i + 1], st);
+}
+#define MR_TIMED(kid, st, launch)              \
+  do {                                         \
+    const int _ti = timing_begin(st);          \
+    launch;                                    \
+    timing_end(_ti, kid, st);                  \
+  } while (0)
+
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
-struct TileGeom {
-  int NSTX, NSTY, NST, cap;
+// ---------------------------------------------------------------------------
+// Workspace: face records, per-(view, 8x8 tile) face lists (count -> scan ->
+// fill), and the compact per-view list of covered pixels (fused path).
+// ---------------------------------------------------------------------------
+struct BinGeom {
+  int TX, TY, T;
+  int64_t list_cap;
 };
-static TileGeom tile_geom(int H, int W, int64_t max_faces_per_view, int32_t mfpb) {
-  TileGeom g;
-  g.NSTX = ceil_div(W, MR_ST);
-  g.NSTY = ceil_div(H, MR_ST);
-  g.NST = g.NSTX * g.NSTY;
-  int64_t cap = mfpb > 0 ? mfpb : MR_DEFAULT_CAP;
-  if (cap > max_faces_per_view) cap = max_faces_per_view;
-  if (cap < 1) cap = 1;
-  g.cap = (int)cap;
+static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
+  BinGeom g;
+  g.TX = ceil_div(W, MR_TS);
+  g.TY = ceil_div(H, MR_TS);
+  g.T = g.TX * g.TY;
+  // Expected entries: ~(1 + 2*edge/8)^2 tiles per face + large faces; overflowing tiles take
+  // the exact full-view path. max_faces_per_bin (if given) scales the reservation.
+  int64_t cap = 6 * Ftot + 2 * N * (int64_t)g.T + 65536;
+  if (mfpb > 0) cap = (int64_t)mfpb * N * 16 + 65536;
+  g.list_cap = cap;
   return g;
 }
 
 struct RasterWS {
   FaceRec* recs;
-  int* bin_count;
-  int* bin_faces;
+  int* cnt;    // (N*T) zeroed per call
+  int* start;  // (N*T + 1)
+  int* cur;    // (N*T)
+  int* list;   // list_cap
+  int* pcnt;   // (N) covered-pixel counts, zeroed per call (pcnt sits right after cnt)
+  int* vtot;   // (N) per-view list entries
+  int* vbase;  // (N+1) exclusive prefix of vtot
+  int* plist;  // (N*H*W) covered pixel indices, view-major regions
   size_t bytes;
 };
-static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, const TileGeom& g) {
+static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g, bool pixlist) {
   RasterWS w;
   size_t off = 0;
   char* b = (char*)base;
   w.recs = (FaceRec*)(b + off);
-  off = align_up(off + sizeof(FaceRec) * (size_t)Ftot, 256);
-  w.bin_count = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)N * g.NST, 256);
-  w.bin_faces = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)N * g.NST * g.cap, 256);
+  off = align_up(off + sizeof(FaceRec) * (size_t)(Ftot > 0 ? Ftot : 1), 256);
+  w.cnt = (int*)(b + off);
+  w.pcnt = w.cnt + (size_t)N * g.T;
+  off = align_up(off + sizeof(int) * ((size_t)N * g.T + (size_t)N), 256);
+  w.start = (int*)(b + off);
+  off = align_up(off + sizeof(int) * ((size_t)N * g.T + 1), 256);
+  w.vtot = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)N, 256);
+  w.vbase = (int*)(b + off);
+  off = align_up(off + sizeof(int) * ((size_t)N + 1), 256);
+  w.cur = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)N * g.T, 256);
+  w.list = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)g.list_cap, 256);
+  w.plist = (int*)(b + off);
+  if (pixlist) off = align_up(off + sizeof(int) * (size_t)N * H * W, 256);
   w.bytes = off;
   return w;
 }
+static size_t zero_bytes(int64_t N, const BinGeom& g) { return sizeof(int) * ((size_t)N * g.T + (size_t)N); }
 
 // ---------------------------------------------------------------------------
-// 1. setup + binning
+// 1. binning: count -> scan -> fill
 // ---------------------------------------------------------------------------
 struct SetupParams {
-  int H, W, NSTX, NSTY, NST, cap;
+  int H, W, TX, TY, T;
   float bbox_pad;
   int persp, cull;
+  int64_t list_cap;
   FaceRec* recs;
-  int* bin_count;
-  int* bin_faces;
+  int* cnt;
+  int* cur;
+  int* list;
+  const int* vbase;
 };
 
-// Inverse of col_ndc/row_ndc (approximate, widened by one pixel; the raster
+// Inverse of col_ndc/row_ndc (approximate, widened by 0.05 px; the raster
 // kernel repeats the exact per-pixel bbox test, so a superset is all we need).
 MR_DEV void ndc_range_to_pix(float lo, float hi, int S1, int S2, int& p0, int& p1) {
   float range = 2.0f;
@@ -112,8 +181,8 @@ MR_DEV void ndc_range_to_pix(float lo, float hi, int S1, int S2, int& p0, int& p
   // i = ((ndc + off) * S1 - off) / range ; pixel = S1 - 1 - i
   float i_hi = ((hi + off) * (float)S1 - off) / range;
   float i_lo = ((lo + off) * (float)S1 - off) / range;
-  float pf0 = (float)(S1 - 1) - i_hi - 1.0f;
-  float pf1 = (float)(S1 - 1) - i_lo + 1.0f;
+  float pf0 = (float)(S1 - 1) - i_hi - 0.05f;  // inverse error is ~1e-4 px; 0.05 px is ample
+  float pf1 = (float)(S1 - 1) - i_lo + 0.05f;
   pf0 = fminf(fmaxf(pf0, -2.0f), (float)S1 + 1.0f);
   pf1 = fminf(fmaxf(pf1, -2.0f), (float)S1 + 1.0f);
   p0 = (int)floorf(pf0);
@@ -122,7 +191,18 @@ MR_DEV void ndc_range_to_pix(float lo, float hi, int S1, int S2, int& p0, int& p
   if (p1 > S1 - 1) p1 = S1 - 1;
 }
 
-MR_DEV void setup_one(const SetupParams& P, int n, int64_t rec, uint32_t face, const float v[3][3]) {
+MR_DEV bool rec_tiles(const SetupParams& P, const FaceRec& r, int& tx0, int& tx1, int& ty0, int& ty1) {
+  if (!(r.flags & FR_VALID)) return false;
+  int cx0, cx1, cy0, cy1;
+  ndc_range_to_pix(r.xmin - P.bbox_pad, r.xmax + P.bbox_pad, P.W, P.H, cx0, cx1);
+  ndc_range_to_pix(r.ymin - P.bbox_pad, r.ymax + P.bbox_pad, P.H, P.W, cy0, cy1);
+  if (cx0 > cx1 || cy0 > cy1) return false;
+  tx0 = cx0 / MR_TS; tx1 = cx1 / MR_TS;
+  ty0 = cy0 / MR_TS; ty1 = cy1 / MR_TS;
+  return true;
+}
+
+MR_DEV FaceRec make_rec(const SetupParams& P, uint32_t face, const float v[3][3]) {
   FaceRec r;
   r.x0 = v[0][0]; r.y0 = v[0][1]; r.z0 = v[0][2];
   r.x1 = v[1][0]; r.y1 = v[1][1]; r.z1 = v[1][2];
@@ -143,30 +223,11 @@ MR_DEV void setup_one(const SetupParams& P, int n, int64_t rec, uint32_t face, c
   bool fast = valid && __builtin_isfinite(r.area) && r.area != 0.0f;
   if (P.persp) fast = fast && r.z0 > 0.0f && r.z1 > 0.0f && r.z2 > 0.0f;
   r.flags = (valid ? FR_VALID : 0u) | (fast ? FR_FAST : 0u);
-  P.recs[rec] = r;
-  if (!valid) return;
-  int cx0, cx1, cy0, cy1;
-  ndc_range_to_pix(r.xmin - P.bbox_pad, r.xmax + P.bbox_pad, P.W, P.H, cx0, cx1);
-  ndc_range_to_pix(r.ymin - P.bbox_pad, r.ymax + P.bbox_pad, P.H, P.W, cy0, cy1);
-  if (cx0 > cx1 || cy0 > cy1) return;
-  const int tx0 = cx0 / MR_ST, tx1 = cx1 / MR_ST, ty0 = cy0 / MR_ST, ty1 = cy1 / MR_ST;
-  for (int ty = ty0; ty <= ty1; ++ty)
-    for (int tx = tx0; tx <= tx1; ++tx) {
-      const int b = n * P.NST + ty * P.NSTX + tx;
-      const int slot = atomicAdd(&P.bin_count[b], 1);
-      if (slot < P.cap) P.bin_faces[(int64_t)b * P.cap + slot] = (int)rec;
-    }
+  return r;
 }
 
-// World mode: one mesh shared by all views (Meshes.extend(N)); rec = n*F + f.
-__global__ void __launch_bounds__(256) k_setup_world(SetupParams P, const float* __restrict__ verts,
-                                                     const int32_t* __restrict__ faces, int64_t F,
-                                                     const ViewRec* __restrict__ views) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int n = blockIdx.y;
-  if (f >= F) return;
-  const ViewRec V = views[n];
-  float v[3][3];
+MR_DEV void world_face_verts(const float* __restrict__ verts, const int32_t* __restrict__ faces, int64_t f,
+                             const ViewRec& V, float v[3][3]) {
   for (int c = 0; c < 3; ++c) {
     const int32_t vi = faces[3 * f + c];
     const float X[3] = {verts[3 * (int64_t)vi], verts[3 * (int64_t)vi + 1], verts[3 * (int64_t)vi + 2]};
@@ -174,37 +235,182 @@ __global__ void __launch_bounds__(256) k_setup_world(SetupParams P, const float*
     project_point(V, X, vx, vy, vz, v[c][0], v[c][1]);
     v[c][2] = vz;
   }
-  setup_one(P, n, (int64_t)n * F + f, (uint32_t)f, v);
 }
 
-// face_verts mode (PyTorch3D _C boundary): rec = packed face id.
-__global__ void __launch_bounds__(256) k_setup_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot,
-                                                  const int64_t* __restrict__ first, int64_t N) {
+// World mode (one mesh shared by N views, rec = n*F + f): project, write the record,
+// count tile overlaps through an LDS histogram, flush one global atomic per touched tile.
+template <bool LDS>
+__global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const float* __restrict__ verts,
+                                                         const int32_t* __restrict__ faces, int64_t F,
+                                                         const ViewRec* __restrict__ views) {
+  extern __shared__ __attribute__((aligned(16))) int hist[];
+  const int n = blockIdx.y;
+  if (LDS) {
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+  }
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= Ftot) return;
-  // mesh owning f: last n with first[n] <= f (packed, ascending)
+  if (f < F) {
+    const ViewRec V = views[n];
+    float v[3][3];
+    world_face_verts(verts, faces, f, V, v);
+    const FaceRec r = make_rec(P, (uint32_t)f, v);
+    P.recs[(int64_t)n * F + f] = r;
+    int tx0, tx1, ty0, ty1;
+    if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+          const int t = ty * P.TX + tx;
+          if (LDS) atomicAdd(&hist[t], 1);
+          else atomicAdd(&P.cnt[(int64_t)n * P.T + t], 1);
+        }
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
+      if (hist[i]) atomicAdd(&P.cnt[(int64_t)n * P.T + i], hist[i]);
+  }
+}
+
+template <bool LDS>
+__global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F) {
+  extern __shared__ __attribute__((aligned(16))) int hist[];
+  const int n = blockIdx.y;
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  FaceRec r;
+  int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+  bool ok = false;
+  if (f < F) {
+    r = P.recs[(int64_t)n * F + f];
+    ok = rec_tiles(P, r, tx0, tx1, ty0, ty1);
+  }
+  const int rid = (int)((int64_t)n * F + f);
+  if (LDS) {
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    if (ok)
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+    __syncthreads();
+    const int vb = P.vbase[n];
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
+      if (hist[i]) hist[i] = vb + atomicAdd(&P.cur[(int64_t)n * P.T + i], hist[i]);  // reserve a block
+    __syncthreads();
+    if (ok)
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+          const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
+          if (pos < P.list_cap) P.list[pos] = rid;
+        }
+  } else if (ok) {
+    for (int ty = ty0; ty <= ty1; ++ty)
+      for (int tx = tx0; tx <= tx1; ++tx) {
+        const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
+        if (pos < P.list_cap) P.list[pos] = rid;
+      }
+  }
+}
+
+MR_DEV int mesh_of_face(const int64_t* __restrict__ first, int64_t N, int64_t f) {
   int64_t lo = 0, hi = N - 1;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
     if (first[mid] <= f) lo = mid;
     else hi = mid - 1;
   }
+  return (int)lo;
+}
+
+// face_verts mode (PyTorch3D _C boundary): rec = packed face id; global atomics.
+__global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot,
+                                                      const int64_t* __restrict__ first, int64_t N) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= Ftot) return;
+  const int n = mesh_of_face(first, N, f);
   float v[3][3];
   for (int c = 0; c < 3; ++c)
     for (int k = 0; k < 3; ++k) v[c][k] = fv[9 * f + 3 * c + k];
-  setup_one(P, (int)lo, f, (uint32_t)f, v);
+  const FaceRec r = make_rec(P, (uint32_t)f, v);
+  P.recs[f] = r;
+  int tx0, tx1, ty0, ty1;
+  if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
+    for (int ty = ty0; ty <= ty1; ++ty)
+      for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&P.cnt[(int64_t)n * P.T + ty * P.TX + tx], 1);
+}
+
+__global__ void __launch_bounds__(256) k_bin_fill_fv(SetupParams P, int64_t Ftot, const int64_t* __restrict__ first,
+                                                     int64_t N) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= Ftot) return;
+  const int n = mesh_of_face(first, N, f);
+  const FaceRec r = P.recs[f];
+  int tx0, tx1, ty0, ty1;
+  if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
+    for (int ty = ty0; ty <= ty1; ++ty)
+      for (int tx = tx0; tx <= tx1; ++tx) {
+        const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
+        if (pos < P.list_cap) P.list[pos] = (int)f;
+      }
+}
+
+// Per-view exclusive scan of the T tile counts (one 1024-thread workgroup per view):
+// start[n*T+t] = cur[n*T+t] = offset inside view n's region; vtot[n] = entries of view n.
+__global__ void __launch_bounds__(1024) k_bin_scan_views(const int* __restrict__ cnt, int T, int* __restrict__ start,
+                                                         int* __restrict__ cur, int* __restrict__ vtot) {
+  __shared__ int part[1024];
+  const int n = blockIdx.x;
+  const int per = (T + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  const int* c = cnt + (int64_t)n * T;
+  int loc[16];
+  int s = 0;
+  if (per <= 16) {
+    for (int i = 0; i < per; ++i) {
+      loc[i] = b0 + i < T ? c[b0 + i] : 0;
+      s += loc[i];
+    }
+  } else {
+    for (int i = b0; i < b0 + per && i < T; ++i) s += c[i];
+  }
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  int run = part[threadIdx.x] - s;
+  for (int i = 0; i < per; ++i) {
+    const int t = b0 + i;
+    if (t >= T) break;
+    start[(int64_t)n * T + t] = run;
+    cur[(int64_t)n * T + t] = run;
+    run += per <= 16 ? loc[i] : c[t];
+  }
+  if (threadIdx.x == 1023) vtot[n] = part[1023];
+}
+
+// vbase = exclusive prefix of per-view totals (saturating at INT_MAX: tiles beyond the
+// list capacity take the exact overflow path).
+__global__ void __launch_bounds__(64) k_bin_scan_base(const int* __restrict__ vtot, int N, int* __restrict__ vbase) {
+  if (threadIdx.x != 0) return;
+  long long run = 0;
+  for (int n = 0; n < N; ++n) {
+    vbase[n] = (int)(run < 0x7fffffffll ? run : 0x7fffffffll);
+    run += vtot[n];
+  }
+  vbase[N] = (int)(run < 0x7fffffffll ? run : 0x7fffffffll);
 }
 
 // ---------------------------------------------------------------------------
-// 2. raster (+ fused shading)
+// 2. raster (+ fused shading): one wave per 8x8 tile
 // ---------------------------------------------------------------------------
 struct RasterParams {
-  int N, H, W, NSTX, NSTY, NST, cap;
+  int N, H, W, TX, TY, T;
+  int64_t list_cap;
   float blur, bbox_pad;
   int persp, clipb;
-  const FaceRec* recs;
-  const int* bin_count;
-  const int* bin_faces;
   const int64_t* view_first;  // NULL: shared mode (first = n*F, count = F)
   const int64_t* view_count;
   int64_t F;
@@ -220,134 +426,313 @@ struct RasterParams {
   float* sil;
   float* rgb;
   int32_t* p2f32;
+  int* pcnt;
+  int* plist;
+};
+
+// Loop-level test of one face at one pixel: exactly the CPU's decision and depth
+// (edge functions, barycentrics, perspective correction, clip, pz < 0, inside / blur),
+// without the point-triangle distance when blur == 0 (it only matters for the winner,
+// whose fragment is recomputed in full by eval_face in the epilogue).
+//
+// Stage 1 (cand_test): branch-free bbox + edge-sign necessary condition, evaluated for
+// several faces back to back so their dependency chains overlap.
+MR_DEV bool cand_test(const FaceRec r, float x, float y, float pad, bool fast_ok) {
+  // Bitwise (non-short-circuit) logic on register values: one branch-free block.
+  // For valid (finite) faces, !(x > a) == (x <= a).
+  const bool inb = (x <= r.xmax + pad) & (x >= r.xmin - pad) & (y <= r.ymax + pad) & (y >= r.ymin - pad);
+  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
+  const bool pos = r.area > 0.0f;
+  const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
+  const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
+  const bool in = pos ? inp : inn;
+  const bool fast = fast_ok & ((r.flags & FR_FAST) != 0u);
+  return inb & ((r.flags & FR_VALID) != 0u) & (!fast | in);
+}
+
+// Stage 2: exact evaluation of a candidate. On the fast path (blur == 0, FR_FAST: finite,
+// all z > 0, pixel strictly inside by edge signs) every barycentric term is positive, so an
+// approximate depth from hardware reciprocals is within a few ulp of the exact one (bounded
+// relative error < 3e-6); a candidate whose approximate depth exceeds the current best by a
+// 3e-5 relative margin cannot win and skips the six correctly-rounded divisions. The winner
+// is always decided by the exact values, so pix_to_face stays bit-identical to the CPU.
+MR_DEV void exact_test(const RasterParams& P, const FaceRec& r, int rid, float x, float y, bool fast, float& bz,
+                       int& bf) {
+  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
+  if (fast && bz < __builtin_inff()) {
+    const float aa = fabsf(r.area);
+    if (aa > 1e-30f && aa < 1e30f) {
+      const float ia = __builtin_amdgcn_rcpf(r.area);
+      const float a0 = e0 * ia, a1 = e1 * ia, a2 = e2 * ia;
+      float za;
+      if (P.persp) {
+        const float t0 = a0 * r.z1 * r.z2, t1 = a1 * r.z0 * r.z2, t2 = a2 * r.z0 * r.z1;
+        const float d = t0 + t1 + t2;
+        za = d > 1e-6f && d < 1e30f ? (t0 * r.z0 + t1 * r.z1 + t2 * r.z2) * __builtin_amdgcn_rcpf(d) : -1.0f;
+      } else {
+        za = a0 * r.z0 + a1 * r.z1 + a2 * r.z2;
+      }
+      if (za * (1.0f - 3e-5f) > bz) return;
+    }
+  }
+  const float w0 = e0 / r.area, w1 = e1 / r.area, w2 = e2 / r.area;
+  float c0, c1, c2, b0, b1, b2;
+  if (P.persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
+  else { c0 = w0; c1 = w1; c2 = w2; }
+  if (P.clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
+  else { b0 = c0; b1 = c1; b2 = c2; }
+  const float pz = b0 * r.z0 + b1 * r.z1 + b2 * r.z2;
+  if (pz < 0.0f) return;
+  const bool inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
+  if (!inside) {
+    if (!(P.blur > 0.0f)) return;
+    if (pt_tri_dist(x, y, r) >= P.blur) return;
+  }
+  if (frag_less(pz, rid, bz, bf)) {
+    bz = pz;
+    bf = rid;
+  }
+}
+
+// Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
+MR_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ---- output staging for the 64x8-pixel strip of one raster workgroup ----
+#define MR_WGT 8                    // tiles (= waves) per workgroup
+#define MR_SPX (MR_WGT * MR_TS * MR_TS)  // 512 pixels per strip
+#define MR_NONE 0x7fffffff          // "no face" sentinel, larger than any face id
+
+struct StageOut {  // 14 KB, union over the two modes
+  union {
+    struct { float depth[MR_SPX], sil[MR_SPX], rgb[MR_SPX * 4]; int p2f[MR_SPX]; } m1;
+    struct { long long p2f[MR_SPX]; float zbuf[MR_SPX], bary[MR_SPX * 3], dists[MR_SPX]; } m0;
+  };
+};
+
+#define MR_STG 32  // face records staged per wave per batch
+
+struct RasterSmem {
+  union {
+    struct { FaceRec rec[MR_WGT][MR_STG]; int id[MR_WGT][MR_STG]; } stage;  // 17 KB, face loop only
+    StageOut out;                                                         // 14 KB, epilogue only
+  };
+  float bz[MR_WGT][MR_WGT][64];  // per (wave, tile, lane) running minimum, merged at the end
+  int bf[MR_WGT][MR_WGT][64];
 };
 
 template <int MODE>
-__global__ void __launch_bounds__(256) k_raster(RasterParams P) {
-  __shared__ FaceRec srec[MR_CH];
-  __shared__ int sid[MR_CH];
-  const int n = blockIdx.y, st = blockIdx.x;
-  const int stx = st % P.NSTX, sty = st / P.NSTX;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int rx0 = stx * MR_ST + (wave & 1) * 16, ry0 = sty * MR_ST + (wave >> 1) * 16;
-  const int lx = lane & 7, ly = lane >> 3;
-  const int H = P.H, W = P.W;
+MR_DEV void stage_pixel(const RasterParams& P, StageOut& O, int n, int sp, bool hit, int f, const FaceRec& r,
+                        const FragEval& e) {
+  if (MODE == 0) {
+    O.m0.p2f[sp] = hit ? (long long)f : -1ll;
+    O.m0.zbuf[sp] = hit ? e.pz : -1.0f;
+    O.m0.bary[3 * sp + 0] = hit ? e.b0 : -1.0f;
+    O.m0.bary[3 * sp + 1] = hit ? e.b1 : -1.0f;
+    O.m0.bary[3 * sp + 2] = hit ? e.b2 : -1.0f;
+    O.m0.dists[sp] = hit ? e.sdist : -1.0f;
+  } else {
+    PixGeom G;
+    ShadeOut o;
+    ShadeCache C;
+    if (hit) gather_geom(P.S, r.face, G);
+    shade_fwd(P.S, n, hit, G, hit ? e.b0 : 0.f, hit ? e.b1 : 0.f, hit ? e.b2 : 0.f, hit ? e.pz : 0.f,
+              hit ? e.sdist : 0.f, o, C);
+    O.m1.depth[sp] = o.depth;
+    O.m1.sil[sp] = o.sil;
+    O.m1.rgb[4 * sp + 0] = o.rgb[0];
+    O.m1.rgb[4 * sp + 1] = o.rgb[1];
+    O.m1.rgb[4 * sp + 2] = o.rgb[2];
+    O.m1.rgb[4 * sp + 3] = o.alpha;
+    O.m1.p2f[sp] = hit ? f : -1;
+  }
+}
 
-  float xf[4], yf[4], bz[4];
-  int bf[4];
-  bool pv[4];
-  float sxl[4], sxh[4], syl[4], syh[4];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const int sx = rx0 + (p & 1) * 8, sy = ry0 + (p >> 1) * 8;
-    const int px = sx + lx, py = sy + ly;
-    pv[p] = px < W && py < H;
-    xf[p] = col_ndc(px < W ? px : W - 1, H, W);
-    yf[p] = row_ndc(py < H ? py : H - 1, H, W);
-    bz[p] = __builtin_inff();
-    bf[p] = -1;
-    if (sx < W && sy < H) {
-      const int cx1 = sx + 7 < W ? sx + 7 : W - 1, cy1 = sy + 7 < H ? sy + 7 : H - 1;
-      sxh[p] = col_ndc(sx, H, W);
-      sxl[p] = col_ndc(cx1, H, W);
-      syh[p] = row_ndc(sy, H, W);
-      syl[p] = row_ndc(cy1, H, W);
-    } else {  // empty sub-tile: bounds that reject every face
-      sxh[p] = -__builtin_inff();
-      sxl[p] = __builtin_inff();
-      syh[p] = -__builtin_inff();
-      syl[p] = __builtin_inff();
+// Coalesced strip write: thread t owns strip row t/64, column t%64 (one wave = one 256-B row).
+template <int MODE>
+MR_DEV void write_strip(const RasterParams& P, const StageOut& O, int n, int x0, int y0) {
+  const int t = threadIdx.x;
+  const int row = t >> 6, col = t & 63;
+  const int px = x0 + col, py = y0 + row;
+  const int sp = row * 64 + col;
+  if (px < P.W && py < P.H) {
+    const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
+    if (MODE == 0) {
+      P.p2f[pix] = O.m0.p2f[sp];
+      P.zbuf[pix] = O.m0.zbuf[sp];
+      P.dists[pix] = O.m0.dists[sp];
+    } else {
+      if (P.out_flags & MR_OUT_DEPTH) P.depth[pix] = O.m1.depth[sp];
+      if (P.out_flags & MR_OUT_SIL) P.sil[pix] = O.m1.sil[sp];
+      P.p2f32[pix] = O.m1.p2f[sp];
     }
   }
+  // 3- or 4-channel rows as flat float streams: 64 consecutive floats per wave-instruction
+  const int ch = MODE == 0 ? 3 : P.rgb_ch;
+  if (MODE == 1 && !(P.out_flags & MR_OUT_RGB)) return;
+  const int rowlen = 64 * ch;
+  const int ncols = (P.W - x0) < 64 ? (P.W - x0) : 64;
+  for (int j = t; j < 8 * rowlen; j += 512) {
+    const int rr = j / rowlen, q = j - rr * rowlen;
+    const int cc = q / ch, k = q - cc * ch;
+    const int yy = y0 + rr;
+    if (cc >= ncols || yy >= P.H) continue;
+    const int64_t base = ((int64_t)n * P.H + yy) * P.W + x0;
+    if (MODE == 0) P.bary[base * 3 + q] = O.m0.bary[3 * (rr * 64 + cc) + k];
+    else P.rgb[base * ch + q] = O.m1.rgb[4 * (rr * 64 + cc) + k];
+  }
+}
 
-  const int bidx = n * P.NST + st;
-  const int cnt = P.bin_count[bidx];
-  const bool ovf = cnt > P.cap;
+// One 512-thread workgroup = 8 waves = one 64x8-pixel strip (8 tiles of 8x8). The waves
+// split the 8 tiles' face lists (entry i of tile k -> wave i % 8), keep per-lane (z, face)
+// minima for all 8 tiles, merge them through LDS (order-independent: lexicographic min),
+// then wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
+template <int MODE>
+__global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
+                                                const int* __restrict__ list, const int* __restrict__ cnt,
+                                                const int* __restrict__ start, const int* __restrict__ vbase) {
+  __shared__ RasterSmem sm;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = blockIdx.y;
+  const int GX = (P.TX + MR_WGT - 1) / MR_WGT;
+  const int gx = blockIdx.x % GX, ty = blockIdx.x / GX;
+  const int H = P.H, W = P.W;
+  const int x0 = gx * MR_WGT * MR_TS, y0 = ty * MR_TS;
+  const int py = y0 + (lane >> 3);
+  const float y = row_ndc(py < H ? py : H - 1, H, W);
+  const bool fast_ok = !(P.blur > 0.0f);
+  const float pad = P.bbox_pad;
   const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
   const int64_t vcount = P.view_first ? P.view_count[n] : P.F;
-  const int total = ovf ? (int)vcount : cnt;
-  const float pad = P.bbox_pad;
-  const bool fast_ok = !(P.blur > 0.0f);
+  const int64_t vb = vbase[n];
 
-  for (int base = 0; base < total; base += MR_CH) {
-    const int m = (total - base) < MR_CH ? (total - base) : MR_CH;
-    __syncthreads();
-    if (tid < m) {
-      const int rid = ovf ? (int)(vfirst + base + tid) : P.bin_faces[(int64_t)bidx * P.cap + base + tid];
-      srec[tid] = P.recs[rid];
-      sid[tid] = rid;
+#pragma unroll 1
+  for (int k = 0; k < MR_WGT; ++k) {
+    float bz = __builtin_inff();
+    int bf = MR_NONE;
+    const int tx = gx * MR_WGT + k;
+    int64_t ck = 0, s0 = 0;
+    bool ovf = false;
+    if (tx < P.TX) {
+      const int64_t bt = (int64_t)n * P.T + (int64_t)ty * P.TX + tx;
+      const int c = cnt[bt];
+      s0 = vb + start[bt];
+      ovf = s0 + c > P.list_cap;
+      ck = ovf ? vcount : c;
     }
-    __syncthreads();
-    for (int j = 0; j < m; ++j) {
-      const FaceRec r = srec[j];
-      if (!(r.flags & FR_VALID)) continue;
-      const int rid = sid[j];
-      const bool fast = fast_ok && (r.flags & FR_FAST);
+    if (ck > 0) {
+      const int px = tx * MR_TS + (lane & 7);
+      const bool pv = px < W && py < H;
+      const float x = col_ndc(pv ? px : 0, H, W);
+      // overflow: the "list" is every face of the view, filtered by the tile's bbox
+      const int tx1 = tx * MR_TS + 7 < W ? tx * MR_TS + 7 : W - 1, ty1 = y0 + 7 < H ? y0 + 7 : H - 1;
+      const float sxh = col_ndc(tx * MR_TS, H, W), sxl = col_ndc(tx1, H, W);
+      const float syh = row_ndc(y0, H, W), syl = row_ndc(ty1, H, W);
+      // software-pipelined gather: batch b+1's records are loaded into registers while
+      // batch b is tested out of LDS
+      auto gather = [&](int64_t i0, FaceRec& q, int& qid) {
+        const int64_t i = i0 + (int64_t)MR_WGT * lane;
+        qid = -1;
+        q.flags = 0u;
+        if (lane < MR_STG && i < ck) {
+          qid = ovf ? (int)(vfirst + i) : list[s0 + i];
+          q = recs[qid];
+          if (ovf && (!(q.flags & FR_VALID) || q.xmax + pad < sxl || q.xmin - pad > sxh || q.ymax + pad < syl ||
+                      q.ymin - pad > syh))
+            q.flags = 0u;
+        }
+      };
+      FaceRec nq;
+      int nid;
+      gather(wave, nq, nid);
+      for (int64_t i0 = wave; i0 < ck; i0 += MR_WGT * MR_STG) {
+        const int64_t rem = (ck - i0 + MR_WGT - 1) / MR_WGT;
+        const int m = rem < MR_STG ? (int)rem : MR_STG;
+        wave_lds_sync();  // previous batch fully read
+        if (lane < MR_STG) {
+          sm.stage.rec[wave][lane] = nq;
+          sm.stage.id[wave][lane] = nid;
+        }
+        wave_lds_sync();
+        if (i0 + MR_WGT * MR_STG < ck) gather(i0 + MR_WGT * MR_STG, nq, nid);
+#pragma unroll 1
+        for (int j = 0; j < m; j += 4) {
+          // stage 1 for four faces (independent chains) -> per-lane candidate bits
+          unsigned cm = 0u;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) {
-        if (r.xmax + pad < sxl[p] || r.xmin - pad > sxh[p] || r.ymax + pad < syl[p] || r.ymin - pad > syh[p])
-          continue;
-        if (!pv[p]) continue;
-        const float x = xf[p], y = yf[p];
-        if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) continue;
-        if (fast && fast_reject(r, x, y)) continue;
-        FragEval e;
-        if (eval_face(r, x, y, pad, P.blur, P.persp, P.clipb, e) && frag_less(e.pz, rid, bz[p], bf[p])) {
-          bz[p] = e.pz;
-          bf[p] = rid;
+          for (int q = 0; q < 4; ++q) {
+            const FaceRec r = sm.stage.rec[wave][j + q];  // by value: 4 x ds_read_b128 (rows past m have flags 0)
+#ifndef MR_EXP_NO_CAND
+            const bool cnd = pv & cand_test(r, x, y, pad, fast_ok);
+#else
+            const bool cnd = false;
+            asm volatile("" ::"v"(r.x0));
+#endif
+            cm |= cnd ? (1u << q) : 0u;
+          }
+#ifdef MR_EXP_NO_EXACT
+          asm volatile("" ::"v"(cm));
+          cm = 0u;
+#endif
+          // stage 2: one exact evaluation path, entered per candidate face
+#pragma unroll 1
+          for (int q = 0; q < 4; ++q) {
+            if ((cm >> q) & 1u) {
+              const FaceRec r = sm.stage.rec[wave][j + q];
+              exact_test(P, r, sm.stage.id[wave][j + q], x, y, fast_ok && (r.flags & FR_FAST), bz, bf);
+            }
+          }
         }
       }
+      wave_lds_sync();
+    }
+    sm.bz[wave][k][lane] = bz;
+    sm.bf[wave][k][lane] = bf;
+  }
+  __syncthreads();
+  float z = __builtin_inff();
+  int f = MR_NONE;
+  for (int v = 0; v < MR_WGT; ++v) {
+    const float zz = sm.bz[v][wave][lane];
+    const int ff = sm.bf[v][wave][lane];
+    if (frag_less(zz, ff, z, f)) {
+      z = zz;
+      f = ff;
     }
   }
-
-  // epilogue
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    if (!pv[p]) continue;
-    const int px = rx0 + (p & 1) * 8 + lx, py = ry0 + (p >> 1) * 8 + ly;
-    const int64_t pix = ((int64_t)n * H + py) * W + px;
-    FragEval e;
-    FaceRec r;
-    bool hit = bf[p] >= 0;
-    if (hit) {
-      r = P.recs[bf[p]];
-      hit = eval_face(r, xf[p], yf[p], pad, P.blur, P.persp, P.clipb, e);  // recompute (deterministic)
-    }
-    if (MODE == 0) {
+  // wave k finalises tile k of the strip
+  const int px = x0 + wave * MR_TS + (lane & 7);
+  const bool pv = px < W && py < H;
+  FragEval e;
+  FaceRec r;
+  bool hit = f != MR_NONE && pv;
+  if (hit) {
+    r = recs[f];
+    hit = eval_face(r, col_ndc(px, H, W), y, P.bbox_pad, P.blur, P.persp, P.clipb, e);
+  }
+  const int sp = (lane >> 3) * 64 + wave * MR_TS + (lane & 7);
+  stage_pixel<MODE>(P, sm.out, n, sp, hit, f, r, e);
+  if (MODE == 1) {  // compact list of covered pixels for the backward (one atomic per wave)
+    const unsigned long long msk = __ballot(hit);
+    if (msk) {
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&P.pcnt[n], __popcll(msk));
+      base = __shfl(base, 0, 64);
       if (hit) {
-        P.p2f[pix] = bf[p];
-        P.zbuf[pix] = e.pz;
-        P.bary[3 * pix + 0] = e.b0;
-        P.bary[3 * pix + 1] = e.b1;
-        P.bary[3 * pix + 2] = e.b2;
-        P.dists[pix] = e.sdist;
-      } else {
-        P.p2f[pix] = -1;
-        P.zbuf[pix] = -1.0f;
-        P.bary[3 * pix + 0] = -1.0f;
-        P.bary[3 * pix + 1] = -1.0f;
-        P.bary[3 * pix + 2] = -1.0f;
-        P.dists[pix] = -1.0f;
+        const int rank = __popcll(msk & ((1ull << lane) - 1ull));
+        P.plist[(int64_t)n * H * W + base + rank] = py * W + px;
       }
-    } else {
-      PixGeom G;
-      ShadeOut o;
-      ShadeCache C;
-      if (hit) gather_geom(P.S, r.face, G);
-      shade_fwd(P.S, n, hit, G, hit ? e.b0 : 0.f, hit ? e.b1 : 0.f, hit ? e.b2 : 0.f, hit ? e.pz : 0.f,
-                hit ? e.sdist : 0.f, o, C);
-      if (P.out_flags & MR_OUT_DEPTH) P.depth[pix] = o.depth;
-      if (P.out_flags & MR_OUT_SIL) P.sil[pix] = o.sil;
-      if (P.out_flags & MR_OUT_RGB) {
-        float* q = P.rgb + pix * P.rgb_ch;
-        q[0] = o.rgb[0];
-        q[1] = o.rgb[1];
-        q[2] = o.rgb[2];
-        if (P.rgb_ch == 4) q[3] = o.alpha;
-      }
-      P.p2f32[pix] = hit ? bf[p] : -1;
     }
   }
+  __syncthreads();
+  write_strip<MODE>(P, sm.out, n, x0, y0);
 }
 
 // ---------------------------------------------------------------------------
@@ -407,7 +792,7 @@ MR_DEV void acc_flush(LdsAcc<ACC>& L, float* __restrict__ gdst) {
 
 // Modular backward (PyTorch3D _C.rasterize_meshes_backward), K = 1.
 struct RasterBwdParams {
-  int N, H, W, NSTX, NST;
+  int N, H, W, NBX;
   int persp, clipb;
   const float* fv;
   const int64_t* p2f;
@@ -421,11 +806,11 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   __shared__ LdsAcc<9> L;
   acc_init(L);
   __syncthreads();
-  const int n = blockIdx.y, st = blockIdx.x;
-  const int stx = st % P.NSTX, sty = st / P.NSTX;
-  const int px = stx * MR_ST + (threadIdx.x & 31);
+  const int n = blockIdx.y, bt = blockIdx.x;
+  const int btx = bt % P.NBX, bty = bt / P.NBX;
+  const int px = btx * MR_BT + (threadIdx.x & 31);
   for (int k = 0; k < 4; ++k) {
-    const int py = sty * MR_ST + (threadIdx.x >> 5) + 8 * k;
+    const int py = bty * MR_BT + (threadIdx.x >> 5) + 8 * k;
     if (px >= P.W || py >= P.H) continue;
     const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
     const int64_t f = P.p2f[pix];
@@ -445,13 +830,16 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   acc_flush(L, P.gfv);
 }
 
-// Fused render backward.
+// Fused render backward over the compact per-view list of covered pixels written by
+// k_raster<1>: workgroup (b, n) handles entries [1024 b, 1024 b + 1024) of view n.
 struct RenderBwdParams {
-  int N, H, W, NSTX, NST;
+  int N, H, W, NB;
   float blur, bbox_pad;
   int persp, clipb;
   const FaceRec* recs;
   const int32_t* p2f32;
+  const int* pcnt;
+  const int* plist;
   const float* gD;
   const float* gS;
   const float* gRGB;
@@ -459,62 +847,71 @@ struct RenderBwdParams {
   ShadeParams S;
   const ViewRec* views;
   float* gface;   // (F, ACC)
-  float* rt_part; // (N*NST, 12)
+  float* rt_part; // (N*NB, 12)
 };
 
 template <int ACC>
 __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdParams P) {
   __shared__ LdsAcc<ACC> L;
   __shared__ float red[4][12];
-  acc_init(L);
-  __syncthreads();
-  const int n = blockIdx.y, st = blockIdx.x;
-  const int stx = st % P.NSTX, sty = st / P.NSTX;
-  const int px = stx * MR_ST + (threadIdx.x & 31);
-  const ViewRec V = P.views[n];
+  const int n = blockIdx.y;
+  const int cntp = P.pcnt[n];
   float gR[9], gT[3];
   for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
   for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
-  for (int k = 0; k < 4; ++k) {
-    const int py = sty * MR_ST + (threadIdx.x >> 5) + 8 * k;
-    if (px >= P.W || py >= P.H) continue;
-    const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
-    const int rid = P.p2f32[pix];
-    if (rid < 0) continue;
-    const FaceRec r = P.recs[rid];
-    const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
-    FragEval e;
-    if (!eval_face(r, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e)) continue;
-    PixGeom G;
-    gather_geom(P.S, r.face, G);
-    ShadeOut o;
-    ShadeCache C;
-    shade_fwd(P.S, n, true, G, e.b0, e.b1, e.b2, e.pz, e.sdist, o, C);
-    const float gD = P.gD ? P.gD[pix] : 0.0f;
-    const float gS = P.gS ? P.gS[pix] : 0.0f;
-    float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
-    if (P.gRGB) {
-      const float* q = P.gRGB + pix * P.rgb_ch;
-      gC[0] = q[0];
-      gC[1] = q[1];
-      gC[2] = q[2];
-      if (P.rgb_ch == 4) gA = q[3];
-    }
-    ShadeGrad SG;
-    shade_bwd(P.S, G, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
-    float gfv[3][3];
-    raster_bwd_pixel(r, xf, yf, P.persp, P.clipb, SG.gz, SG.gb, SG.gsd, gfv);
-    float row[ACC];
-    for (int c = 0; c < 3; ++c) {
-      float gX[3];
-      project_bwd(V, G.X[c], gfv[c], gX, gR, gT);
-      for (int a = 0; a < 3; ++a) {
-        row[3 * c + a] = SG.gX[c][a] + gX[a];
-        row[9 + 3 * c + a] = SG.gN[c][a];
-        if (ACC == 27) row[18 + 3 * c + a] = SG.gC[c][a];
+  if ((int64_t)blockIdx.x * 256 >= cntp) {  // uniform over the workgroup: nothing to do
+    if (threadIdx.x < 12) P.rt_part[((int64_t)n * P.NB + blockIdx.x) * 12 + threadIdx.x] = 0.0f;
+    return;
+  }
+  acc_init(L);
+  __syncthreads();
+  const ViewRec V = P.views[n];
+  const int64_t HW = (int64_t)P.H * P.W;
+  // grid-stride over 256-pixel chunks of view n's compact covered-pixel list (one pixel per thread)
+  for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < cntp; c0 += (int64_t)gridDim.x * 256) {
+    {
+      const int64_t idx = c0 + threadIdx.x;
+      if (idx >= cntp) continue;
+      const int q = P.plist[n * HW + idx];
+      const int px = q % P.W, py = q / P.W;
+      const int64_t pix = n * HW + q;
+      const int rid = P.p2f32[pix];
+      if (rid < 0) continue;
+      const FaceRec r = P.recs[rid];
+      const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
+      FragEval e;
+      if (!eval_face(r, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e)) continue;
+      PixGeom G;
+      gather_geom(P.S, r.face, G);
+      ShadeOut o;
+      ShadeCache C;
+      shade_fwd(P.S, n, true, G, e.b0, e.b1, e.b2, e.pz, e.sdist, o, C);
+      const float gD = P.gD ? P.gD[pix] : 0.0f;
+      const float gS = P.gS ? P.gS[pix] : 0.0f;
+      float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
+      if (P.gRGB) {
+        const float* g = P.gRGB + pix * P.rgb_ch;
+        gC[0] = g[0];
+        gC[1] = g[1];
+        gC[2] = g[2];
+        if (P.rgb_ch == 4) gA = g[3];
       }
+      ShadeGrad SG;
+      shade_bwd(P.S, G, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
+      float gfv[3][3];
+      raster_bwd_pixel(r, xf, yf, P.persp, P.clipb, SG.gz, SG.gb, SG.gsd, gfv);
+      float row[ACC];
+      for (int c = 0; c < 3; ++c) {
+        float gX[3];
+        project_bwd(V, G.X[c], gfv[c], gX, gR, gT);
+        for (int a = 0; a < 3; ++a) {
+          row[3 * c + a] = SG.gX[c][a] + gX[a];
+          row[9 + 3 * c + a] = SG.gN[c][a];
+          if (ACC == 27) row[18 + 3 * c + a] = SG.gC[c][a];
+        }
+      }
+      acc_add<ACC>(L, P.gface, (int)r.face, row);
     }
-    acc_add<ACC>(L, P.gface, (int)r.face, row);
   }
   // per-view R/T partial sums: wave shuffle + LDS across the 4 waves
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -526,7 +923,7 @@ __global__ void __launch_bounds__(256) k_render_bwd(RenderBwdParams P) {
   __syncthreads();
   if (threadIdx.x < 12) {
     const int i = threadIdx.x;
-    P.rt_part[((int64_t)n * P.NST + st) * 12 + i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
+    P.rt_part[((int64_t)n * P.NB + blockIdx.x) * 12 + i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
   }
   acc_flush(L, P.gface);
 }
@@ -721,35 +1118,45 @@ static int check_settings(const mr_raster_settings_t* s) {
 
 size_t mr_rasterize_meshes_workspace(int64_t num_meshes, int64_t total_faces, int32_t H, int32_t W,
                                      int32_t max_faces_per_bin) {
-  TileGeom g = tile_geom(H, W, total_faces, max_faces_per_bin);
-  return carve_raster_ws(nullptr, num_meshes, total_faces, g).bytes;
+  const int64_t Ftot = total_faces > 0 ? total_faces : 1;
+  BinGeom g = bin_geom(H, W, num_meshes, Ftot, max_faces_per_bin);
+  return carve_raster_ws(nullptr, num_meshes, Ftot, H, W, g, false).bytes;
 }
 
-static SetupParams make_setup(const mr_raster_settings_t* s, const TileGeom& g, const RasterWS& w) {
+static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, const RasterWS& w) {
   SetupParams P;
-  P.H = s->H; P.W = s->W; P.NSTX = g.NSTX; P.NSTY = g.NSTY; P.NST = g.NST; P.cap = g.cap;
+  P.H = s->H; P.W = s->W; P.TX = g.TX; P.TY = g.TY; P.T = g.T;
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
   P.cull = s->cull_backfaces;
+  P.list_cap = g.list_cap;
   P.recs = w.recs;
-  P.bin_count = w.bin_count;
-  P.bin_faces = w.bin_faces;
+  P.cnt = w.cnt;
+  P.cur = w.cur;
+  P.list = w.list;
+  P.vbase = w.vbase;
   return P;
 }
 
-static RasterParams make_raster(const mr_raster_settings_t* s, const TileGeom& g, const RasterWS& w, int64_t N) {
+static RasterParams make_raster(const mr_raster_settings_t* s, const BinGeom& g, int64_t N) {
   RasterParams P;
   memset(&P, 0, sizeof(P));
   P.N = (int)N; P.H = s->H; P.W = s->W;
-  P.NSTX = g.NSTX; P.NSTY = g.NSTY; P.NST = g.NST; P.cap = g.cap;
+  P.TX = g.TX; P.TY = g.TY; P.T = g.T;
+  P.list_cap = g.list_cap;
   P.blur = s->blur_radius;
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
   P.clipb = s->clip_barycentric_coords;
-  P.recs = w.recs;
-  P.bin_count = w.bin_count;
-  P.bin_faces = w.bin_faces;
   return P;
+}
+
+static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, hipStream_t st) {
+  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_views<<<(unsigned)N, 1024, 0, st>>>(w.cnt, g.T, w.start, w.cur, w.vtot)));
+  MR_CHECK_LAUNCH("k_bin_scan_views");
+  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_base<<<1, 64, 0, st>>>(w.vtot, (int)N, w.vbase)));
+  MR_CHECK_LAUNCH("k_bin_scan_base");
+  return MR_OK;
 }
 
 int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const int64_t* count, int64_t N,
@@ -762,24 +1169,27 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   if (!p2f || !zbuf || !bary || !dists || !first || !count || (Ftot > 0 && !face_verts))
     return set_err(MR_EINVAL, "NULL tensor argument");
   hipStream_t st = (hipStream_t)stream;
-  const int64_t Fbound = Ftot > 0 ? Ftot : 1;
-  TileGeom g = tile_geom(s->H, s->W, Fbound, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws(ws, N, Fbound, g);
+  const int64_t Fb = Ftot > 0 ? Ftot : 1;
+  BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g, false);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
-  if (hipMemsetAsync(w.bin_count, 0, sizeof(int) * (size_t)N * g.NST, st) != hipSuccess)
-    return set_err(MR_ELAUNCH, "memset failed");
+  if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
+  SetupParams SP = make_setup(s, g, w);
   if (Ftot > 0) {
-    SetupParams SP = make_setup(s, g, w);
-    k_setup_fv<<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N);
-    MR_CHECK_LAUNCH("k_setup_fv");
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
+    MR_CHECK_LAUNCH("k_bin_count_fv");
   }
-  RasterParams P = make_raster(s, g, w, N);
+  if ((rc = launch_scan(w, N, g, st))) return rc;
+  if (Ftot > 0) {
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
+    MR_CHECK_LAUNCH("k_bin_fill_fv");
+  }
+  RasterParams P = make_raster(s, g, N);
   P.view_first = first;
   P.view_count = count;
-  P.F = 0;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
-  dim3 grid(g.NST, (unsigned)N);
-  k_raster<0><<<grid, 256, 0, st>>>(P);
+  dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
+  MR_TIMED(KID_RASTER_FRAG, st, (k_raster<0><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
   MR_CHECK_LAUNCH("k_raster<0>");
   return MR_OK;
 }
@@ -795,13 +1205,12 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
   if (Ftot > 0 && hipMemsetAsync(gfv, 0, sizeof(float) * 9 * (size_t)Ftot, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   if (Ftot == 0) return MR_OK;
-  TileGeom g = tile_geom(s->H, s->W, Ftot, s->max_faces_per_bin);
   RasterBwdParams P;
-  P.N = (int)N; P.H = s->H; P.W = s->W; P.NSTX = g.NSTX; P.NST = g.NST;
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.NBX = ceil_div(s->W, MR_BT);
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
   P.fv = fv; P.p2f = p2f; P.gz = gz; P.gb = gb; P.gd = gd; P.gfv = gfv;
-  dim3 grid(g.NST, (unsigned)N);
-  k_raster_bwd<<<grid, 256, 0, st>>>(P);
+  dim3 grid(P.NBX * ceil_div(s->H, MR_BT), (unsigned)N);
+  MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd<<<grid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_raster_bwd");
   return MR_OK;
 }
@@ -812,7 +1221,7 @@ int32_t mr_project_faces(const float* verts, int64_t V, const int32_t* faces, in
   if (F == 0) return MR_OK;
   if (!verts || !faces || !views || !fv) return set_err(MR_EINVAL, "NULL argument");
   dim3 grid(ceil_div(F, 256), (unsigned)N);
-  k_project_faces<<<grid, 256, 0, (hipStream_t)stream>>>(verts, faces, F, (const ViewRec*)views, fv);
+  MR_TIMED(KID_PROJECT, (hipStream_t)stream, (k_project_faces<<<grid, 256, 0, (hipStream_t)stream>>>(verts, faces, F, (const ViewRec*)views, fv)));
   MR_CHECK_LAUNCH("k_project_faces");
   return MR_OK;
 }
@@ -829,7 +1238,7 @@ int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* 
     return set_err(MR_ELAUNCH, "memset failed");
   if (V == 0) return MR_OK;
   dim3 grid(ceil_div(V, 256), (unsigned)N);
-  k_project_faces_bwd<<<grid, 256, 0, st>>>(verts, V, F, ptr, adj, (const ViewRec*)views, gfv, gverts, gviews);
+  MR_TIMED(KID_PROJECT_BWD, st, (k_project_faces_bwd<<<grid, 256, 0, st>>>(verts, V, F, ptr, adj, (const ViewRec*)views, gfv, gverts, gviews)));
   MR_CHECK_LAUNCH("k_project_faces_bwd");
   return MR_OK;
 }
@@ -838,7 +1247,7 @@ int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, i
                           const int32_t* adj, float* vn, float* vraw, void* stream) {
   (void)F;
   if (V <= 0) return MR_OK;
-  k_vertex_normals<<<ceil_div(V, 256), 256, 0, (hipStream_t)stream>>>(verts, V, faces, ptr, adj, vn, vraw);
+  MR_TIMED(KID_VNORMALS, (hipStream_t)stream, (k_vertex_normals<<<ceil_div(V, 256), 256, 0, (hipStream_t)stream>>>(verts, V, faces, ptr, adj, vn, vraw)));
   MR_CHECK_LAUNCH("k_vertex_normals");
   return MR_OK;
 }
@@ -892,8 +1301,8 @@ static int check_mesh(const mr_mesh_t* m, const mr_shade_params_t* sp) {
 }
 
 size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin) {
-  TileGeom g = tile_geom(H, W, F, max_faces_per_bin);
-  return carve_raster_ws(nullptr, N, N * F, g).bytes;
+  BinGeom g = bin_geom(H, W, N, N * F, max_faces_per_bin);
+  return carve_raster_ws(nullptr, N, N * F, H, W, g, true).bytes;
 }
 
 int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
@@ -905,24 +1314,33 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   if (rc) return rc;
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if ((int64_t)N * m->F >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
+  if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
   if (!p2f32 || !views) return set_err(MR_EINVAL, "NULL output");
   if ((sp->out_flags & MR_OUT_DEPTH) && !depth) return set_err(MR_EINVAL, "depth output NULL");
   if ((sp->out_flags & MR_OUT_SIL) && !sil) return set_err(MR_EINVAL, "silhouette output NULL");
   if ((sp->out_flags & MR_OUT_RGB) && !rgb) return set_err(MR_EINVAL, "rgb output NULL");
   if (sp->light_kind == 0 && (!cc || (ncc != 1 && ncc != N))) return set_err(MR_EINVAL, "camera centres");
   hipStream_t st = (hipStream_t)stream;
-  TileGeom g = tile_geom(s->H, s->W, m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws(ws, N, N * m->F, g);
+  BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, true);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
-  if (hipMemsetAsync(w.bin_count, 0, sizeof(int) * (size_t)N * g.NST, st) != hipSuccess)
-    return set_err(MR_ELAUNCH, "memset failed");
+  if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
   dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
-  k_setup_world<<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views);
-  MR_CHECK_LAUNCH("k_setup_world");
-  RasterParams P = make_raster(s, g, w, N);
-  P.view_first = nullptr;
-  P.view_count = nullptr;
+  const bool lds = g.T <= MR_LDS_HIST;
+  const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+  if (lds)
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+  else
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+  MR_CHECK_LAUNCH("k_bin_count_world");
+  if ((rc = launch_scan(w, N, g, st))) return rc;
+  if (lds)
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
+  else
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
+  MR_CHECK_LAUNCH("k_bin_fill_world");
+  RasterParams P = make_raster(s, g, N);
   P.F = m->F;
   P.S = make_shade(m, sp, cc, ncc);
   P.out_flags = sp->out_flags;
@@ -931,16 +1349,26 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  dim3 grid(g.NST, (unsigned)N);
-  k_raster<1><<<grid, 256, 0, st>>>(P);
+  P.pcnt = w.pcnt;
+  P.plist = w.plist;
+  dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
+  MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
   MR_CHECK_LAUNCH("k_raster<1>");
   return MR_OK;
 }
 
+// Backward workgroups per view: ~4096 in total, never more than the view's 256-pixel chunks.
+static int bwd_blocks_per_view(int64_t N, int H, int W) {
+  const int chunks = ceil_div((int64_t)H * W, 256);
+  int nb = ceil_div(4096, N);
+  if (nb > chunks) nb = chunks;
+  return nb < 1 ? 1 : nb;
+}
+
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
-  const int NST = ceil_div(W, MR_ST) * ceil_div(H, MR_ST);
+  const int NB = bwd_blocks_per_view(N, H, W);
   size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * NST, 256);
+  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB, 256);
   off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);
   return off;
 }
@@ -960,25 +1388,28 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   const size_t need = mr_render_backward_workspace(N, m->V, m->F, s->H, s->W);
   if (bws_bytes < need) return set_err(MR_EWORKSPACE, "backward workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  TileGeom g = tile_geom(s->H, s->W, m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, g);
+  BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, s->H, s->W, g, true);
   const bool vcol = m->tex_kind == 1;
   const int ACC = vcol ? 27 : 18;
+  const int NB = bwd_blocks_per_view(N, s->H, s->W);
   char* b = (char*)bws;
   float* gface = (float*)b;
   size_t off = align_up(sizeof(float) * 27 * (size_t)m->F, 256);
   float* rt_part = (float*)(b + off);
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * g.NST, 256);
+  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB, 256);
   float* gnu = (float*)(b + off);
   if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
   memset(&P, 0, sizeof(P));
-  P.N = (int)N; P.H = s->H; P.W = s->W; P.NSTX = g.NSTX; P.NST = g.NST;
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.NB = NB;
   P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
   P.recs = w.recs;
   P.p2f32 = p2f32;
+  P.pcnt = w.pcnt;
+  P.plist = w.plist;
   P.gD = (sp->out_flags & MR_OUT_DEPTH) ? gD : nullptr;
   P.gS = (sp->out_flags & MR_OUT_SIL) ? gS : nullptr;
   P.gRGB = (sp->out_flags & MR_OUT_RGB) ? gRGB : nullptr;
@@ -987,23 +1418,61 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   P.views = (const ViewRec*)views;
   P.gface = gface;
   P.rt_part = rt_part;
-  dim3 grid(g.NST, (unsigned)N);
-  if (vcol) k_render_bwd<27><<<grid, 256, 0, st>>>(P);
-  else k_render_bwd<18><<<grid, 256, 0, st>>>(P);
+  dim3 grid(NB, (unsigned)N);
+  if (vcol) MR_TIMED(KID_RENDER_BWD, st, (k_render_bwd<27><<<grid, 256, 0, st>>>(P)));
+  else MR_TIMED(KID_RENDER_BWD, st, (k_render_bwd<18><<<grid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_render_bwd");
-  k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, g.NST, gviews);
+  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, NB, gviews)));
   MR_CHECK_LAUNCH("k_rt_reduce");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V, 256);
   if (vcol) {
-    if (use_n) k_vgrad_a<27><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
-    k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol);
+    if (use_n) MR_TIMED(KID_VGRAD_A, st, (k_vgrad_a<27><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   } else {
-    if (use_n) k_vgrad_a<18><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
-    k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol);
+    if (use_n) MR_TIMED(KID_VGRAD_A, st, (k_vgrad_a<18><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");
   return MR_OK;
 }
+
+int32_t mr_timing_enable(int32_t enable) {
+  if (enable && !g_t.created) {
+    for (int i = 0; i < 2 * MR_TPOOL; ++i)
+      if (hipEventCreate(&g_t.ev[i]) != hipSuccess) return set_err(MR_ELAUNCH, "hipEventCreate failed");
+    g_t.created = 1;
+  }
+  g_t.enabled = enable ? 1 : 0;
+  if (enable) {
+    g_t.used = 0;
+    g_t.dropped = 0;
+  }
+  return MR_OK;
+}
+
+int32_t mr_timing_read(int32_t* launches, double* total_ms, int32_t n) {
+  if (!g_t.created) return set_err(MR_EINVAL, "timing never enabled");
+  for (int k = 0; k < n && k < KID_COUNT; ++k) {
+    launches[k] = 0;
+    total_ms[k] = 0.0;
+  }
+  for (int i = 0; i < g_t.used; ++i) {
+    if (hipEventSynchronize(g_t.ev[2 * i + 1]) != hipSuccess) return set_err(MR_ELAUNCH, "event sync failed");
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, g_t.ev[2 * i], g_t.ev[2 * i + 1]) != hipSuccess)
+      return set_err(MR_ELAUNCH, "elapsed time failed");
+    const int k = g_t.kid[i];
+    if (k < n) {
+      launches[k] += 1;
+      total_ms[k] += ms;
+    }
+  }
+  g_t.used = 0;
+  return g_t.dropped ? set_err(MR_EWORKSPACE, "timing pool overflow (%d launches dropped)", g_t.dropped) : MR_OK;
+}
+
+const char* mr_timing_kernel_name(int32_t k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : ""; }
+int32_t mr_timing_kernel_count(void) { return KID_COUNT; }
 
 }  // extern "C"

@@ -1,6 +1,6 @@
 // Cycles per face iteration of the real raster kernel: one view, F tiny faces piled into
 // one 8x8 tile (the "blob"), or spread so that each tile holds ~80 faces (the cow case).
-// Build variants with -DMR_EXP_NO_EXACT / -DMR_EXP_NO_CAND.
+// Usage: rc F spread N
 #include "../../torch_renderer_amd/csrc/mr_raster.hip"
 #include <stdlib.h>
 #include <vector>

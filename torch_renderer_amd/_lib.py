@@ -98,7 +98,7 @@ def load(path: str | None = None) -> ctypes.CDLL:
     with _lock:
         if _lib is not None and path is None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("MI355R_LIB") or LIB_PATH  # override: experiment builds
         if not os.path.exists(p):
             raise RuntimeError(
                 f"mi355r: native library not found at {p}. Build it first "

@@ -430,72 +430,78 @@ struct RasterParams {
   int* plist;
 };
 
-// Loop-level test of one face at one pixel: exactly the CPU's decision and depth
-// (edge functions, barycentrics, perspective correction, clip, pz < 0, inside / blur),
-// without the point-triangle distance when blur == 0 (it only matters for the winner,
-// whose fragment is recomputed in full by eval_face in the epilogue).
-//
-// Stage 1 (cand_test): branch-free bbox + edge-sign necessary condition, evaluated for
-// several faces back to back so their dependency chains overlap.
-MR_DEV bool cand_test(const FaceRec r, float x, float y, float pad, bool fast_ok) {
-  // Bitwise (non-short-circuit) logic on register values: one branch-free block.
-  // For valid (finite) faces, !(x > a) == (x <= a).
-  const bool inb = (x <= r.xmax + pad) & (x >= r.xmin - pad) & (y <= r.ymax + pad) & (y >= r.ymin - pad);
+// Exact per-(pixel, face) decision and depth: eval_face's return value and pz, without
+// the point-triangle distance unless blur > 0 and the pixel is outside. On the fast path
+// (blur == 0, FR_FAST) the edge signs reject before any division: a pixel whose edge
+// functions do not all carry the area's strict sign has some w_i <= 0, hence c_i <= 0
+// (all z > 0), hence is not inside, hence eval_face rejects it too.
+MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur, bool persp, bool clipb,
+                      bool fast, float& pz) {
+  if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) return false;
   const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
   const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
   const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
-  const bool pos = r.area > 0.0f;
-  const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
-  const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
-  const bool in = pos ? inp : inn;
-  const bool fast = fast_ok & ((r.flags & FR_FAST) != 0u);
-  return inb & ((r.flags & FR_VALID) != 0u) & (!fast | in);
-}
-
-// Stage 2: exact evaluation of a candidate. On the fast path (blur == 0, FR_FAST: finite,
-// all z > 0, pixel strictly inside by edge signs) every barycentric term is positive, so an
-// approximate depth from hardware reciprocals is within a few ulp of the exact one (bounded
-// relative error < 3e-6); a candidate whose approximate depth exceeds the current best by a
-// 3e-5 relative margin cannot win and skips the six correctly-rounded divisions. The winner
-// is always decided by the exact values, so pix_to_face stays bit-identical to the CPU.
-MR_DEV void exact_test(const RasterParams& P, const FaceRec& r, int rid, float x, float y, bool fast, float& bz,
-                       int& bf) {
-  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
-  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
-  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
-  if (fast && bz < __builtin_inff()) {
-    const float aa = fabsf(r.area);
-    if (aa > 1e-30f && aa < 1e30f) {
-      const float ia = __builtin_amdgcn_rcpf(r.area);
-      const float a0 = e0 * ia, a1 = e1 * ia, a2 = e2 * ia;
-      float za;
-      if (P.persp) {
-        const float t0 = a0 * r.z1 * r.z2, t1 = a1 * r.z0 * r.z2, t2 = a2 * r.z0 * r.z1;
-        const float d = t0 + t1 + t2;
-        za = d > 1e-6f && d < 1e30f ? (t0 * r.z0 + t1 * r.z1 + t2 * r.z2) * __builtin_amdgcn_rcpf(d) : -1.0f;
-      } else {
-        za = a0 * r.z0 + a1 * r.z1 + a2 * r.z2;
-      }
-      if (za * (1.0f - 3e-5f) > bz) return;
-    }
+  if (fast) {
+    const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
+    const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
+    if (!(r.area > 0.0f ? inp : inn)) return false;
   }
   const float w0 = e0 / r.area, w1 = e1 / r.area, w2 = e2 / r.area;
   float c0, c1, c2, b0, b1, b2;
-  if (P.persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
+  if (persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
   else { c0 = w0; c1 = w1; c2 = w2; }
-  if (P.clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
+  if (clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
   else { b0 = c0; b1 = c1; b2 = c2; }
-  const float pz = b0 * r.z0 + b1 * r.z1 + b2 * r.z2;
-  if (pz < 0.0f) return;
+  pz = b0 * r.z0 + b1 * r.z1 + b2 * r.z2;
+  if (pz < 0.0f) return false;
   const bool inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
   if (!inside) {
-    if (!(P.blur > 0.0f)) return;
-    if (pt_tri_dist(x, y, r) >= P.blur) return;
+    if (!(blur > 0.0f)) return false;
+    if (pt_tri_dist(x, y, r) >= blur) return false;
   }
-  if (frag_less(pz, rid, bz, bf)) {
-    bz = pz;
-    bf = rid;
-  }
+  return true;
+}
+
+#define MR_WGT 8                    // tiles (= waves) per workgroup
+#define MR_SPX (MR_WGT * MR_TS * MR_TS)  // 512 pixels per strip
+#define MR_NONE 0x7fffffff          // "no face" sentinel, larger than any face id
+
+// (z, face) packed so that unsigned order == frag_less order on the depths that are ever
+// kept (pz >= 0; -0 folds onto +0, which the CPU compares equal). The empty key sorts
+// after every kept fragment, +inf depth included.
+#define MR_KEY_EMPTY ((0x7f800000ull << 32) | (unsigned long long)MR_NONE)
+MR_DEV unsigned long long frag_key(float z, int f) {
+  const unsigned zb = z == 0.0f ? 0u : __float_as_uint(z);
+  return ((unsigned long long)zb << 32) | (unsigned)f;
+}
+
+// Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP).
+MR_DEV int wave_incl_sum(int v) {
+#ifdef MR_DBG_SHFL
+  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v += u; }
+  return v;
+#endif
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+MR_DEV int wave_incl_max(int v) {
+#ifdef MR_DBG_SHFL
+  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v = max(v, u); }
+  return v;
+#endif
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
+  return v;
 }
 
 // Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
@@ -505,26 +511,33 @@ MR_DEV void wave_lds_sync() {
 }
 
 // ---- output staging for the 64x8-pixel strip of one raster workgroup ----
-#define MR_WGT 8                    // tiles (= waves) per workgroup
-#define MR_SPX (MR_WGT * MR_TS * MR_TS)  // 512 pixels per strip
-#define MR_NONE 0x7fffffff          // "no face" sentinel, larger than any face id
+// Rows padded to 72 entries so the 8 rows one wave's tile touches land in different banks.
+#define MR_SROW 72
+#define MR_SSZ (MR_TS * MR_SROW)
+MR_DEV int strip_slot(int row, int col) { return row * MR_SROW + col; }
 
-struct StageOut {  // 14 KB, union over the two modes
+struct StageOut {  // 18 KB, union over the two modes
   union {
-    struct { float depth[MR_SPX], sil[MR_SPX], rgb[MR_SPX * 4]; int p2f[MR_SPX]; } m1;
-    struct { long long p2f[MR_SPX]; float zbuf[MR_SPX], bary[MR_SPX * 3], dists[MR_SPX]; } m0;
+    struct { float depth[MR_SSZ], sil[MR_SSZ], rgb[MR_SSZ * 4]; int p2f[MR_SSZ]; } m1;
+    struct { long long p2f[MR_SSZ]; float zbuf[MR_SSZ], bary[MR_SSZ * 3], dists[MR_SSZ]; } m0;
   };
 };
 
-#define MR_STG 32  // face records staged per wave per batch
+// One wave's batch of up to 64 (tile, face) entries, expanded into (face, pixel) pairs.
+struct PairStage {
+  FaceRec rec[64];
+  int id[64];
+  int meta[64];  // first pair index | (rect width - 1) << 13 | strip col << 16 | strip row << 22
+  int mark[64];  // pass-local: pair slot -> entry lane that starts there
+};
 
 struct RasterSmem {
   union {
-    struct { FaceRec rec[MR_WGT][MR_STG]; int id[MR_WGT][MR_STG]; } stage;  // 17 KB, face loop only
-    StageOut out;                                                         // 14 KB, epilogue only
+    PairStage ps[MR_WGT];  // 39 KB, face loop only
+    StageOut out;          // epilogue only
   };
-  float bz[MR_WGT][MR_WGT][64];  // per (wave, tile, lane) running minimum, merged at the end
-  int bf[MR_WGT][MR_WGT][64];
+  unsigned long long key[MR_SPX];  // per-pixel (z, face) minimum
+  float xs[64], ys[MR_TS];         // pixel-centre NDC of the strip's columns / rows
 };
 
 template <int MODE>
@@ -554,171 +567,206 @@ MR_DEV void stage_pixel(const RasterParams& P, StageOut& O, int n, int sp, bool 
   }
 }
 
-// Coalesced strip write: thread t owns strip row t/64, column t%64 (one wave = one 256-B row).
+// Coalesced strip write: thread t owns strip row t/64, column t%64 (one wave = one 256-B row);
+// multi-channel rows (bary, rgb) go out as flat float streams, 64 consecutive floats per
+// wave instruction. With O == nullptr the strip is empty and the background is written
+// straight from registers (no LDS round trip).
 template <int MODE>
-MR_DEV void write_strip(const RasterParams& P, const StageOut& O, int n, int x0, int y0) {
+MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0, int y0) {
   const int t = threadIdx.x;
   const int row = t >> 6, col = t & 63;
   const int px = x0 + col, py = y0 + row;
-  const int sp = row * 64 + col;
+  const int sp = strip_slot(row, col);
+  float bgv[4] = {-1.0f, -1.0f, -1.0f, -1.0f}, bgd = -1.0f, bgs = -1.0f;
+  if (MODE == 1 && !O) {
+    PixGeom G;
+    ShadeOut o;
+    ShadeCache C;
+    shade_fwd(P.S, n, false, G, 0.f, 0.f, 0.f, 0.f, 0.f, o, C);
+    bgd = o.depth;
+    bgs = o.sil;
+    bgv[0] = o.rgb[0]; bgv[1] = o.rgb[1]; bgv[2] = o.rgb[2]; bgv[3] = o.alpha;
+  }
   if (px < P.W && py < P.H) {
     const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
     if (MODE == 0) {
-      P.p2f[pix] = O.m0.p2f[sp];
-      P.zbuf[pix] = O.m0.zbuf[sp];
-      P.dists[pix] = O.m0.dists[sp];
+      P.p2f[pix] = O ? O->m0.p2f[sp] : -1ll;
+      P.zbuf[pix] = O ? O->m0.zbuf[sp] : -1.0f;
+      P.dists[pix] = O ? O->m0.dists[sp] : -1.0f;
     } else {
-      if (P.out_flags & MR_OUT_DEPTH) P.depth[pix] = O.m1.depth[sp];
-      if (P.out_flags & MR_OUT_SIL) P.sil[pix] = O.m1.sil[sp];
-      P.p2f32[pix] = O.m1.p2f[sp];
+      if (P.out_flags & MR_OUT_DEPTH) P.depth[pix] = O ? O->m1.depth[sp] : bgd;
+      if (P.out_flags & MR_OUT_SIL) P.sil[pix] = O ? O->m1.sil[sp] : bgs;
+      P.p2f32[pix] = O ? O->m1.p2f[sp] : -1;
     }
   }
-  // 3- or 4-channel rows as flat float streams: 64 consecutive floats per wave-instruction
   const int ch = MODE == 0 ? 3 : P.rgb_ch;
   if (MODE == 1 && !(P.out_flags & MR_OUT_RGB)) return;
   const int rowlen = 64 * ch;
   const int ncols = (P.W - x0) < 64 ? (P.W - x0) : 64;
-  for (int j = t; j < 8 * rowlen; j += 512) {
+  for (int j = t; j < MR_TS * rowlen; j += MR_SPX) {
     const int rr = j / rowlen, q = j - rr * rowlen;
     const int cc = q / ch, k = q - cc * ch;
     const int yy = y0 + rr;
     if (cc >= ncols || yy >= P.H) continue;
     const int64_t base = ((int64_t)n * P.H + yy) * P.W + x0;
-    if (MODE == 0) P.bary[base * 3 + q] = O.m0.bary[3 * (rr * 64 + cc) + k];
-    else P.rgb[base * ch + q] = O.m1.rgb[4 * (rr * 64 + cc) + k];
+    const int s = strip_slot(rr, cc);
+    if (MODE == 0) P.bary[base * 3 + q] = O ? O->m0.bary[3 * s + k] : -1.0f;
+    else P.rgb[base * ch + q] = O ? O->m1.rgb[4 * s + k] : (k == 0 ? bgv[0] : k == 1 ? bgv[1] : k == 2 ? bgv[2] : bgv[3]);
   }
 }
 
-// One 512-thread workgroup = 8 waves = one 64x8-pixel strip (8 tiles of 8x8). The waves
-// split the 8 tiles' face lists (entry i of tile k -> wave i % 8), keep per-lane (z, face)
-// minima for all 8 tiles, merge them through LDS (order-independent: lexicographic min),
-// then wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
+// One 512-thread workgroup = 8 waves = one 64x8-pixel strip (8 tiles of 8x8).
+//  (1) the strip's 8 tile lists are concatenated; each wave takes 64 entries at a time,
+//      one per lane, and clips the face's pixel bbox to its tile (<= 64 pixels);
+//  (2) a wave prefix sum over the rectangle sizes numbers the (face, pixel) pairs, and
+//      64 pairs per pass are evaluated exactly (frag_keep), one per lane — so a ~3-pixel
+//      face costs ~3 lanes, not a whole wave;
+//  (3) kept fragments meet in a per-pixel LDS atomicMin on the packed (z, face) key, which
+//      is order-independent and equals the CPU's "strictly nearer, earlier face wins";
+//  (4) wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
+// Strips with no entries skip (1)-(4) and write the background from registers.
 template <int MODE>
 __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
                                                 const int* __restrict__ list, const int* __restrict__ cnt,
                                                 const int* __restrict__ start, const int* __restrict__ vbase) {
   __shared__ RasterSmem sm;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int n = blockIdx.y;
   const int GX = (P.TX + MR_WGT - 1) / MR_WGT;
   const int gx = blockIdx.x % GX, ty = blockIdx.x / GX;
   const int H = P.H, W = P.W;
   const int x0 = gx * MR_WGT * MR_TS, y0 = ty * MR_TS;
-  const int py = y0 + (lane >> 3);
-  const float y = row_ndc(py < H ? py : H - 1, H, W);
-  const bool fast_ok = !(P.blur > 0.0f);
-  const float pad = P.bbox_pad;
+  const int64_t vb = vbase[n];
   const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
   const int64_t vcount = P.view_first ? P.view_count[n] : P.F;
-  const int64_t vb = vbase[n];
 
-#pragma unroll 1
-  for (int k = 0; k < MR_WGT; ++k) {
-    float bz = __builtin_inff();
-    int bf = MR_NONE;
-    const int tx = gx * MR_WGT + k;
-    int64_t ck = 0, s0 = 0;
-    bool ovf = false;
-    if (tx < P.TX) {
-      const int64_t bt = (int64_t)n * P.T + (int64_t)ty * P.TX + tx;
+  // lanes 0..7 <-> tiles 0..7 of the strip: entry count, list start, overflow flag
+  int tc = 0, ts = 0, tovf = 0;
+  {
+    const int txl = gx * MR_WGT + lane;
+    if (lane < MR_WGT && txl < P.TX) {
+      const int64_t bt = (int64_t)n * P.T + (int64_t)ty * P.TX + txl;
       const int c = cnt[bt];
-      s0 = vb + start[bt];
-      ovf = s0 + c > P.list_cap;
-      ck = ovf ? vcount : c;
-    }
-    if (ck > 0) {
-      const int px = tx * MR_TS + (lane & 7);
-      const bool pv = px < W && py < H;
-      const float x = col_ndc(pv ? px : 0, H, W);
-      // overflow: the "list" is every face of the view, filtered by the tile's bbox
-      const int tx1 = tx * MR_TS + 7 < W ? tx * MR_TS + 7 : W - 1, ty1 = y0 + 7 < H ? y0 + 7 : H - 1;
-      const float sxh = col_ndc(tx * MR_TS, H, W), sxl = col_ndc(tx1, H, W);
-      const float syh = row_ndc(y0, H, W), syl = row_ndc(ty1, H, W);
-      // software-pipelined gather: batch b+1's records are loaded into registers while
-      // batch b is tested out of LDS
-      auto gather = [&](int64_t i0, FaceRec& q, int& qid) {
-        const int64_t i = i0 + (int64_t)MR_WGT * lane;
-        qid = -1;
-        q.flags = 0u;
-        if (lane < MR_STG && i < ck) {
-          qid = ovf ? (int)(vfirst + i) : list[s0 + i];
-          q = recs[qid];
-          if (ovf && (!(q.flags & FR_VALID) || q.xmax + pad < sxl || q.xmin - pad > sxh || q.ymax + pad < syl ||
-                      q.ymin - pad > syh))
-            q.flags = 0u;
-        }
-      };
-      FaceRec nq;
-      int nid;
-      gather(wave, nq, nid);
-      for (int64_t i0 = wave; i0 < ck; i0 += MR_WGT * MR_STG) {
-        const int64_t rem = (ck - i0 + MR_WGT - 1) / MR_WGT;
-        const int m = rem < MR_STG ? (int)rem : MR_STG;
-        wave_lds_sync();  // previous batch fully read
-        if (lane < MR_STG) {
-          sm.stage.rec[wave][lane] = nq;
-          sm.stage.id[wave][lane] = nid;
-        }
-        wave_lds_sync();
-        if (i0 + MR_WGT * MR_STG < ck) gather(i0 + MR_WGT * MR_STG, nq, nid);
-#pragma unroll 1
-        for (int j = 0; j < m; j += 4) {
-          // stage 1 for four faces (independent chains) -> per-lane candidate bits
-          unsigned cm = 0u;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const FaceRec r = sm.stage.rec[wave][j + q];  // by value: 4 x ds_read_b128 (rows past m have flags 0)
-#ifndef MR_EXP_NO_CAND
-            const bool cnd = pv & cand_test(r, x, y, pad, fast_ok);
-#else
-            const bool cnd = false;
-            asm volatile("" ::"v"(r.x0));
-#endif
-            cm |= cnd ? (1u << q) : 0u;
-          }
-#ifdef MR_EXP_NO_EXACT
-          asm volatile("" ::"v"(cm));
-          cm = 0u;
-#endif
-          // stage 2: one exact evaluation path, entered per candidate face
-#pragma unroll 1
-          for (int q = 0; q < 4; ++q) {
-            if ((cm >> q) & 1u) {
-              const FaceRec r = sm.stage.rec[wave][j + q];
-              exact_test(P, r, sm.stage.id[wave][j + q], x, y, fast_ok && (r.flags & FR_FAST), bz, bf);
-            }
-          }
-        }
+      ts = start[bt];
+      // overflowed list: the tile's entries are every face of the view (bbox-filtered below)
+      if (vb + ts + c > P.list_cap) {
+        tovf = 1;
+        tc = (int)(vcount < 0x7fffffffll ? vcount : 0x7fffffffll);
+      } else {
+        tc = c;
       }
-      wave_lds_sync();
     }
-    sm.bz[wave][k][lane] = bz;
-    sm.bf[wave][k][lane] = bf;
+  }
+  const int tincl = wave_incl_sum(tc);
+  const int E = __builtin_amdgcn_readlane(tincl, MR_WGT - 1);
+  if (E == 0) {  // uniform over the workgroup
+    write_strip<MODE>(P, nullptr, n, x0, y0);
+    return;
+  }
+  const int texcl = tincl - tc;
+
+  if (t < 64) sm.xs[t] = col_ndc(x0 + t < W ? x0 + t : W - 1, H, W);
+  else if (t < 64 + MR_TS) sm.ys[t - 64] = row_ndc(y0 + t - 64 < H ? y0 + t - 64 : H - 1, H, W);
+  sm.key[t] = MR_KEY_EMPTY;
+  PairStage& S = sm.ps[wave];
+  S.mark[lane] = -1;
+  __syncthreads();
+
+  const float pad = P.bbox_pad, blur = P.blur;
+  const bool persp = P.persp != 0, clipb = P.clipb != 0;
+#ifdef MR_DBG_NOFAST
+  const bool fast_ok = false;
+#else
+  const bool fast_ok = !(blur > 0.0f);
+#endif
+#pragma unroll 1
+  for (int eb = wave * 64; eb < E; eb += MR_WGT * 64) {
+    // (1) one entry per lane
+    const int e = eb + lane;
+    int k = 0;
+#pragma unroll
+    for (int kk = 1; kk < MR_WGT; ++kk) k += e >= __builtin_amdgcn_readlane(texcl, kk) ? 1 : 0;
+    // cross-lane reads at full EXEC (ds_bpermute from an inactive lane is undefined)
+    const int kex = __shfl(texcl, k, 64);
+    const int kst = __shfl(ts, k, 64);
+    const int kovf = __shfl(tovf, k, 64);
+    int np = 0, meta = 0;
+    if (e < E) {
+      const int i = e - kex;
+      const int id = kovf ? (int)(vfirst + i) : list[vb + kst + i];
+      const FaceRec r = recs[id];
+      int cx0, cx1, cy0, cy1;
+      ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
+      ndc_range_to_pix(r.ymin - pad, r.ymax + pad, H, W, cy0, cy1);
+      const int tx0 = x0 + k * MR_TS;
+      cx0 = cx0 > tx0 ? cx0 : tx0;
+      cx1 = cx1 < tx0 + MR_TS - 1 ? cx1 : tx0 + MR_TS - 1;
+      cy0 = cy0 > y0 ? cy0 : y0;
+      cy1 = cy1 < y0 + MR_TS - 1 ? cy1 : y0 + MR_TS - 1;
+      if ((r.flags & FR_VALID) && cx0 <= cx1 && cy0 <= cy1) {
+        const int w = cx1 - cx0 + 1;
+        np = w * (cy1 - cy0 + 1);
+        meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 22);
+      }
+      S.rec[lane] = r;
+      S.id[lane] = id;
+    }
+    // (2) pair numbering
+    const int pincl = wave_incl_sum(np);
+    const int pexcl = pincl - np;
+    const int NP = __builtin_amdgcn_readlane(pincl, 63);
+    S.meta[lane] = meta | pexcl;
+#pragma unroll 1
+    for (int pb = 0; pb < NP; pb += 64) {
+      wave_lds_sync();
+      // entry starting inside this pass marks its first slot; slot 0 belongs to the entry
+      // straddling pb (the last non-empty entry starting at or before it)
+      if (np > 0 && pexcl > pb && pexcl < pb + 64) S.mark[pexcl - pb] = lane;
+      const unsigned long long own = __ballot(np > 0 && pexcl <= pb);
+      const int straddle = 63 - __builtin_clzll(own);
+      wave_lds_sync();
+      int m = S.mark[lane];
+      S.mark[lane] = -1;
+      if (lane == 0) m = straddle;
+      m = wave_incl_max(m);
+      const int q = pb + lane;
+      if (q < NP) {
+        // (3) one (face, pixel) pair per lane
+        const int mt = S.meta[m];
+        const int loc = q - (mt & 0x1fff);
+        const int w = ((mt >> 13) & 7) + 1;
+#ifdef MR_DBG_IDIV
+        const int ly = loc / w;
+#else
+        const int ly = (int)((float)loc * __builtin_amdgcn_rcpf((float)w) + 1e-3f);
+#endif
+        const int lx = loc - ly * w;
+        const int sx = ((mt >> 16) & 63) + lx, sy = ((mt >> 22) & 7) + ly;
+        const FaceRec r = S.rec[m];
+        float pz;
+        if (frag_keep(r, sm.xs[sx], sm.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
+          atomicMin(&sm.key[sy * 64 + sx], frag_key(pz, S.id[m]));
+      }
+    }
+    wave_lds_sync();  // the stage is rewritten by the next batch
   }
   __syncthreads();
-  float z = __builtin_inff();
-  int f = MR_NONE;
-  for (int v = 0; v < MR_WGT; ++v) {
-    const float zz = sm.bz[v][wave][lane];
-    const int ff = sm.bf[v][wave][lane];
-    if (frag_less(zz, ff, z, f)) {
-      z = zz;
-      f = ff;
-    }
-  }
-  // wave k finalises tile k of the strip
-  const int px = x0 + wave * MR_TS + (lane & 7);
-  const bool pv = px < W && py < H;
-  FragEval e;
+
+  // (4) wave k finalises tile k of the strip
+  const int ly = lane >> 3, lx = wave * MR_TS + (lane & 7);
+  const int px = x0 + lx, py = y0 + ly;
+  const unsigned long long key = sm.key[ly * 64 + lx];
+  const int f = (int)(unsigned)(key & 0xffffffffull);
+  FragEval ev;
   FaceRec r;
-  bool hit = f != MR_NONE && pv;
+  bool hit = f != MR_NONE && px < W && py < H;
   if (hit) {
     r = recs[f];
-    hit = eval_face(r, col_ndc(px, H, W), y, P.bbox_pad, P.blur, P.persp, P.clipb, e);
+    hit = eval_face(r, sm.xs[lx], sm.ys[ly], P.bbox_pad, P.blur, P.persp, P.clipb, ev);
   }
-  const int sp = (lane >> 3) * 64 + wave * MR_TS + (lane & 7);
-  stage_pixel<MODE>(P, sm.out, n, sp, hit, f, r, e);
+  stage_pixel<MODE>(P, sm.out, n, strip_slot(ly, lx), hit, f, r, ev);
   if (MODE == 1) {  // compact list of covered pixels for the backward (one atomic per wave)
     const unsigned long long msk = __ballot(hit);
     if (msk) {
@@ -732,7 +780,7 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
     }
   }
   __syncthreads();
-  write_strip<MODE>(P, sm.out, n, x0, y0);
+  write_strip<MODE>(P, &sm.out, n, x0, y0);
 }
 
 // ---------------------------------------------------------------------------

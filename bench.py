@@ -85,14 +85,21 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
                       f"torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
 
 
-# algorithmic bytes per frame for each kernel we may find dominant
+# Algorithmic bytes per launch (DESIGN.md "Measurement") for each kernel that may dominate.
 def algorithmic_bytes(kernel, H, W, F, views):
     HW = H * W
-    if kernel == "k_raster<1>":          # fragment pass: 28 B/px/K + 36 B/face
+    if kernel == "k_raster<0>":          # modular fragment pass: p2f i64 + zbuf + bary + dists = 28 B/px, 36 B/face
         return (28 * HW + 36 * F) * views
-    if kernel == "k_render_bwd":         # read fragments 28 + read upstream grads 20 B/px + 72 B/face
-        return (48 * HW + 72 * F) * views
+    if kernel == "k_raster<1>":          # fused pass: depth + sil + rgb (3 ch) + p2f i32 = 24 B/px, 36 B/face
+        return (24 * HW + 36 * F) * views
+    if kernel == "k_render_bwd":         # read upstream grads 20 B/px + p2f 4 B/px, 72 B/face (read + grad write)
+        return (24 * HW + 72 * F) * views
     return None
+
+
+# SURVEY.md §8d API-minimum traffic of the whole fwd+bwd path per frame
+def path_bytes_per_frame(H, W, F, tex_texels, views):
+    return 96 * H * W + 108 * F + 12 * tex_texels / views
 
 
 def main():
@@ -197,6 +204,9 @@ def main():
                     "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": b}
     kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2),
                    "share": round(v[1] / sum(x[1] for x in kt.values()), 3)} for k, v in kt.items()}
+    pb = path_bytes_per_frame(H, W, Fn, d["texture_u8"].shape[0] * d["texture_u8"].shape[1], nv)
+    path_roof = {"bytes_per_frame": int(pb), "achieved": round(value * pb / 1e9, 1), "peak": HBM_PEAK_GBS,
+                 "unit": "GB/s", "frac": round(value * pb / 1e9 / HBM_PEAK_GBS, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(verts0, faces.cpu(), d, R_all, t_all, K, H, W, n_views=args.cpu_views)
@@ -209,7 +219,7 @@ def main():
                                "depth+silhouette+Phong RGB from one raster pass, grads to verts and per-view R,t",
                    "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "global_views": nv * world,
                    "parallelism": f"view-sharded x{world}"},
-        "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+        "roofline": roof, "path_roofline": path_roof, "cpu_baseline": cpu, "kernels": kernels,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -124,6 +124,7 @@ def main():
     dev = torch.device("cuda", local)
 
     from torch_renderer_amd import _lib
+    from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset, load_asset_arrays
     from torch_renderer_amd.structures import Meshes
     from torch_renderer_amd.torch_renderer import DepthColorRender
@@ -136,9 +137,9 @@ def main():
     Fn = faces.shape[0]
     nv = args.views
     R_all, t_all, K = canonical_views(verts0, nv * world, H, W)
-    sl = slice(rank * nv, (rank + 1) * nv)
-    R_cv = R_all[sl].to(dev).requires_grad_(True)
-    t_cv = t_all[sl].to(dev).requires_grad_(True)
+    R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
+    R_cv = R_cv.to(dev).requires_grad_(True)
+    t_cv = t_cv.to(dev).requires_grad_(True)
     verts = meshes.shared_verts().clone().requires_grad_(True)
     bmesh = Meshes([verts], [faces], meshes.textures).extend(nv)
     renderer = DepthColorRender(K.to(dev), (H, W), device=dev)
@@ -154,7 +155,7 @@ def main():
         depth, sil, rgb = renderer.render(bmesh, R_cv, t_cv)
         torch.autograd.backward([depth, sil, rgb], [gD, gS, gC])
         if world > 1:
-            dist.all_reduce(verts.grad)
+            D.allreduce_grads([verts])  # the step's only exchange: shared vertex grads
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,76 @@
+"""The N > 1 path's host logic on CPU: world-size-2 gloo process groups exercising view sharding,
+the flattened shared-gradient all_reduce and the point-to-point gather to the root
+(torch_renderer_amd/distributed.py). The GPU ranks run the same code over RCCL."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from torch_renderer_amd import distributed as D
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # every rank holds the same global batch; each renders (here: fabricates) only its shard
+        g = torch.Generator().manual_seed(0)
+        full = torch.rand(n_total, 4, 5, 3, generator=g)
+        local = D.shard_views(full) * 2.0
+        s, e = D.shard_range(n_total, rank, world)
+        assert D.global_view_offset(n_total) == s
+        # replicated "vertex" parameter with rank-dependent grads
+        v = torch.zeros(7, 3, requires_grad=True)
+        c = torch.zeros(5, requires_grad=True)
+        ((v * (rank + 1)).sum() + (c * (rank + 2)).sum()).backward()
+        D.allreduce_grads([v, c, None])
+        got = D.gather_to_root(local, n_total)
+        res = {"v": v.grad.clone(), "c": c.grad.clone(), "range": (s, e), "gather": got}
+        q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n_total", [64, 5])
+def test_gloo_world2_shard_allreduce_gather(n_total):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = torch.Generator().manual_seed(0)
+    full = torch.rand(n_total, 4, 5, 3, generator=g)
+    # shards tile the batch contiguously
+    assert res[0]["range"][0] == 0 and res[0]["range"][1] == res[1]["range"][0] and res[1]["range"][1] == n_total
+    # all_reduce(sum): 1 + 2 and 2 + 3
+    for r in range(world):
+        assert torch.equal(res[r]["v"], torch.full((7, 3), 3.0))
+        assert torch.equal(res[r]["c"], torch.full((5,), 5.0))
+    assert torch.equal(res[0]["gather"], full * 2.0)
+    assert res[1]["gather"] is None
+
+
+def test_shard_range_edges():
+    assert D.shard_range(64, 0, 8) == (0, 8) and D.shard_range(64, 7, 8) == (56, 64)
+    assert [D.shard_range(3, r, 4) for r in range(4)] == [(0, 1), (1, 2), (2, 3), (3, 3)]
+    with pytest.raises(ValueError):
+        D.shard_range(4, 2, 2)
+    assert D.world() == (0, 1)
+    x = torch.arange(10)
+    assert torch.equal(D.shard_views(x), x)

@@ -7,3 +7,6 @@ from .transforms import (quaternion_to_matrix, matrix_to_quaternion, look_at_vie
                          look_at_rotation)
 
 __version__ = "0.1.0"
+from .mesh_renderer import (RasterizationSettings, MeshRasterizer, MeshRenderer, Fragments, rasterize,  # noqa: F401
+                            PointLights, AmbientLights, Materials, BlendParams, SoftPhongShader,
+                            SoftSilhouetteShader)

@@ -1,0 +1,292 @@
+"""PyTorch3D-style rendering API on the MI355X kernels.
+
+The reference reaches the render path through PyTorch3D's classes
+(torch_renderer.py:87-108,132-153; renderer.py:71-101; camera_pose_optimizer.py:131-158,244-250):
+``RasterizationSettings``, ``MeshRasterizer`` -> ``Fragments``, ``PointLights`` /
+``AmbientLights`` / ``Materials`` / ``BlendParams``, ``SoftPhongShader``,
+``SoftSilhouetteShader`` and ``MeshRenderer``. This module mirrors their constructors,
+argument meaning and outputs:
+
+* ``MeshRasterizer(meshes)`` runs the modular path — ``mr_project_faces`` then
+  ``mr_rasterize_meshes`` (the ``pytorch3d._C.rasterize_meshes`` boundary) — and returns
+  ``Fragments`` in PyTorch3D layout (int64 packed ``pix_to_face`` (N,H,W,K), zbuf, bary_coords,
+  dists), differentiable w.r.t. vertex positions and R, T.
+* ``MeshRenderer(meshes)`` with a Soft* shader runs ONE fused launch (project + bin +
+  raster + shade + blend, ``mr_render_forward``) and returns the shader's (N,H,W,4) image,
+  differentiable w.r.t. vertex positions, R, T and vertex colours.
+
+Everything runs on the HIP kernels; there is no CPU fallback. Settings the MI355X path does not
+implement yet (K > 1 or blur > 0 through the shaders, near-plane clipping) raise
+``NotImplementedError`` rather than returning different numbers.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .cameras import CamerasBase, view_batch
+from .kernels import ProjectFaces, RasterizeFaceVerts, ShadeConfig
+from .structures import Meshes
+
+
+# --------------------------------------------------------------------------- settings / params
+@dataclass
+class RasterizationSettings:
+    """upstream mesh/rasterizer.py RasterizationSettings (image_size int -> square)."""
+    image_size: int | tuple = 256
+    blur_radius: float = 0.0
+    faces_per_pixel: int = 1
+    bin_size: int | None = None           # accepted; the MI355X binning uses fixed 8x8 tiles
+    max_faces_per_bin: int | None = None  # list-pool reservation; overflow stays exact
+    perspective_correct: bool | None = None
+    clip_barycentric_coords: bool | None = None
+    cull_backfaces: bool = False
+    z_clip_value: float | None = None
+    cull_to_frustum: bool = False
+
+    def hw(self):
+        s = self.image_size
+        if isinstance(s, int):
+            return s, s
+        return int(s[0]), int(s[1])
+
+
+@dataclass
+class BlendParams:
+    """upstream blending.py BlendParams."""
+    sigma: float = 1e-4
+    gamma: float = 1e-4
+    background_color: tuple = (1.0, 1.0, 1.0)
+
+
+def _triple(x, default):
+    if x is None:
+        x = default
+    t = torch.as_tensor(x, dtype=torch.float32).reshape(-1)
+    if t.numel() == 1:
+        t = t.expand(3)
+    if t.numel() != 3:
+        raise NotImplementedError("lights/materials: one colour per batch (3 values) is supported")
+    return tuple(float(v) for v in t)
+
+
+class PointLights:
+    """upstream lighting.py PointLights (one light shared by the batch)."""
+
+    def __init__(self, ambient_color=((0.5, 0.5, 0.5),), diffuse_color=((0.3, 0.3, 0.3),),
+                 specular_color=((0.2, 0.2, 0.2),), location=((0, 1, 0),), device="cpu"):
+        self.ambient_color = _triple(ambient_color, None)
+        self.diffuse_color = _triple(diffuse_color, None)
+        self.specular_color = _triple(specular_color, None)
+        self.location = location
+        self.device = device
+
+    def location_tuple(self):
+        return _triple(self.location, None)
+
+
+class AmbientLights:
+    """upstream lighting.py AmbientLights (mesh_deformer.py:113): colour = ambient * texel."""
+
+    def __init__(self, ambient_color=((1.0, 1.0, 1.0),), device="cpu"):
+        self.ambient_color = _triple(ambient_color, None)
+        self.device = device
+
+
+class Materials:
+    """upstream materials.py Materials."""
+
+    def __init__(self, ambient_color=((1, 1, 1),), diffuse_color=((1, 1, 1),), specular_color=((1, 1, 1),),
+                 shininess=64, device="cpu"):
+        self.ambient_color = _triple(ambient_color, None)
+        self.diffuse_color = _triple(diffuse_color, None)
+        self.specular_color = _triple(specular_color, None)
+        self.shininess = float(torch.as_tensor(shininess).reshape(-1)[0])
+        self.device = device
+
+
+@dataclass
+class Fragments:
+    """upstream mesh/rasterizer.py Fragments."""
+    pix_to_face: torch.Tensor
+    zbuf: torch.Tensor
+    bary_coords: torch.Tensor
+    dists: torch.Tensor
+
+
+# --------------------------------------------------------------------------- rasterizer
+def _z_clip_value(cameras: CamerasBase, rs: RasterizationSettings):
+    """MeshRasterizer: z_clip_value = znear / 2 for perspective cameras that have a znear."""
+    if rs.z_clip_value is not None:
+        return float(rs.z_clip_value)
+    if cameras.is_perspective() and cameras.get_znear() is not None:
+        return float(torch.as_tensor(cameras.get_znear()).min()) / 2.0
+    return None
+
+
+def _check_no_clipping(face_verts: torch.Tensor, z_clip, cull_to_frustum):
+    """upstream clip_faces is the identity when no vertex lies in front of the clip plane and
+    nothing is culled; anything else needs face splitting -> refuse."""
+    if cull_to_frustum:
+        raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
+    if z_clip is None or face_verts.numel() == 0:
+        return
+    if bool((face_verts[..., 2] < z_clip).any()):
+        raise NotImplementedError(
+            f"geometry crosses the near clip plane z={z_clip}: triangle clipping (clip_faces) is not "
+            "implemented on the MI355X path yet")
+
+
+def _views(meshes: Meshes, cameras: CamerasBase, hw, kwargs):
+    R = kwargs.get("R", None)
+    T = kwargs.get("T", None)
+    n = max(len(meshes), 1 if R is None else R.reshape(-1, 3, 3).shape[0],
+            1 if T is None else T.reshape(-1, 3).shape[0])
+    return view_batch(cameras, hw, R, T, n_views=n)
+
+
+class MeshRasterizer(torch.nn.Module):
+    """upstream mesh/rasterizer.py MeshRasterizer: world -> view -> NDC (MeshRasterizer.transform,
+    with view z kept as the depth), then _C.rasterize_meshes (mr_rasterize_meshes)."""
+
+    def __init__(self, cameras=None, raster_settings=None):
+        super().__init__()
+        self.cameras = cameras
+        self.raster_settings = raster_settings or RasterizationSettings()
+
+    def transform(self, meshes: Meshes, **kwargs):
+        """Packed face_verts (sum F_n, 3, 3): NDC xy + view z, packed ids n*F + f."""
+        cameras = kwargs.get("cameras", self.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward pass")
+        hw = self.raster_settings.hw()
+        R, T, intr = _views(meshes, cameras, hw, kwargs)
+        if meshes.is_shared():
+            return ProjectFaces.apply(meshes.shared_verts(), R, T, meshes.shared_faces(), intr.contiguous())
+        if len(meshes) != R.shape[0]:
+            raise ValueError(f"Meshes batch ({len(meshes)}) and camera batch ({R.shape[0]}) differ")
+        parts = []
+        for i in range(len(meshes)):
+            mi = meshes[i]
+            parts.append(ProjectFaces.apply(mi.shared_verts(), R[i:i + 1], T[i:i + 1], mi.shared_faces(),
+                                            intr[i:i + 1].contiguous()))
+        return torch.cat(parts, 0)
+
+    def forward(self, meshes: Meshes, **kwargs) -> Fragments:
+        cameras = kwargs.get("cameras", self.cameras)
+        rs = kwargs.get("raster_settings", self.raster_settings)
+        H, W = rs.hw()
+        fv = self.transform(meshes, **kwargs)
+        _check_no_clipping(fv, _z_clip_value(cameras, rs), rs.cull_to_frustum)
+        persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
+        clip = rs.blur_radius > 0.0 if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
+        first = meshes.mesh_to_faces_packed_first_idx().to(fv.device)
+        count = meshes.num_faces_per_mesh().to(fv.device)
+        p2f, zbuf, bary, dists = RasterizeFaceVerts.apply(fv, first, count, H, W, int(rs.faces_per_pixel),
+                                                          float(rs.blur_radius), persp, clip,
+                                                          bool(rs.cull_backfaces), rs.max_faces_per_bin)
+        return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+
+
+def rasterize(meshes: Meshes, cameras: CamerasBase, raster_settings: RasterizationSettings, **kwargs) -> Fragments:
+    """Functional form used by callers that consume fragments directly
+    (camera_pose_optimizer.py:244-246, batch_rendering_test.py:274)."""
+    return MeshRasterizer(cameras, raster_settings)(meshes, **kwargs)
+
+
+# --------------------------------------------------------------------------- shaders / renderer
+class _SoftShader(torch.nn.Module):
+    def __init__(self, device="cpu", cameras=None, lights=None, materials=None, blend_params=None):
+        super().__init__()
+        self.cameras = cameras
+        self.lights = lights if lights is not None else PointLights(device=device)
+        self.materials = materials if materials is not None else Materials(device=device)
+        self.blend_params = blend_params if blend_params is not None else BlendParams()
+
+    def forward(self, fragments, meshes, **kwargs):
+        raise NotImplementedError(
+            "shading stored Fragments is not a separate pass on the MI355X path: use MeshRenderer, which "
+            "rasterizes and shades in one fused launch")
+
+
+class SoftPhongShader(_SoftShader):
+    """upstream mesh/shader.py SoftPhongShader: phong_shading + softmax_rgb_blend -> RGBA."""
+
+
+class SoftSilhouetteShader(_SoftShader):
+    """upstream mesh/shader.py SoftSilhouetteShader: sigmoid_alpha_blend -> (1, 1, 1, alpha)."""
+
+    def __init__(self, blend_params=None):
+        super().__init__(blend_params=blend_params)
+
+
+class MeshRenderer(torch.nn.Module):
+    """upstream mesh/renderer.py MeshRenderer: rasterizer + shader, here ONE fused launch."""
+
+    def __init__(self, rasterizer: MeshRasterizer, shader):
+        super().__init__()
+        self.rasterizer = rasterizer
+        self.shader = shader
+
+    def _config(self, cameras, H, W):
+        rs = self.rasterizer.raster_settings
+        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0:
+            raise NotImplementedError("MeshRenderer: faces_per_pixel > 1 / blur_radius > 0 (soft rasterization) "
+                                      "is not implemented on the MI355X fused path yet")
+        if rs.cull_to_frustum:
+            raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
+        sh = self.shader
+        bp = sh.blend_params
+        persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
+        clip = False if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
+        znear = getattr(cameras, "znear", 1.0)
+        zfar = getattr(cameras, "zfar", 100.0)
+        cfg = ShadeConfig(H=H, W=W, persp=persp, clip=clip, cull=bool(rs.cull_backfaces),
+                          max_faces_per_bin=rs.max_faces_per_bin, sigma_rgb=float(bp.sigma), gamma=float(bp.gamma),
+                          background=_triple(bp.background_color, None), znear=float(znear), zfar=float(zfar),
+                          sigma_sil=float(bp.sigma), want_depth=False)
+        if isinstance(sh, SoftSilhouetteShader):
+            cfg.want_rgb = False
+            cfg.want_sil = True
+            return cfg
+        if not isinstance(sh, SoftPhongShader):
+            raise NotImplementedError(f"shader {type(sh).__name__} is not implemented on the MI355X path")
+        lights, mats = sh.lights, sh.materials
+        if isinstance(lights, AmbientLights):
+            cfg.light_kind = 1
+            cfg.light_ambient = lights.ambient_color
+        elif isinstance(lights, PointLights):
+            cfg.light_kind = 0
+            cfg.light_location = lights.location_tuple()
+            cfg.light_ambient = lights.ambient_color
+            cfg.light_diffuse = lights.diffuse_color
+            cfg.light_specular = lights.specular_color
+        else:
+            raise NotImplementedError(f"lights of type {type(lights).__name__}")
+        cfg.mat_ambient, cfg.mat_diffuse, cfg.mat_specular = (mats.ambient_color, mats.diffuse_color,
+                                                              mats.specular_color)
+        cfg.shininess = mats.shininess
+        cfg.want_sil = False
+        cfg.rgb_channels = 4
+        return cfg
+
+    def forward(self, meshes: Meshes, **kwargs) -> torch.Tensor:
+        from .torch_renderer import render_mesh_batch
+
+        cameras = kwargs.get("cameras", self.rasterizer.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward pass")
+        H, W = self.rasterizer.raster_settings.hw()
+        cfg = self._config(cameras, H, W)
+        R, T, _ = _views(meshes, cameras, (H, W), kwargs)
+        z_clip = _z_clip_value(cameras, self.rasterizer.raster_settings)
+        if z_clip is not None:
+            _check_no_clipping(self.rasterizer.transform(meshes, cameras=cameras, R=R, T=T).detach(), z_clip, False)
+        # specular camera position: cameras.get_camera_center() without the R/T kwargs (upstream
+        # shading.py), i.e. from the camera object's own R, T
+        out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg)
+        if cfg.want_rgb:
+            return out["rgb"]
+        sil = out["sil"]
+        return torch.cat([torch.ones(sil.shape + (3,), device=sil.device, dtype=sil.dtype), sil[..., None]], -1)

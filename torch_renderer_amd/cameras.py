@@ -112,13 +112,38 @@ class FoVPerspectiveCameras(CamerasBase):
         return torch.tensor([[ax, 0.0, ay, 0.0]], dtype=torch.float32, device=self.device).expand(n, 4).contiguous()
 
 
+def _param_key(cameras):
+    return tuple((k, v.data_ptr(), v._version) for k, v in sorted(vars(cameras).items()) if torch.is_tensor(v))
+
+
+def cached_ndc_affine(cameras: CamerasBase, image_size, device):
+    """ndc_affine on `device`, recomputed only when the camera's tensors change (their
+    storage or version) — the per-call double-precision conversions are host-side launches."""
+    key = (tuple(int(x) for x in image_size), str(device), _param_key(cameras))
+    c = cameras.__dict__.get("_ndc_cache")
+    if c is None or c[0] != key:
+        c = (key, cameras.ndc_affine(image_size).to(device).contiguous())
+        cameras.__dict__["_ndc_cache"] = c
+    return c[1]
+
+
+def cached_camera_center(cameras: CamerasBase, device):
+    """get_camera_center() (camera's own R, T) on `device`, cached like cached_ndc_affine."""
+    key = (str(device), _param_key(cameras))
+    c = cameras.__dict__.get("_cc_cache")
+    if c is None or c[0] != key:
+        c = (key, cameras.get_camera_center().to(device).contiguous())
+        cameras.__dict__["_cc_cache"] = c
+    return c[1]
+
+
 def view_batch(cameras: CamerasBase, image_size, R=None, T=None, n_views=None):
     """(R (N,3,3), T (N,3), intr (N,4)) for N views, broadcasting singleton camera params."""
     R = cameras.R if R is None else R
     T = cameras.T if T is None else T
     R = R.reshape(-1, 3, 3)
     T = T.reshape(-1, 3)
-    intr = cameras.ndc_affine(image_size).to(R.device)
+    intr = cached_ndc_affine(cameras, image_size, R.device)
     N = n_views or max(R.shape[0], T.shape[0], intr.shape[0])
     for name, t in (("R", R), ("T", T), ("intrinsics", intr)):
         if t.shape[0] not in (1, N):

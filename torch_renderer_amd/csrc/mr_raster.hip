@@ -571,7 +571,7 @@ MR_DEV void stage_pixel(const RasterParams& P, StageOut& O, int n, int sp, bool 
 // multi-channel rows (bary, rgb) go out as flat float streams, 64 consecutive floats per
 // wave instruction. With O == nullptr the strip is empty and the background is written
 // straight from registers (no LDS round trip).
-template <int MODE>
+template <int MODE, int CH>
 MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0, int y0) {
   const int t = threadIdx.x;
   const int row = t >> 6, col = t & 63;
@@ -599,7 +599,7 @@ MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0,
       P.p2f32[pix] = O ? O->m1.p2f[sp] : -1;
     }
   }
-  const int ch = MODE == 0 ? 3 : P.rgb_ch;
+  constexpr int ch = CH;  // compile-time channel count: the flat-stream index math is shifts/multiplies
   if (MODE == 1 && !(P.out_flags & MR_OUT_RGB)) return;
   const int rowlen = 64 * ch;
   const int ncols = (P.W - x0) < 64 ? (P.W - x0) : 64;
@@ -615,6 +615,21 @@ MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0,
   }
 }
 
+// Optional phase timestamps (build with -DMR_PROF; tools/raster_phases.py): per wave 16 slots,
+// s_memtime at phase boundaries, s_memrealtime at start/end, entry/pass counts.
+#ifdef MR_PROF
+__device__ unsigned long long* g_prof = nullptr;
+#define PROF_AT(i, v)                                                                                 \
+  do {                                                                                                \
+    if (g_prof && lane == 0)                                                                          \
+      g_prof[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * MR_WGT + wave) * 16 + (i)] = (v);      \
+  } while (0)
+#define PROF_T(i) PROF_AT(i, __builtin_amdgcn_s_memtime())
+#else
+#define PROF_AT(i, v) do {} while (0)
+#define PROF_T(i) do {} while (0)
+#endif
+
 // One 512-thread workgroup = 8 waves = one 64x8-pixel strip (8 tiles of 8x8).
 //  (1) the strip's 8 tile lists are concatenated; each wave takes 64 entries at a time,
 //      one per lane, and clips the face's pixel bbox to its tile (<= 64 pixels);
@@ -625,7 +640,7 @@ MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0,
 //      is order-independent and equals the CPU's "strictly nearer, earlier face wins";
 //  (4) wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
 // Strips with no entries skip (1)-(4) and write the background from registers.
-template <int MODE>
+template <int MODE, int CH>
 __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
                                                 const int* __restrict__ list, const int* __restrict__ cnt,
                                                 const int* __restrict__ start, const int* __restrict__ vbase) {
@@ -634,6 +649,8 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
   const int n = blockIdx.y;
+  PROF_AT(8, __builtin_amdgcn_s_memrealtime());
+  PROF_T(0);
   const int GX = (P.TX + MR_WGT - 1) / MR_WGT;
   const int gx = blockIdx.x % GX, ty = blockIdx.x / GX;
   const int H = P.H, W = P.W;
@@ -661,8 +678,11 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
   }
   const int tincl = wave_incl_sum(tc);
   const int E = __builtin_amdgcn_readlane(tincl, MR_WGT - 1);
+  PROF_T(1);
   if (E == 0) {  // uniform over the workgroup
-    write_strip<MODE>(P, nullptr, n, x0, y0);
+    write_strip<MODE, CH>(P, nullptr, n, x0, y0);
+    PROF_T(6);
+    PROF_AT(9, __builtin_amdgcn_s_memrealtime());
     return;
   }
   const int texcl = tincl - tc;
@@ -673,6 +693,10 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
   PairStage& S = sm.ps[wave];
   S.mark[lane] = -1;
   __syncthreads();
+  PROF_T(2);
+#ifdef MR_PROF
+  int prof_passes = 0;
+#endif
 
   const float pad = P.bbox_pad, blur = P.blur;
   const bool persp = P.persp != 0, clipb = P.clipb != 0;
@@ -682,9 +706,9 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
   const bool fast_ok = !(blur > 0.0f);
 #endif
 #pragma unroll 1
-  for (int eb = wave * 64; eb < E; eb += MR_WGT * 64) {
-    // (1) one entry per lane
-    const int e = eb + lane;
+  for (int eb = 0; eb < E; eb += MR_WGT * 64) {
+    // (1) one entry per lane, interleaved over the 8 waves so every wave gets ~E/8 of them
+    const int e = eb + lane * MR_WGT + wave;
     int k = 0;
 #pragma unroll
     for (int kk = 1; kk < MR_WGT; ++kk) k += e >= __builtin_amdgcn_readlane(texcl, kk) ? 1 : 0;
@@ -720,6 +744,9 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
     S.meta[lane] = meta | pexcl;
 #pragma unroll 1
     for (int pb = 0; pb < NP; pb += 64) {
+#ifdef MR_PROF
+      ++prof_passes;
+#endif
       wave_lds_sync();
       // entry starting inside this pass marks its first slot; slot 0 belongs to the entry
       // straddling pb (the last non-empty entry starting at or before it)
@@ -752,7 +779,9 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
     }
     wave_lds_sync();  // the stage is rewritten by the next batch
   }
+  PROF_T(3);
   __syncthreads();
+  PROF_T(4);
 
   // (4) wave k finalises tile k of the strip
   const int ly = lane >> 3, lx = wave * MR_TS + (lane & 7);
@@ -779,8 +808,14 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
       }
     }
   }
+  PROF_T(5);
   __syncthreads();
-  write_strip<MODE>(P, &sm.out, n, x0, y0);
+  write_strip<MODE, CH>(P, &sm.out, n, x0, y0);
+  PROF_T(6);
+  PROF_AT(9, __builtin_amdgcn_s_memrealtime());
+#ifdef MR_PROF
+  PROF_AT(7, ((unsigned long long)E << 32) | (unsigned)prof_passes);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1151,6 +1186,13 @@ __global__ void __launch_bounds__(256) k_project_faces_bwd(const float* __restri
 extern "C" {
 
 const char* mr_last_error(void) { return g_err; }
+
+#ifdef MR_PROF
+// Debug-only (MR_PROF builds): device buffer of N*strips*8*16 u64 for k_raster phase stamps.
+int32_t mr_debug_set_prof(void* buf) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), &buf, sizeof(buf)) == hipSuccess ? MR_OK : MR_ELAUNCH;
+}
+#endif
 int32_t mr_version(void) { return 1; }
 
 static int check_settings(const mr_raster_settings_t* s) {
@@ -1237,7 +1279,7 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   P.view_count = count;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
-  MR_TIMED(KID_RASTER_FRAG, st, (k_raster<0><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
+  MR_TIMED(KID_RASTER_FRAG, st, (k_raster<0, 3><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
   MR_CHECK_LAUNCH("k_raster<0>");
   return MR_OK;
 }
@@ -1400,7 +1442,10 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.pcnt = w.pcnt;
   P.plist = w.plist;
   dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
-  MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
+  if (P.rgb_ch == 4)
+    MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1, 4><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
+  else
+    MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1, 3><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
   MR_CHECK_LAUNCH("k_raster<1>");
   return MR_OK;
 }

@@ -259,6 +259,7 @@ class RenderViews(torch.autograd.Function):
     @staticmethod
     def forward(ctx, verts, R, T, vcolors, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs):
         _require_cuda(verts, R, T, faces)
+        ctx.set_materialize_grads(False)  # unused outputs get no zero-filled (N,H,W) grads
         L = _lib.load()
         dev = verts.device
         v = verts.detach().float().contiguous()

@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import torch
 
-from .cameras import PerspectiveCameras, view_batch
+from .cameras import PerspectiveCameras, cached_camera_center, view_batch
 from .kernels import ShadeConfig, TextureArgs, render_views
 from .structures import Meshes, TexturesUV, TexturesVertex
 from .transforms import opencv_to_pytorch3d
@@ -47,11 +47,11 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
     n = max(len(meshes), R.reshape(-1, 3, 3).shape[0], T.reshape(-1, 3).shape[0])
     Rb, Tb, intr = view_batch(cameras, (H, W), R, T, n_views=n)
     if cam_center is None:
-        cam_center = cameras.get_camera_center().to(Rb.device)
+        cam_center = cached_camera_center(cameras, Rb.device)
     need_color = cfg.want_rgb
     if meshes.is_shared():
         tex, vcol = texture_args(meshes, need_color)
-        return render_views(meshes.shared_verts(), Rb, Tb, meshes.shared_faces(), intr.contiguous(), cam_center,
+        return render_views(meshes.shared_verts(), Rb, Tb, meshes.shared_faces(), intr, cam_center,
                             cfg, tex, vcolors=vcol)
     if len(meshes) != n:
         raise ValueError(f"Meshes batch ({len(meshes)}) and camera batch ({n}) differ")

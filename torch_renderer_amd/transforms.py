@@ -105,10 +105,20 @@ def opencv_look_at(centers, targets, up=(0.0, 1.0, 0.0)):
     return R.float(), t.float()
 
 
+_SIGN_CACHE: dict = {}
+
+
+def _col_sign(device, dtype):
+    key = (str(device), dtype)
+    s = _SIGN_CACHE.get(key)
+    if s is None:
+        s = _SIGN_CACHE[key] = torch.tensor([-1.0, -1.0, 1.0], dtype=dtype, device=device)
+    return s
+
+
 def opencv_to_pytorch3d(R: torch.Tensor, tvec: torch.Tensor):
-    """DifferentiableRenderer._camera_pose_from_opencv_to_pytorch (torch_renderer.py:73-80)."""
-    R_p = R.clone().permute(0, 2, 1)
-    T_p = tvec.clone()
-    R_p[:, :, :2] *= -1
-    T_p[:, :2] *= -1
-    return R_p, T_p
+    """DifferentiableRenderer._camera_pose_from_opencv_to_pytorch (torch_renderer.py:73-80):
+    R_p = R^T with columns 0 and 1 negated, T_p = tvec with entries 0 and 1 negated.
+    One multiply each (exact: x * -1), no in-place slice updates in the autograd graph."""
+    s = _col_sign(R.device, R.dtype)
+    return R.transpose(1, 2) * s, tvec * s.to(tvec.dtype)

@@ -70,10 +70,11 @@ def main():
     torch.cuda.synchronize()
     _lib.check(L.mr_debug_set_prof(None))
     p = buf.cpu().numpy().view(np.uint64).reshape(nwg, 8, 16).astype(np.float64)
+    p = p[p[:, 0, 0] > 0]  # strips k_raster visited (background strips are written by k_bg)
+    t0 = p[:, :, 0]
+    ne = p[:, 0, 2] > 0
     E = (p[:, 0, 7].astype(np.uint64) >> np.uint64(32)).astype(np.int64)
     passes = (p[:, :, 7].astype(np.uint64) & np.uint64(0xffffffff)).astype(np.int64)
-    t0 = p[:, :, 0]
-    ne = p[:, 0, 2] > 0  # non-empty workgroups reached phase 2
     dur = p[:, :, 6] - t0
     rt0, rt1 = p[:, 0, 8], p[:, 0, 9]
     span = (rt1.max() - rt0.min()) * 10e-3

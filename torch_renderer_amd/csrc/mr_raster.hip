@@ -59,11 +59,11 @@ static int set_err(int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_RASTER_FRAG, KID_RASTER_RENDER, KID_RASTER_BWD,
                 KID_RENDER_BWD, KID_RT_REDUCE, KID_VGRAD_A, KID_VGRAD_B, KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD,
-                KID_COUNT };
+                KID_BG, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_raster<0>", "k_raster<1>",
                                               "k_raster_bwd", "k_render_bwd", "k_rt_reduce", "k_vgrad_a",
                                               "k_vgrad_b", "k_vertex_normals", "k_project_faces",
-                                              "k_project_faces_bwd"};
+                                              "k_project_faces_bwd", "k_bg"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -104,6 +104,7 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // ---------------------------------------------------------------------------
 struct BinGeom {
   int TX, TY, T;
+  int GX, S;  // 64x8-pixel strips: GX per strip row, S = GX * TY per view
   int64_t list_cap;
 };
 static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
@@ -111,6 +112,8 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   g.TX = ceil_div(W, MR_TS);
   g.TY = ceil_div(H, MR_TS);
   g.T = g.TX * g.TY;
+  g.GX = ceil_div(g.TX, 8);
+  g.S = g.GX * g.TY;
   // Expected entries: ~(1 + 2*edge/8)^2 tiles per face + large faces; overflowing tiles take
   // the exact full-view path. max_faces_per_bin (if given) scales the reservation.
   int64_t cap = 6 * Ftot + 2 * N * (int64_t)g.T + 65536;
@@ -126,6 +129,9 @@ struct RasterWS {
   int* cur;    // (N*T)
   int* list;   // list_cap
   int* pcnt;   // (N) covered-pixel counts, zeroed per call (pcnt sits right after cnt)
+  int* wctr;   // (4) strips per work bucket [3] + the raster's work counter, zeroed with cnt
+  int* scount; // (N*S) entries per strip (0: background strip)
+  int* work;   // (3 * N*S) non-empty strip ids per bucket (heavy, medium, light)
   int* vtot;   // (N) per-view list entries
   int* vbase;  // (N+1) exclusive prefix of vtot
   int* plist;  // (N*H*W) covered pixel indices, view-major regions
@@ -139,7 +145,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(FaceRec) * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.cnt = (int*)(b + off);
   w.pcnt = w.cnt + (size_t)N * g.T;
-  off = align_up(off + sizeof(int) * ((size_t)N * g.T + (size_t)N), 256);
+  w.wctr = w.pcnt + N;
+  off = align_up(off + sizeof(int) * ((size_t)N * g.T + (size_t)N + 4), 256);
   w.start = (int*)(b + off);
   off = align_up(off + sizeof(int) * ((size_t)N * g.T + 1), 256);
   w.vtot = (int*)(b + off);
@@ -148,6 +155,10 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * ((size_t)N + 1), 256);
   w.cur = (int*)(b + off);
   off = align_up(off + sizeof(int) * (size_t)N * g.T, 256);
+  w.scount = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)N * g.S, 256);
+  w.work = (int*)(b + off);
+  off = align_up(off + sizeof(int) * 3 * (size_t)N * g.S, 256);
   w.list = (int*)(b + off);
   off = align_up(off + sizeof(int) * (size_t)g.list_cap, 256);
   w.plist = (int*)(b + off);
@@ -155,7 +166,7 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   w.bytes = off;
   return w;
 }
-static size_t zero_bytes(int64_t N, const BinGeom& g) { return sizeof(int) * ((size_t)N * g.T + (size_t)N); }
+static size_t zero_bytes(int64_t N, const BinGeom& g) { return sizeof(int) * ((size_t)N * g.T + (size_t)N + 4); }
 
 // ---------------------------------------------------------------------------
 // 1. binning: count -> scan -> fill
@@ -356,7 +367,9 @@ __global__ void __launch_bounds__(256) k_bin_fill_fv(SetupParams P, int64_t Ftot
 // Per-view exclusive scan of the T tile counts (one 1024-thread workgroup per view):
 // start[n*T+t] = cur[n*T+t] = offset inside view n's region; vtot[n] = entries of view n.
 __global__ void __launch_bounds__(1024) k_bin_scan_views(const int* __restrict__ cnt, int T, int* __restrict__ start,
-                                                         int* __restrict__ cur, int* __restrict__ vtot) {
+                                                         int* __restrict__ cur, int* __restrict__ vtot, int TX,
+                                                         int GX, int S, int64_t NS, int* __restrict__ scount,
+                                                         int* __restrict__ work, int* __restrict__ wctr) {
   __shared__ int part[1024];
   const int n = blockIdx.x;
   const int per = (T + 1023) / 1024;
@@ -389,6 +402,21 @@ __global__ void __launch_bounds__(1024) k_bin_scan_views(const int* __restrict__
     run += per <= 16 ? loc[i] : c[t];
   }
   if (threadIdx.x == 1023) vtot[n] = part[1023];
+  // Strip table: entries per 64x8 strip; non-empty strips go to one of three work buckets
+  // by size, so the persistent raster takes the heaviest strips first (shorter tail).
+  for (int sidx = threadIdx.x; sidx < S; sidx += 1024) {
+    const int ty = sidx / GX, gx = sidx - ty * GX;
+    int e = 0;
+    for (int k = 0; k < 8; ++k) {
+      const int tx = gx * 8 + k;
+      if (tx < TX) e += c[ty * TX + tx];
+    }
+    scount[(int64_t)n * S + sidx] = e;
+    if (e > 0) {
+      const int b = e >= 384 ? 0 : e >= 96 ? 1 : 2;
+      work[(int64_t)b * NS + atomicAdd(&wctr[b], 1)] = n * S + sidx;
+    }
+  }
 }
 
 // vbase = exclusive prefix of per-view totals (saturating at INT_MAX: tiles beyond the
@@ -622,7 +650,7 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROF_AT(i, v)                                                                                 \
   do {                                                                                                \
     if (g_prof && lane == 0)                                                                          \
-      g_prof[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * MR_WGT + wave) * 16 + (i)] = (v);      \
+      g_prof[((size_t)prof_slot * MR_WGT + wave) * 16 + (i)] = (v);                                 \
   } while (0)
 #define PROF_T(i) PROF_AT(i, __builtin_amdgcn_s_memtime())
 #else
@@ -630,29 +658,24 @@ __device__ unsigned long long* g_prof = nullptr;
 #define PROF_T(i) do {} while (0)
 #endif
 
-// One 512-thread workgroup = 8 waves = one 64x8-pixel strip (8 tiles of 8x8).
-//  (1) the strip's 8 tile lists are concatenated; each wave takes 64 entries at a time,
-//      one per lane, and clips the face's pixel bbox to its tile (<= 64 pixels);
+// One 512-thread workgroup = 8 waves rasterizes one 64x8-pixel strip (8 tiles of 8x8):
+//  (1) the strip's 8 tile lists are concatenated and dealt to the waves 64 entries at a
+//      time, one per lane; each lane clips its face's pixel bbox to its tile (<= 64 pixels);
 //  (2) a wave prefix sum over the rectangle sizes numbers the (face, pixel) pairs, and
 //      64 pairs per pass are evaluated exactly (frag_keep), one per lane — so a ~3-pixel
 //      face costs ~3 lanes, not a whole wave;
 //  (3) kept fragments meet in a per-pixel LDS atomicMin on the packed (z, face) key, which
 //      is order-independent and equals the CPU's "strictly nearer, earlier face wins";
 //  (4) wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
-// Strips with no entries skip (1)-(4) and write the background from registers.
 template <int MODE, int CH>
-__global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
-                                                const int* __restrict__ list, const int* __restrict__ cnt,
-                                                const int* __restrict__ start, const int* __restrict__ vbase) {
-  __shared__ RasterSmem sm;
+__device__ __attribute__((noinline)) void raster_strip(const RasterParams& P, RasterSmem& sm, const FaceRec* __restrict__ recs,
+                         const int* __restrict__ list, const int* __restrict__ cnt, const int* __restrict__ start,
+                         const int* __restrict__ vbase, int n, int gx, int ty, int prof_slot) {
   const int t = threadIdx.x;
   const int lane = t & 63;
   const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int n = blockIdx.y;
   PROF_AT(8, __builtin_amdgcn_s_memrealtime());
   PROF_T(0);
-  const int GX = (P.TX + MR_WGT - 1) / MR_WGT;
-  const int gx = blockIdx.x % GX, ty = blockIdx.x / GX;
   const int H = P.H, W = P.W;
   const int x0 = gx * MR_WGT * MR_TS, y0 = ty * MR_TS;
   const int64_t vb = vbase[n];
@@ -667,8 +690,9 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
       const int64_t bt = (int64_t)n * P.T + (int64_t)ty * P.TX + txl;
       const int c = cnt[bt];
       ts = start[bt];
-      // overflowed list: the tile's entries are every face of the view (bbox-filtered below)
-      if (vb + ts + c > P.list_cap) {
+      // overflowed list: the tile's entries are every face of the view (bbox-filtered below);
+      // counts are exact, so an empty tile stays empty
+      if (c > 0 && vb + ts + c > P.list_cap) {
         tovf = 1;
         tc = (int)(vcount < 0x7fffffffll ? vcount : 0x7fffffffll);
       } else {
@@ -679,10 +703,8 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
   const int tincl = wave_incl_sum(tc);
   const int E = __builtin_amdgcn_readlane(tincl, MR_WGT - 1);
   PROF_T(1);
-  if (E == 0) {  // uniform over the workgroup
+  if (E == 0) {  // uniform over the workgroup (work lists only hold non-empty strips)
     write_strip<MODE, CH>(P, nullptr, n, x0, y0);
-    PROF_T(6);
-    PROF_AT(9, __builtin_amdgcn_s_memrealtime());
     return;
   }
   const int texcl = tincl - tc;
@@ -816,6 +838,134 @@ __global__ void __launch_bounds__(512) k_raster(RasterParams P, const FaceRec* _
 #ifdef MR_PROF
   PROF_AT(7, ((unsigned long long)E << 32) | (unsigned)prof_passes);
 #endif
+}
+
+// Persistent raster: a grid sized to the resident capacity (CUs x workgroups per CU) pulls
+// non-empty strips from the three work buckets (heaviest first) through one atomic counter;
+// background strips never reach this kernel (k_bg writes them). Every workgroup leaves
+// when the counter passes the total, so the grid always drains.
+template <int MODE, int CH>
+__global__ void __launch_bounds__(512, 6) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
+                                                const int* __restrict__ list, const int* __restrict__ cnt,
+                                                const int* __restrict__ start, const int* __restrict__ vbase,
+                                                const int* __restrict__ work, int* __restrict__ wctr, int64_t NS,
+                                                int S, int GX) {
+  __shared__ RasterSmem sm;
+  __shared__ int s_item;
+  const int c0 = wctr[0], c1 = wctr[1], c2 = wctr[2];
+  const int total = c0 + c1 + c2;
+  for (;;) {
+    if (threadIdx.x == 0) s_item = atomicAdd(&wctr[3], 1);
+    __syncthreads();  // also orders the previous strip's LDS reads before this strip's writes
+    const int item = s_item;
+    if (item >= total) break;
+    const int sid = item < c0 ? work[item] : item < c0 + c1 ? work[NS + (item - c0)] : work[2 * NS + (item - c0 - c1)];
+    const int n = sid / S, r = sid - n * S;
+    const int ty = r / GX, gx = r - ty * GX;
+    raster_strip<MODE, CH>(P, sm, recs, list, cnt, start, vbase, n, gx, ty, sid);
+  }
+}
+
+// Background for every strip without entries: streaming vector stores, one workgroup per
+// strip row (8 image rows) of one view; strips holding faces are skipped (k_raster writes them).
+template <int MODE, int CH>
+__global__ void __launch_bounds__(256) k_bg(RasterParams P, const int* __restrict__ scount, int S, int GX) {
+  const int n = blockIdx.y, ty = blockIdx.x;
+  float bgd = -1.0f, bgs = -1.0f, bgv[4] = {-1.0f, -1.0f, -1.0f, -1.0f};
+  if (MODE == 1) {
+    PixGeom G;
+    ShadeOut o;
+    ShadeCache C;
+    shade_fwd(P.S, n, false, G, 0.f, 0.f, 0.f, 0.f, 0.f, o, C);
+    bgd = o.depth;
+    bgs = o.sil;
+    bgv[0] = o.rgb[0]; bgv[1] = o.rgb[1]; bgv[2] = o.rgb[2]; bgv[3] = o.alpha;
+  }
+  const int* sc = scount + (int64_t)n * S + (int64_t)ty * GX;
+  const int W = P.W, H = P.H;
+  const bool vec = (W & 3) == 0;
+  const int W4 = (W + 3) >> 2;
+  const bool rgb = MODE == 1 && (P.out_flags & MR_OUT_RGB);
+  for (int rr = threadIdx.x >> 7; rr < MR_TS; rr += 2) {
+    const int y = ty * MR_TS + rr;
+    if (y >= H) break;
+    for (int x4 = threadIdx.x & 127; x4 < W4; x4 += 128) {
+      if (sc[x4 >> 4] != 0) continue;  // 16 groups of 4 pixels per 64-pixel strip
+      const int x = x4 * 4;
+      const int64_t pix = ((int64_t)n * H + y) * W + x;
+      if (vec) {
+        if (MODE == 0) {
+          longlong2* q = (longlong2*)(P.p2f + pix);
+          q[0] = make_longlong2(-1ll, -1ll);
+          q[1] = make_longlong2(-1ll, -1ll);
+          const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+          *(float4*)(P.zbuf + pix) = m1;
+          *(float4*)(P.dists + pix) = m1;
+          float4* b = (float4*)(P.bary + pix * 3);
+          b[0] = m1; b[1] = m1; b[2] = m1;
+        } else {
+          if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = make_float4(bgd, bgd, bgd, bgd);
+          if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = make_float4(bgs, bgs, bgs, bgs);
+          *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
+          if (rgb) {
+            float4* c = (float4*)(P.rgb + pix * CH);
+            if (CH == 4) {
+              const float4 v = make_float4(bgv[0], bgv[1], bgv[2], bgv[3]);
+              c[0] = v; c[1] = v; c[2] = v; c[3] = v;
+            } else {
+              c[0] = make_float4(bgv[0], bgv[1], bgv[2], bgv[0]);
+              c[1] = make_float4(bgv[1], bgv[2], bgv[0], bgv[1]);
+              c[2] = make_float4(bgv[2], bgv[0], bgv[1], bgv[2]);
+            }
+          }
+        }
+      } else {
+        for (int k = 0; k < 4 && x + k < W; ++k) {
+          const int64_t q = pix + k;
+          if (MODE == 0) {
+            P.p2f[q] = -1ll;
+            P.zbuf[q] = -1.0f;
+            P.dists[q] = -1.0f;
+            for (int c = 0; c < 3; ++c) P.bary[q * 3 + c] = -1.0f;
+          } else {
+            if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = bgd;
+            if (P.out_flags & MR_OUT_SIL) P.sil[q] = bgs;
+            P.p2f32[q] = -1;
+            if (rgb)
+              for (int c = 0; c < CH; ++c) P.rgb[q * CH + c] = bgv[c];
+          }
+        }
+      }
+    }
+  }
+}
+
+// Resident workgroups of k_raster<MODE,CH> on the current device (persistent grid size).
+template <int MODE, int CH>
+static int raster_grid(int64_t strips_total) {
+  static int cached = 0;
+  if (!cached) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_raster<MODE, CH>, 512, 0) != hipSuccess || per <= 0)
+      per = 2;
+    cached = cus * per;
+  }
+  return (int)(strips_total < cached ? (strips_total > 0 ? strips_total : 1) : cached);
+}
+
+template <int MODE, int CH>
+static int launch_raster(const RasterParams& P, const RasterWS& w, const BinGeom& g, int64_t N, int kid,
+                         hipStream_t st) {
+  dim3 bgrid((unsigned)g.TY, (unsigned)N);
+  MR_TIMED(KID_BG, st, (k_bg<MODE, CH><<<bgrid, 256, 0, st>>>(P, w.scount, g.S, g.GX)));
+  MR_CHECK_LAUNCH("k_bg");
+  const int grid = raster_grid<MODE, CH>(N * g.S);
+  MR_TIMED(kid, st, (k_raster<MODE, CH><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase, w.work,
+                                                                w.wctr, N * g.S, g.S, g.GX)));
+  MR_CHECK_LAUNCH("k_raster");
+  return MR_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -1242,7 +1392,8 @@ static RasterParams make_raster(const mr_raster_settings_t* s, const BinGeom& g,
 }
 
 static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, hipStream_t st) {
-  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_views<<<(unsigned)N, 1024, 0, st>>>(w.cnt, g.T, w.start, w.cur, w.vtot)));
+  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_views<<<(unsigned)N, 1024, 0, st>>>(w.cnt, g.T, w.start, w.cur, w.vtot, g.TX, g.GX, g.S,
+                                                                   N * g.S, w.scount, w.work, w.wctr)));
   MR_CHECK_LAUNCH("k_bin_scan_views");
   MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_base<<<1, 64, 0, st>>>(w.vtot, (int)N, w.vbase)));
   MR_CHECK_LAUNCH("k_bin_scan_base");
@@ -1278,9 +1429,7 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   P.view_first = first;
   P.view_count = count;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
-  dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
-  MR_TIMED(KID_RASTER_FRAG, st, (k_raster<0, 3><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
-  MR_CHECK_LAUNCH("k_raster<0>");
+  if ((rc = launch_raster<0, 3>(P, w, g, N, KID_RASTER_FRAG, st))) return rc;
   return MR_OK;
 }
 
@@ -1441,12 +1590,9 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.p2f32 = p2f32;
   P.pcnt = w.pcnt;
   P.plist = w.plist;
-  dim3 grid(ceil_div(g.TX, MR_WGT) * g.TY, (unsigned)N);
-  if (P.rgb_ch == 4)
-    MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1, 4><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
-  else
-    MR_TIMED(KID_RASTER_RENDER, st, (k_raster<1, 3><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase)));
-  MR_CHECK_LAUNCH("k_raster<1>");
+  if (P.rgb_ch == 4) rc = launch_raster<1, 4>(P, w, g, N, KID_RASTER_RENDER, st);
+  else rc = launch_raster<1, 3>(P, w, g, N, KID_RASTER_RENDER, st);
+  if (rc) return rc;
   return MR_OK;
 }
 

@@ -85,15 +85,16 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
                       f"torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
 
 
-# Algorithmic bytes per launch (DESIGN.md "Measurement") for each kernel that may dominate.
-def algorithmic_bytes(kernel, H, W, F, views):
+# Algorithmic bytes per launch for each kernel that may dominate. `covered` =
+# covered pixels of the launch's batch (measured once, outside the timed region).
+def algorithmic_bytes(kernel, H, W, F, views, covered):
     HW = H * W
-    if kernel == "k_raster<0>":          # modular fragment pass: p2f i64 + zbuf + bary + dists = 28 B/px, 36 B/face
-        return (28 * HW + 36 * F) * views
-    if kernel == "k_raster<1>":          # fused pass: depth + sil + rgb (3 ch) + p2f i32 = 24 B/px, 36 B/face
-        return (24 * HW + 36 * F) * views
-    if kernel == "k_render_bwd":         # read upstream grads 20 B/px + p2f 4 B/px, 72 B/face (read + grad write)
-        return (24 * HW + 72 * F) * views
+    if kernel == "k_resolve<1>":    # fused output stream: depth + sil + rgb (3 ch) = 20 B/px
+        return 20 * HW * views
+    if kernel == "k_resolve<0>":    # PyTorch3D fragments: p2f i64 + zbuf + bary + dists = 28 B/px
+        return 28 * HW * views
+    if kernel == "k_render_bwd":    # per covered pixel: upstream grads 20 B + list entry 8 B; face rows 72 B
+        return 28 * covered + 72 * F
     return None
 
 
@@ -159,6 +160,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    with torch.no_grad():  # covered pixels of this rank's batch (roofline bytes of the backward)
+        covered = int((renderer.render(bmesh, R_cv, t_cv)[0] > 0).sum().item())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -189,7 +192,7 @@ def main():
     if dom is not None:
         name, (launches, total_ms) = dom
         avg_s = total_ms / launches / 1e3
-        b = algorithmic_bytes(name, H, W, Fn, nv)
+        b = algorithmic_bytes(name, H, W, Fn, nv, covered)
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         if os.path.exists(pmc_path):

@@ -122,7 +122,8 @@ int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, i
 /* ---------------- fused render (one raster pass -> depth, silhouette, rgb) ---------------- */
 size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
 /* Outputs (each optional per out_flags): depth (N,H,W), silhouette (N,H,W), rgb (N,H,W,C);
- * pix_to_face32 (N,H,W) int32 packed face id n*F+f or -1 (kept for the backward).
+ * pix_to_face32 (N,H,W) int32 packed face id n*F+f or -1 — optional (NULL: not written; the
+ * backward does not need it: the workspace keeps a compact list of covered pixels).
  * cam_centers (Nc,3) world-space specular camera centres, Nc in {1, N}. */
 int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t N, const float* cam_centers,
                           int64_t num_cam_centers, const mr_raster_settings_t* rs, const mr_shade_params_t* sp,
@@ -130,11 +131,12 @@ int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t
                           size_t workspace_bytes, void* stream);
 /* Backward from upstream grads (each may be NULL when not requested in out_flags).
  * Writes grad_verts (V,3), grad_views (N,12), grad_vcolors (V,3; tex_kind 1 only, may be NULL).
- * `workspace` must be the one passed to the matching mr_render_forward (face records reused). */
+ * `fwd_workspace` must be the one passed to the matching mr_render_forward: its face records and
+ * covered-pixel list are reused (nothing is re-rasterized). */
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W);
 int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, const mr_view_t* views, int64_t N,
                            const float* cam_centers, int64_t num_cam_centers, const mr_raster_settings_t* rs,
-                           const mr_shade_params_t* sp, const int32_t* pix_to_face32, const float* grad_depth,
+                           const mr_shade_params_t* sp, const float* grad_depth,
                            const float* grad_silhouette, const float* grad_rgb, const void* fwd_workspace,
                            void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts, float* grad_views,
                            float* grad_vcolors, void* stream);

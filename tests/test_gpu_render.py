@@ -49,7 +49,7 @@ def _run(name, H, W, N, texture, light_kind=0, persp=True, seed=1, bg=(1.0, 1.0,
     loss = (ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()
     loss.backward()
     # GPU
-    cfg = Kn.ShadeConfig(H=H, W=W, persp=persp, light_kind=light_kind, background=bg)
+    cfg = Kn.ShadeConfig(H=H, W=W, persp=persp, light_kind=light_kind, background=bg, want_p2f=True)
     if light_kind == 1:
         cfg.light_ambient = (1.0, 1.0, 1.0)
     vg = verts.to(DEV).requires_grad_(True)

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 TAG=${1:-r1}
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_${TAG}.log 2>&1 || { echo "PYTEST FAILED"; tail -40 gpurun_out/pytest_${TAG}.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_${TAG}.log 2>&1 || { echo "PYTEST FAILED"; tail -40 gpurun_out/pytest_${TAG}.log; exit 1; }
 tail -3 gpurun_out/pytest_${TAG}.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_${TAG}.log 2>&1 || { echo "SMOKE FAILED"; tail -30 gpurun_out/smoke_${TAG}.log; exit 1; }
 cat gpurun_out/smoke_${TAG}.log | tail -2

@@ -37,7 +37,7 @@ def main():
     first = torch.arange(a.views, device=dev) * Fn
     count = torch.full((a.views,), Fn, device=dev)
     tex, vcol = texture_args(m, True)
-    cfg = Kn.ShadeConfig(H=H, W=W)
+    cfg = Kn.ShadeConfig(H=H, W=W, want_p2f=True)
     vg = v.clone().requires_grad_(True)
     gD = torch.rand(a.views, H, W, device=dev)
     gS = torch.rand(a.views, H, W, device=dev)

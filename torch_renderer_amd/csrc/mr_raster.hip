@@ -1,29 +1,30 @@
 // mi355r — MI355X (gfx950, CDNA4) rasterizer kernels + C ABI.
 //
-// Pipeline for a batch of N views (one launch each, all async on one stream):
-//   1. k_setup_*   : one thread per (view, face): project (or read face_verts),
-//                    build a 64-B FaceRec, and append the face id to every
-//                    32x32-pixel super-tile its (conservative) bbox touches
-//                    (global atomics on per-tile counters; order irrelevant).
-//   2. k_raster<M> : one 256-thread workgroup per (super-tile, view). Face
-//                    records of the tile's list are staged in LDS in chunks of
-//                    256; each wave owns a 16x16 region = 4 sub-tiles of 8x8
-//                    (lane = pixel). Per face: wave-uniform sub-tile bbox test,
-//                    then the exact per-pixel test (cheap edge-sign reject,
-//                    then the CPU-identical barycentric/depth evaluation).
-//                    K=1 keeps the lexicographic (z, face) minimum == the CPU
-//                    tie-break, so the result is independent of list order.
-//                    Epilogue: M=0 writes PyTorch3D Fragments; M=1 shades
-//                    (depth relu, sigmoid silhouette, Phong + softmax blend)
-//                    and writes only the requested images + int32 face ids.
-//   3. backward    : k_render_bwd / k_raster_bwd — one workgroup per
-//                    (super-tile, view); per covered pixel the forward is
-//                    recomputed, the analytic backward produces per-face
-//                    gradient rows that are pre-reduced in an LDS hash table
-//                    (ds_add_f32) and flushed with one global atomic per
-//                    (workgroup, face, component); per-view R/T gradients are
-//                    reduced in-workgroup and written without atomics.
-//   4. vertex kernels gather per-face rows through a CSR vertex adjacency
+// Pipeline for a batch of N views (all launches async on one stream, no host sync):
+//   1. binning     : k_bin_count (thread per (view, face): project or read face_verts,
+//                    write a 64-B FaceRec, count the 8x8 tiles its padded bbox touches
+//                    through an LDS histogram) -> k_bin_scan (one workgroup per view:
+//                    entry offsets per tile, compact slot per non-empty tile, and work
+//                    UNITS of <= 64 (tile, face) entries) -> k_bin_fill (tile lists).
+//   2. k_tile_raster: persistent grid of independent waves, one unit per wave: each lane
+//                    clips one face's pixel bbox to the tile, the wave expands the
+//                    (face, pixel) pairs 64 at a time (DPP prefix sums), evaluates each
+//                    pair exactly and keeps the per-pixel minimum of the packed (z, face)
+//                    key with ds_min_u64; the tile's 64 keys go to a compact slot buffer
+//                    (a plain store, or a global u64 atomicMin when a tile has > 1 unit).
+//                    The minimum equals the CPU's "strictly nearer, earlier face wins".
+//   3. k_resolve<M>: streaming pass over EVERY pixel, 4 per thread: background pixels
+//                    are written with 16-B vector stores; pixels of non-empty tiles read
+//                    their key, recompute the winning fragment exactly and write M=0
+//                    PyTorch3D Fragments or M=1 shaded depth/silhouette/rgb (+ a compact
+//                    list of covered (pixel, face) pairs for the backward).
+//   4. backward    : k_render_bwd — waves over the covered-pixel list; per pixel the
+//                    fragment and shading are recomputed and differentiated; per-face
+//                    gradient rows are summed over runs of equal faces inside the wave
+//                    (segmented shuffles) and scattered with one float atomic per run
+//                    and component; per-view R/T gradients are wave-reduced.
+//                    k_raster_bwd is the modular _C.rasterize_meshes_backward.
+//   5. vertex kernels gather per-face rows through a CSR vertex adjacency
 //      (deterministic order) and chain the vertex-normal backward.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -57,13 +58,16 @@ static int set_err(int code, const char* fmt, ...) {
 // Optional per-kernel timing: HIP events recorded on the launch stream around
 // every kernel while enabled (bench.py reads them to price the dominant kernel).
 // ---------------------------------------------------------------------------
-enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_RASTER_FRAG, KID_RASTER_RENDER, KID_RASTER_BWD,
-                KID_RENDER_BWD, KID_RT_REDUCE, KID_VGRAD_A, KID_VGRAD_B, KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD,
-                KID_BG, KID_COUNT };
-static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_raster<0>", "k_raster<1>",
-                                              "k_raster_bwd", "k_render_bwd", "k_rt_reduce", "k_vgrad_a",
-                                              "k_vgrad_b", "k_vertex_normals", "k_project_faces",
-                                              "k_project_faces_bwd", "k_bg"};
+enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_FILL_FRAG, KID_FILL_RENDER,
+                KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
+                KID_VGRAD_A, KID_VGRAD_B,
+                KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_COUNT };
+static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
+                                              "k_fill_bg<0>", "k_fill_bg<1>", "k_shade<0>", "k_shade<1>",
+                                              "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
+                                              "k_vgrad_a", "k_vgrad_b",
+                                              "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
+                                              "k_shade_rec"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -95,78 +99,103 @@ static void timing_end(int i, int kid, hipStream_t st) {
     timing_end(_ti, kid, st);                  \
   } while (0)
 
+// Debug-only phase stamps (build with -DMR_PROF; tools/phase_stamps.py): per wave 8 u64
+// slots of s_memtime at phase boundaries, indexed by the wave's global id.
+#ifdef MR_PROF
+__device__ unsigned long long* g_prof = nullptr;
+#define PROF_T(gw, i)                                                                    \
+  do {                                                                                   \
+    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(size_t)(gw) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define PROF_T(gw, i) do {} while (0)
+#endif
+
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------------------
 // Workspace: face records, per-(view, 8x8 tile) face lists (count -> scan ->
-// fill), and the compact per-view list of covered pixels (fused path).
+// fill), work units, compact per-tile depth keys, and (fused path) the compact
+// per-view list of covered (pixel, face) pairs.
 // ---------------------------------------------------------------------------
+#define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COUNT = 4 };
+
 struct BinGeom {
   int TX, TY, T;
-  int GX, S;  // 64x8-pixel strips: GX per strip row, S = GX * TY per view
   int64_t list_cap;
+  int64_t unit_cap;  // >= units the scan can emit: one per non-empty tile + list_cap / MR_UE
 };
 static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   BinGeom g;
   g.TX = ceil_div(W, MR_TS);
   g.TY = ceil_div(H, MR_TS);
   g.T = g.TX * g.TY;
-  g.GX = ceil_div(g.TX, 8);
-  g.S = g.GX * g.TY;
-  // Expected entries: ~(1 + 2*edge/8)^2 tiles per face + large faces; overflowing tiles take
-  // the exact full-view path. max_faces_per_bin (if given) scales the reservation.
+  // Expected entries: ~(1 + 2*edge/8)^2 tiles per face + large faces; tiles whose list would
+  // overflow take the exact full-view path (one unit scanning every face of the view).
+  // max_faces_per_bin (if given) scales the reservation.
   int64_t cap = 6 * Ftot + 2 * N * (int64_t)g.T + 65536;
   if (mfpb > 0) cap = (int64_t)mfpb * N * 16 + 65536;
   g.list_cap = cap;
+  g.unit_cap = N * (int64_t)g.T + cap / MR_UE + 1;
   return g;
 }
 
 struct RasterWS {
   FaceRec* recs;
-  int* cnt;    // (N*T) zeroed per call
-  int* start;  // (N*T + 1)
-  int* cur;    // (N*T)
+  int* cnt;    // (N*T) entries per tile; zeroed per call together with pcnt, vtot, ctr
+  int* pcnt;   // (N) covered pixels per view (fused path)
+  int* vtot;   // (N) list entries per view
+  int* ctr;    // (CTR_COUNT) units / slots emitted by the scan
+  int* start;  // (N*T) entry offset of each tile inside its view's region
+  int* cur;    // (N*T) fill cursors
+  int* vbase;  // (N) first list entry of each view (saturating)
+  int* tdone;  // (N*T) per slot: units of a shared slot still to finish (count-down; the last appends)
+  int4* units; // (unit_cap) {view*T + tile, first list entry (-1: every face of the view), entries, slot | multi<<31}
   int* list;   // list_cap
-  int* pcnt;   // (N) covered-pixel counts, zeroed per call (pcnt sits right after cnt)
-  int* wctr;   // (4) strips per work bucket [3] + the raster's work counter, zeroed with cnt
-  int* scount; // (N*S) entries per strip (0: background strip)
-  int* work;   // (3 * N*S) non-empty strip ids per bucket (heavy, medium, light)
-  int* vtot;   // (N) per-view list entries
-  int* vbase;  // (N+1) exclusive prefix of vtot
-  int* plist;  // (N*H*W) covered pixel indices, view-major regions
+  unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
+  int2* plist; // (N*H*W) covered (pixel, face record) pairs, view-major regions
+  ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
   size_t bytes;
 };
-static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g, bool pixlist) {
+static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
+                                int64_t Fshade = 0) {
   RasterWS w;
   size_t off = 0;
   char* b = (char*)base;
+  const size_t NT = (size_t)N * g.T;
   w.recs = (FaceRec*)(b + off);
   off = align_up(off + sizeof(FaceRec) * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.cnt = (int*)(b + off);
-  w.pcnt = w.cnt + (size_t)N * g.T;
-  w.wctr = w.pcnt + N;
-  off = align_up(off + sizeof(int) * ((size_t)N * g.T + (size_t)N + 4), 256);
+  w.pcnt = w.cnt + NT;
+  w.vtot = w.pcnt + N;
+  w.ctr = w.vtot + N;
+  off = align_up(off + sizeof(int) * (NT + 2 * (size_t)N + CTR_COUNT), 256);
   w.start = (int*)(b + off);
-  off = align_up(off + sizeof(int) * ((size_t)N * g.T + 1), 256);
-  w.vtot = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)N, 256);
-  w.vbase = (int*)(b + off);
-  off = align_up(off + sizeof(int) * ((size_t)N + 1), 256);
+  off = align_up(off + sizeof(int) * NT, 256);
   w.cur = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)N * g.T, 256);
-  w.scount = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)N * g.S, 256);
-  w.work = (int*)(b + off);
-  off = align_up(off + sizeof(int) * 3 * (size_t)N * g.S, 256);
+  off = align_up(off + sizeof(int) * NT, 256);
+  w.vbase = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)N, 256);
+  w.tdone = (int*)(b + off);
+  off = align_up(off + sizeof(int) * NT, 256);
+  w.units = (int4*)(b + off);
+  off = align_up(off + sizeof(int4) * (size_t)g.unit_cap, 256);
   w.list = (int*)(b + off);
   off = align_up(off + sizeof(int) * (size_t)g.list_cap, 256);
-  w.plist = (int*)(b + off);
-  if (pixlist) off = align_up(off + sizeof(int) * (size_t)N * H * W, 256);
+  w.tkey = (unsigned long long*)(b + off);
+  off = align_up(off + sizeof(unsigned long long) * 64 * NT, 256);
+  w.plist = (int2*)(b + off);
+  off = align_up(off + sizeof(int2) * (size_t)N * H * W, 256);
+  w.srec = (ShadeRec*)(b + off);
+  off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
   w.bytes = off;
   return w;
 }
-static size_t zero_bytes(int64_t N, const BinGeom& g) { return sizeof(int) * ((size_t)N * g.T + (size_t)N + 4); }
+static size_t zero_bytes(int64_t N, const BinGeom& g) {
+  return sizeof(int) * ((size_t)N * g.T + 2 * (size_t)N + CTR_COUNT);
+}
 
 // ---------------------------------------------------------------------------
 // 1. binning: count -> scan -> fill
@@ -180,8 +209,59 @@ struct SetupParams {
   int* cnt;
   int* cur;
   int* list;
+  int* vtot;
   const int* vbase;
 };
+
+// Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP). Full EXEC required.
+MR_DEV int wave_incl_sum(int v) {
+#ifdef MR_DBG_SHFL
+  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v += u; }
+  return v;
+#endif
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+MR_DEV int wave_incl_max(int v) {
+#ifdef MR_DBG_SHFL
+  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v = max(v, u); }
+  return v;
+#endif
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+MR_DEV int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
+
+// Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
+MR_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Inclusive scan over a 1024-thread workgroup (16 waves): DPP inside each wave, then the
+// 16 wave totals scanned by every wave from LDS. `tot` = workgroup total. Uniform call only.
+MR_DEV int block_incl_sum(int v, int* part16, int& tot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int w = wave_incl_sum(v);
+  if (lane == 63) part16[wave] = w;
+  __syncthreads();
+  const int ws = wave_incl_sum(lane < 16 ? part16[lane] : 0);
+  tot = __builtin_amdgcn_readlane(ws, 15);
+  const int before = __shfl(ws, wave > 0 ? wave - 1 : 0, 64);
+  __syncthreads();  // part16 is reused by the next call
+  return w + (wave > 0 ? before : 0);
+}
 
 // Inverse of col_ndc/row_ndc (approximate, widened by 0.05 px; the raster
 // kernel repeats the exact per-pixel bbox test, so a superset is all we need).
@@ -249,7 +329,8 @@ MR_DEV void world_face_verts(const float* __restrict__ verts, const int32_t* __r
 }
 
 // World mode (one mesh shared by N views, rec = n*F + f): project, write the record,
-// count tile overlaps through an LDS histogram, flush one global atomic per touched tile.
+// count tile overlaps through an LDS histogram, flush one global atomic per touched tile
+// and one per wave into the view's entry total.
 template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const float* __restrict__ verts,
                                                          const int32_t* __restrict__ faces, int64_t F,
@@ -261,6 +342,7 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
     __syncthreads();
   }
   const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int mine = 0;
   if (f < F) {
     const ViewRec V = views[n];
     float v[3][3];
@@ -268,14 +350,18 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
     const FaceRec r = make_rec(P, (uint32_t)f, v);
     P.recs[(int64_t)n * F + f] = r;
     int tx0, tx1, ty0, ty1;
-    if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
+    if (rec_tiles(P, r, tx0, tx1, ty0, ty1)) {
+      mine = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
       for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) {
           const int t = ty * P.TX + tx;
           if (LDS) atomicAdd(&hist[t], 1);
           else atomicAdd(&P.cnt[(int64_t)n * P.T + t], 1);
         }
+    }
   }
+  const int tot = wave_sum(mine);
+  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&P.vtot[n], tot);
   if (LDS) {
     __syncthreads();
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
@@ -332,132 +418,202 @@ MR_DEV int mesh_of_face(const int64_t* __restrict__ first, int64_t N, int64_t f)
   return (int)lo;
 }
 
-// face_verts mode (PyTorch3D _C boundary): rec = packed face id; global atomics.
+// face_verts mode (PyTorch3D _C boundary): rec = packed face id. A workgroup whose 256
+// faces all belong to one mesh counts through an LDS histogram (the common case: meshes
+// are contiguous runs of faces); otherwise global atomics.
+template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot,
                                                       const int64_t* __restrict__ first, int64_t N) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= Ftot) return;
-  const int n = mesh_of_face(first, N, f);
-  float v[3][3];
-  for (int c = 0; c < 3; ++c)
-    for (int k = 0; k < 3; ++k) v[c][k] = fv[9 * f + 3 * c + k];
-  const FaceRec r = make_rec(P, (uint32_t)f, v);
-  P.recs[f] = r;
-  int tx0, tx1, ty0, ty1;
-  if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
-    for (int ty = ty0; ty <= ty1; ++ty)
-      for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&P.cnt[(int64_t)n * P.T + ty * P.TX + tx], 1);
+  extern __shared__ __attribute__((aligned(16))) int hist[];
+  const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t f = f0 + threadIdx.x;
+  const int64_t fl = f0 + blockDim.x - 1 < Ftot ? f0 + blockDim.x - 1 : Ftot - 1;
+  const int n0 = mesh_of_face(first, N, f0), n1 = mesh_of_face(first, N, fl);
+  const bool lds = LDS && n0 == n1;  // uniform over the workgroup
+  if (lds) {
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+  }
+  int mine = 0;
+  int n = n0;
+  if (f < Ftot) {
+    n = lds ? n0 : mesh_of_face(first, N, f);
+    float v[3][3];
+    for (int c = 0; c < 3; ++c)
+      for (int k = 0; k < 3; ++k) v[c][k] = fv[9 * f + 3 * c + k];
+    const FaceRec r = make_rec(P, (uint32_t)f, v);
+    P.recs[f] = r;
+    int tx0, tx1, ty0, ty1;
+    if (rec_tiles(P, r, tx0, tx1, ty0, ty1)) {
+      mine = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+          if (lds) atomicAdd(&hist[ty * P.TX + tx], 1);
+          else atomicAdd(&P.cnt[(int64_t)n * P.T + ty * P.TX + tx], 1);
+        }
+    }
+  }
+  if (lds) {
+    const int tot = wave_sum(mine);
+    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&P.vtot[n0], tot);
+    __syncthreads();
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
+      if (hist[i]) atomicAdd(&P.cnt[(int64_t)n0 * P.T + i], hist[i]);
+  } else if (mine) {
+    atomicAdd(&P.vtot[n], mine);
+  }
 }
 
+template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_fill_fv(SetupParams P, int64_t Ftot, const int64_t* __restrict__ first,
                                                      int64_t N) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f >= Ftot) return;
-  const int n = mesh_of_face(first, N, f);
-  const FaceRec r = P.recs[f];
-  int tx0, tx1, ty0, ty1;
-  if (rec_tiles(P, r, tx0, tx1, ty0, ty1))
+  extern __shared__ __attribute__((aligned(16))) int hist[];
+  const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
+  const int64_t f = f0 + threadIdx.x;
+  const int64_t fl = f0 + blockDim.x - 1 < Ftot ? f0 + blockDim.x - 1 : Ftot - 1;
+  const int n0 = mesh_of_face(first, N, f0), n1 = mesh_of_face(first, N, fl);
+  const bool lds = LDS && n0 == n1;
+  FaceRec r;
+  int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
+  bool ok = false;
+  if (f < Ftot) {
+    r = P.recs[f];
+    ok = rec_tiles(P, r, tx0, tx1, ty0, ty1);
+  }
+  if (lds) {
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
+    __syncthreads();
+    if (ok)
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+    __syncthreads();
+    const int vb = P.vbase[n0];
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
+      if (hist[i]) hist[i] = vb + atomicAdd(&P.cur[(int64_t)n0 * P.T + i], hist[i]);  // reserve a block
+    __syncthreads();
+    if (ok)
+      for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+          const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
+          if (pos < P.list_cap) P.list[pos] = (int)f;
+        }
+  } else if (ok) {
+    const int n = mesh_of_face(first, N, f);
     for (int ty = ty0; ty <= ty1; ++ty)
       for (int tx = tx0; tx <= tx1; ++tx) {
         const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
         if (pos < P.list_cap) P.list[pos] = (int)f;
       }
-}
-
-// Per-view exclusive scan of the T tile counts (one 1024-thread workgroup per view):
-// start[n*T+t] = cur[n*T+t] = offset inside view n's region; vtot[n] = entries of view n.
-__global__ void __launch_bounds__(1024) k_bin_scan_views(const int* __restrict__ cnt, int T, int* __restrict__ start,
-                                                         int* __restrict__ cur, int* __restrict__ vtot, int TX,
-                                                         int GX, int S, int64_t NS, int* __restrict__ scount,
-                                                         int* __restrict__ work, int* __restrict__ wctr) {
-  __shared__ int part[1024];
-  const int n = blockIdx.x;
-  const int per = (T + 1023) / 1024;
-  const int b0 = threadIdx.x * per;
-  const int* c = cnt + (int64_t)n * T;
-  int loc[16];
-  int s = 0;
-  if (per <= 16) {
-    for (int i = 0; i < per; ++i) {
-      loc[i] = b0 + i < T ? c[b0 + i] : 0;
-      s += loc[i];
-    }
-  } else {
-    for (int i = b0; i < b0 + per && i < T; ++i) s += c[i];
-  }
-  part[threadIdx.x] = s;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    const int v = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  int run = part[threadIdx.x] - s;
-  for (int i = 0; i < per; ++i) {
-    const int t = b0 + i;
-    if (t >= T) break;
-    start[(int64_t)n * T + t] = run;
-    cur[(int64_t)n * T + t] = run;
-    run += per <= 16 ? loc[i] : c[t];
-  }
-  if (threadIdx.x == 1023) vtot[n] = part[1023];
-  // Strip table: entries per 64x8 strip; non-empty strips go to one of three work buckets
-  // by size, so the persistent raster takes the heaviest strips first (shorter tail).
-  for (int sidx = threadIdx.x; sidx < S; sidx += 1024) {
-    const int ty = sidx / GX, gx = sidx - ty * GX;
-    int e = 0;
-    for (int k = 0; k < 8; ++k) {
-      const int tx = gx * 8 + k;
-      if (tx < TX) e += c[ty * TX + tx];
-    }
-    scount[(int64_t)n * S + sidx] = e;
-    if (e > 0) {
-      const int b = e >= 384 ? 0 : e >= 96 ? 1 : 2;
-      work[(int64_t)b * NS + atomicAdd(&wctr[b], 1)] = n * S + sidx;
-    }
   }
 }
 
-// vbase = exclusive prefix of per-view totals (saturating at INT_MAX: tiles beyond the
-// list capacity take the exact overflow path).
-__global__ void __launch_bounds__(64) k_bin_scan_base(const int* __restrict__ vtot, int N, int* __restrict__ vbase) {
-  if (threadIdx.x != 0) return;
-  long long run = 0;
-  for (int n = 0; n < N; ++n) {
-    vbase[n] = (int)(run < 0x7fffffffll ? run : 0x7fffffffll);
-    run += vtot[n];
-  }
-  vbase[N] = (int)(run < 0x7fffffffll ? run : 0x7fffffffll);
-}
-
-// ---------------------------------------------------------------------------
-// 2. raster (+ fused shading): one wave per 8x8 tile
-// ---------------------------------------------------------------------------
-struct RasterParams {
-  int N, H, W, TX, TY, T;
+struct ScanParams {
+  int T;
   int64_t list_cap;
-  float blur, bbox_pad;
-  int persp, clipb;
-  const int64_t* view_first;  // NULL: shared mode (first = n*F, count = F)
-  const int64_t* view_count;
+  const int* cnt;
+  const int* vtot;
+  int* start;
+  int* cur;
+  int* vbase;
+  int* tdone;
+  int4* units;
+  int* ctr;
+  unsigned long long* tkey;
+  const int64_t* view_count;  // NULL: shared mode (count = F)
   int64_t F;
-  // MODE 0 outputs
-  int64_t* p2f;
-  float* zbuf;
-  float* bary;
-  float* dists;
-  // MODE 1
-  ShadeParams S;
-  int out_flags, rgb_ch;
-  float* depth;
-  float* sil;
-  float* rgb;
-  int32_t* p2f32;
-  int* pcnt;
-  int* plist;
 };
 
+// One 1024-thread workgroup per view:
+//  * vbase[n] = entries of the views before n (from the per-view totals of k_bin_count);
+//  * start/cur = per-tile exclusive scan of the entry counts inside the view's region;
+//  * every non-empty tile gets a compact slot and ceil(entries / MR_UE) work units
+//    (one unit scanning every face of the view when its list would overflow the pool);
+//    view bases for slots and units come from one atomic each (any view order is fine:
+//    the raster result does not depend on the order units run in);
+//  * the 64 keys of a slot that several units share start at EMPTY (they merge by atomicMin)
+//    and its count-down starts at units - 1 (the unit that takes it to -1 appends the pixels).
+#define MR_KEY_EMPTY ((0x7f800000ull << 32) | 0x7fffffffull)
+__global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
+  __shared__ int part[16];
+  __shared__ long long red[16];
+  __shared__ int base[2];
+  const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  // vb = sum of vtot[m < n]
+  long long s = 0;
+  for (int m = t; m < n; m += 1024) s += P.vtot[m];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) red[wave] = s;
+  __syncthreads();
+  long long vb = 0;
+  for (int k = 0; k < 16; ++k) vb += red[k];
+  if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
+  const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
+  const int* c = P.cnt + (int64_t)n * P.T;
+  // pass 1: entry offsets; unit and slot totals of the view
+  int run_e = 0, tot_u = 0, tot_s = 0;
+  for (int b0 = 0; b0 < P.T; b0 += 1024) {
+    const int tt = b0 + t;
+    const int cc = tt < P.T ? c[tt] : 0;
+    int te;
+    const int ie = block_incl_sum(cc, part, te);
+    const int ex = run_e + ie - cc;
+    run_e += te;
+    if (tt < P.T) {
+      P.start[(int64_t)n * P.T + tt] = ex;
+      P.cur[(int64_t)n * P.T + tt] = ex;
+    }
+    const bool ovf = cc > 0 && vb + ex + cc > P.list_cap;
+    const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
+    tot_u += nu;
+    tot_s += cc > 0 ? 1 : 0;
+  }
+  {
+    const int su = wave_sum(tot_u), ss = wave_sum(tot_s);
+    if (lane == 0) { part[wave] = su; red[wave] = ss; }
+    __syncthreads();
+    if (t == 0) {
+      int au = 0, as = 0;
+      for (int k = 0; k < 16; ++k) { au += part[k]; as += (int)red[k]; }
+      base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
+      base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
+    }
+    __syncthreads();
+  }
+  // pass 2: units, slots, key init for shared slots (each thread re-reads its own tiles)
+  int run_u = base[0], run_s = base[1];
+  for (int b0 = 0; b0 < P.T; b0 += 1024) {
+    const int tt = b0 + t;
+    const int cc = tt < P.T ? c[tt] : 0;
+    const int ex = tt < P.T ? P.start[(int64_t)n * P.T + tt] : 0;
+    const bool ovf = cc > 0 && vb + ex + cc > P.list_cap;
+    const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
+    const int ns = cc > 0 ? 1 : 0;
+    int tu, ts;
+    const int iu = block_incl_sum(nu, part, tu);
+    const int is = block_incl_sum(ns, part, ts);
+    const int u0 = run_u + iu - nu, slot = run_s + is - ns;
+    run_u += tu;
+    run_s += ts;
+    const int gt = n * P.T + tt;
+    const int multi = nu > 1 ? (int)0x80000000u : 0;
+    for (int k = 0; k < nu; ++k) {
+      int4 U;
+      U.x = gt;
+      U.y = ovf ? -1 : (int)(vb + ex) + k * MR_UE;
+      U.z = ovf ? vcount : min(MR_UE, cc - k * MR_UE);
+      U.w = slot | multi;
+      P.units[u0 + k] = U;
+    }
+    if (nu > 1) {
+      P.tdone[slot] = nu - 1;
+      for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 2. raster: per-tile depth keys (k_tile_raster), then a streaming resolve (k_resolve)
+// ---------------------------------------------------------------------------
 // Exact per-(pixel, face) decision and depth: eval_face's return value and pz, without
 // the point-triangle distance unless blur > 0 and the pixel is outside. On the fast path
 // (blur == 0, FR_FAST) the edge signs reject before any division: a pixel whose edge
@@ -490,236 +646,62 @@ MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur,
   return true;
 }
 
-#define MR_WGT 8                    // tiles (= waves) per workgroup
-#define MR_SPX (MR_WGT * MR_TS * MR_TS)  // 512 pixels per strip
-#define MR_NONE 0x7fffffff          // "no face" sentinel, larger than any face id
+#define MR_NONE 0x7fffffff  // "no face" sentinel, larger than any face id
 
 // (z, face) packed so that unsigned order == frag_less order on the depths that are ever
 // kept (pz >= 0; -0 folds onto +0, which the CPU compares equal). The empty key sorts
 // after every kept fragment, +inf depth included.
-#define MR_KEY_EMPTY ((0x7f800000ull << 32) | (unsigned long long)MR_NONE)
 MR_DEV unsigned long long frag_key(float z, int f) {
   const unsigned zb = z == 0.0f ? 0u : __float_as_uint(z);
   return ((unsigned long long)zb << 32) | (unsigned)f;
 }
 
-// Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
-// row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP).
-MR_DEV int wave_incl_sum(int v) {
-#ifdef MR_DBG_SHFL
-  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v += u; }
-  return v;
-#endif
-  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
-  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
-  return v;
-}
-MR_DEV int wave_incl_max(int v) {
-#ifdef MR_DBG_SHFL
-  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v = max(v, u); }
-  return v;
-#endif
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
-  return v;
-}
-
-// Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
-MR_DEV void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-  __builtin_amdgcn_wave_barrier();
-}
-
-// ---- output staging for the 64x8-pixel strip of one raster workgroup ----
-// Rows padded to 72 entries so the 8 rows one wave's tile touches land in different banks.
-#define MR_SROW 72
-#define MR_SSZ (MR_TS * MR_SROW)
-MR_DEV int strip_slot(int row, int col) { return row * MR_SROW + col; }
-
-struct StageOut {  // 18 KB, union over the two modes
-  union {
-    struct { float depth[MR_SSZ], sil[MR_SSZ], rgb[MR_SSZ * 4]; int p2f[MR_SSZ]; } m1;
-    struct { long long p2f[MR_SSZ]; float zbuf[MR_SSZ], bary[MR_SSZ * 3], dists[MR_SSZ]; } m0;
-  };
+struct TileParams {
+  int H, W, TX, T;
+  float blur, bbox_pad;
+  int persp, clipb;
+  const int64_t* view_first;  // NULL: shared mode (overflow units scan faces n*F ..)
+  int64_t F;
+  const FaceRec* recs;
+  const int* list;
+  const int4* units;
+  const int* ctr;
+  unsigned long long* tkey;
+  int* tdone;
+  int* pcnt;    // (N) covered pixels per view
+  int2* plist;  // (N, H*W) covered (pixel, face record) pairs
 };
 
-// One wave's batch of up to 64 (tile, face) entries, expanded into (face, pixel) pairs.
-struct PairStage {
+// One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).
+struct WaveStage {
   FaceRec rec[64];
   int id[64];
-  int meta[64];  // first pair index | (rect width - 1) << 13 | strip col << 16 | strip row << 22
+  int meta[64];  // first pair index | (rect width - 1) << 13 | tile col << 16 | tile row << 19
   int mark[64];  // pass-local: pair slot -> entry lane that starts there
+  unsigned long long key[64];
+  float xs[MR_TS], ys[MR_TS];
 };
 
-struct RasterSmem {
-  union {
-    PairStage ps[MR_WGT];  // 39 KB, face loop only
-    StageOut out;          // epilogue only
-  };
-  unsigned long long key[MR_SPX];  // per-pixel (z, face) minimum
-  float xs[64], ys[MR_TS];         // pixel-centre NDC of the strip's columns / rows
-};
-
-template <int MODE>
-MR_DEV void stage_pixel(const RasterParams& P, StageOut& O, int n, int sp, bool hit, int f, const FaceRec& r,
-                        const FragEval& e) {
-  if (MODE == 0) {
-    O.m0.p2f[sp] = hit ? (long long)f : -1ll;
-    O.m0.zbuf[sp] = hit ? e.pz : -1.0f;
-    O.m0.bary[3 * sp + 0] = hit ? e.b0 : -1.0f;
-    O.m0.bary[3 * sp + 1] = hit ? e.b1 : -1.0f;
-    O.m0.bary[3 * sp + 2] = hit ? e.b2 : -1.0f;
-    O.m0.dists[sp] = hit ? e.sdist : -1.0f;
-  } else {
-    PixGeom G;
-    ShadeOut o;
-    ShadeCache C;
-    if (hit) gather_geom(P.S, r.face, G);
-    shade_fwd(P.S, n, hit, G, hit ? e.b0 : 0.f, hit ? e.b1 : 0.f, hit ? e.b2 : 0.f, hit ? e.pz : 0.f,
-              hit ? e.sdist : 0.f, o, C);
-    O.m1.depth[sp] = o.depth;
-    O.m1.sil[sp] = o.sil;
-    O.m1.rgb[4 * sp + 0] = o.rgb[0];
-    O.m1.rgb[4 * sp + 1] = o.rgb[1];
-    O.m1.rgb[4 * sp + 2] = o.rgb[2];
-    O.m1.rgb[4 * sp + 3] = o.alpha;
-    O.m1.p2f[sp] = hit ? f : -1;
-  }
-}
-
-// Coalesced strip write: thread t owns strip row t/64, column t%64 (one wave = one 256-B row);
-// multi-channel rows (bary, rgb) go out as flat float streams, 64 consecutive floats per
-// wave instruction. With O == nullptr the strip is empty and the background is written
-// straight from registers (no LDS round trip).
-template <int MODE, int CH>
-MR_DEV void write_strip(const RasterParams& P, const StageOut* O, int n, int x0, int y0) {
-  const int t = threadIdx.x;
-  const int row = t >> 6, col = t & 63;
-  const int px = x0 + col, py = y0 + row;
-  const int sp = strip_slot(row, col);
-  float bgv[4] = {-1.0f, -1.0f, -1.0f, -1.0f}, bgd = -1.0f, bgs = -1.0f;
-  if (MODE == 1 && !O) {
-    PixGeom G;
-    ShadeOut o;
-    ShadeCache C;
-    shade_fwd(P.S, n, false, G, 0.f, 0.f, 0.f, 0.f, 0.f, o, C);
-    bgd = o.depth;
-    bgs = o.sil;
-    bgv[0] = o.rgb[0]; bgv[1] = o.rgb[1]; bgv[2] = o.rgb[2]; bgv[3] = o.alpha;
-  }
-  if (px < P.W && py < P.H) {
-    const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
-    if (MODE == 0) {
-      P.p2f[pix] = O ? O->m0.p2f[sp] : -1ll;
-      P.zbuf[pix] = O ? O->m0.zbuf[sp] : -1.0f;
-      P.dists[pix] = O ? O->m0.dists[sp] : -1.0f;
-    } else {
-      if (P.out_flags & MR_OUT_DEPTH) P.depth[pix] = O ? O->m1.depth[sp] : bgd;
-      if (P.out_flags & MR_OUT_SIL) P.sil[pix] = O ? O->m1.sil[sp] : bgs;
-      P.p2f32[pix] = O ? O->m1.p2f[sp] : -1;
-    }
-  }
-  constexpr int ch = CH;  // compile-time channel count: the flat-stream index math is shifts/multiplies
-  if (MODE == 1 && !(P.out_flags & MR_OUT_RGB)) return;
-  const int rowlen = 64 * ch;
-  const int ncols = (P.W - x0) < 64 ? (P.W - x0) : 64;
-  for (int j = t; j < MR_TS * rowlen; j += MR_SPX) {
-    const int rr = j / rowlen, q = j - rr * rowlen;
-    const int cc = q / ch, k = q - cc * ch;
-    const int yy = y0 + rr;
-    if (cc >= ncols || yy >= P.H) continue;
-    const int64_t base = ((int64_t)n * P.H + yy) * P.W + x0;
-    const int s = strip_slot(rr, cc);
-    if (MODE == 0) P.bary[base * 3 + q] = O ? O->m0.bary[3 * s + k] : -1.0f;
-    else P.rgb[base * ch + q] = O ? O->m1.rgb[4 * s + k] : (k == 0 ? bgv[0] : k == 1 ? bgv[1] : k == 2 ? bgv[2] : bgv[3]);
-  }
-}
-
-// Optional phase timestamps (build with -DMR_PROF; tools/raster_phases.py): per wave 16 slots,
-// s_memtime at phase boundaries, s_memrealtime at start/end, entry/pass counts.
-#ifdef MR_PROF
-__device__ unsigned long long* g_prof = nullptr;
-#define PROF_AT(i, v)                                                                                 \
-  do {                                                                                                \
-    if (g_prof && lane == 0)                                                                          \
-      g_prof[((size_t)prof_slot * MR_WGT + wave) * 16 + (i)] = (v);                                 \
-  } while (0)
-#define PROF_T(i) PROF_AT(i, __builtin_amdgcn_s_memtime())
-#else
-#define PROF_AT(i, v) do {} while (0)
-#define PROF_T(i) do {} while (0)
-#endif
-
-// One 512-thread workgroup = 8 waves rasterizes one 64x8-pixel strip (8 tiles of 8x8):
-//  (1) the strip's 8 tile lists are concatenated and dealt to the waves 64 entries at a
-//      time, one per lane; each lane clips its face's pixel bbox to its tile (<= 64 pixels);
-//  (2) a wave prefix sum over the rectangle sizes numbers the (face, pixel) pairs, and
-//      64 pairs per pass are evaluated exactly (frag_keep), one per lane — so a ~3-pixel
-//      face costs ~3 lanes, not a whole wave;
-//  (3) kept fragments meet in a per-pixel LDS atomicMin on the packed (z, face) key, which
-//      is order-independent and equals the CPU's "strictly nearer, earlier face wins";
-//  (4) wave k finalises tile k (exact recompute + shading) and the strip is written row-wise.
-template <int MODE, int CH>
-__device__ __attribute__((noinline)) void raster_strip(const RasterParams& P, RasterSmem& sm, const FaceRec* __restrict__ recs,
-                         const int* __restrict__ list, const int* __restrict__ cnt, const int* __restrict__ start,
-                         const int* __restrict__ vbase, int n, int gx, int ty, int prof_slot) {
-  const int t = threadIdx.x;
-  const int lane = t & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
-  PROF_AT(8, __builtin_amdgcn_s_memrealtime());
-  PROF_T(0);
-  const int H = P.H, W = P.W;
-  const int x0 = gx * MR_WGT * MR_TS, y0 = ty * MR_TS;
-  const int64_t vb = vbase[n];
-  const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
-  const int64_t vcount = P.view_first ? P.view_count[n] : P.F;
-
-  // lanes 0..7 <-> tiles 0..7 of the strip: entry count, list start, overflow flag
-  int tc = 0, ts = 0, tovf = 0;
-  {
-    const int txl = gx * MR_WGT + lane;
-    if (lane < MR_WGT && txl < P.TX) {
-      const int64_t bt = (int64_t)n * P.T + (int64_t)ty * P.TX + txl;
-      const int c = cnt[bt];
-      ts = start[bt];
-      // overflowed list: the tile's entries are every face of the view (bbox-filtered below);
-      // counts are exact, so an empty tile stays empty
-      if (c > 0 && vb + ts + c > P.list_cap) {
-        tovf = 1;
-        tc = (int)(vcount < 0x7fffffffll ? vcount : 0x7fffffffll);
-      } else {
-        tc = c;
-      }
-    }
-  }
-  const int tincl = wave_incl_sum(tc);
-  const int E = __builtin_amdgcn_readlane(tincl, MR_WGT - 1);
-  PROF_T(1);
-  if (E == 0) {  // uniform over the workgroup (work lists only hold non-empty strips)
-    write_strip<MODE, CH>(P, nullptr, n, x0, y0);
-    return;
-  }
-  const int texcl = tincl - tc;
-
-  if (t < 64) sm.xs[t] = col_ndc(x0 + t < W ? x0 + t : W - 1, H, W);
-  else if (t < 64 + MR_TS) sm.ys[t - 64] = row_ndc(y0 + t - 64 < H ? y0 + t - 64 : H - 1, H, W);
-  sm.key[t] = MR_KEY_EMPTY;
-  PairStage& S = sm.ps[wave];
-  S.mark[lane] = -1;
-  __syncthreads();
-  PROF_T(2);
-#ifdef MR_PROF
-  int prof_passes = 0;
-#endif
-
+// Persistent grid of independent waves (4 per workgroup, no workgroup barriers): wave g
+// takes units g, g + G, ... of the list k_bin_scan emitted (G = resident waves). Per unit:
+//  (1) one entry per lane: load its face record, clip the face's padded pixel bbox to the
+//      tile (<= 64 pixels);
+//  (2) a DPP prefix sum over the rectangle sizes numbers the (face, pixel) pairs, and the
+//      wave evaluates 64 pairs per pass exactly (frag_keep), one per lane — a ~3-pixel
+//      face costs ~3 lanes, not a wave;
+//  (3) kept fragments meet in a per-pixel ds_min_u64 on the packed (z, face) key, which is
+//      order-independent and equals the CPU's "strictly nearer, earlier face wins";
+//  (4) a tile that is a single unit appends its covered pixels (pixel, winning face record)
+//      to the view's list straight from LDS (one atomic per wave); units sharing a tile
+//      merge their keys with global u64 atomicMin, and the last of them to finish (a
+//      count-down with agent-scope release/acquire) reads the merged keys back with
+//      returning atomics and appends.
+__global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
+  __shared__ WaveStage stage[4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  WaveStage& S = stage[wave];
+  const int nunits = P.ctr[CTR_UNITS];
   const float pad = P.bbox_pad, blur = P.blur;
   const bool persp = P.persp != 0, clipb = P.clipb != 0;
 #ifdef MR_DBG_NOFAST
@@ -727,150 +709,152 @@ __device__ __attribute__((noinline)) void raster_strip(const RasterParams& P, Ra
 #else
   const bool fast_ok = !(blur > 0.0f);
 #endif
+  const int H = P.H, W = P.W;
 #pragma unroll 1
-  for (int eb = 0; eb < E; eb += MR_WGT * 64) {
-    // (1) one entry per lane, interleaved over the 8 waves so every wave gets ~E/8 of them
-    const int e = eb + lane * MR_WGT + wave;
-    int k = 0;
-#pragma unroll
-    for (int kk = 1; kk < MR_WGT; ++kk) k += e >= __builtin_amdgcn_readlane(texcl, kk) ? 1 : 0;
-    // cross-lane reads at full EXEC (ds_bpermute from an inactive lane is undefined)
-    const int kex = __shfl(texcl, k, 64);
-    const int kst = __shfl(ts, k, 64);
-    const int kovf = __shfl(tovf, k, 64);
-    int np = 0, meta = 0;
-    if (e < E) {
-      const int i = e - kex;
-      const int id = kovf ? (int)(vfirst + i) : list[vb + kst + i];
-      const FaceRec r = recs[id];
-      int cx0, cx1, cy0, cy1;
-      ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
-      ndc_range_to_pix(r.ymin - pad, r.ymax + pad, H, W, cy0, cy1);
-      const int tx0 = x0 + k * MR_TS;
-      cx0 = cx0 > tx0 ? cx0 : tx0;
-      cx1 = cx1 < tx0 + MR_TS - 1 ? cx1 : tx0 + MR_TS - 1;
-      cy0 = cy0 > y0 ? cy0 : y0;
-      cy1 = cy1 < y0 + MR_TS - 1 ? cy1 : y0 + MR_TS - 1;
-      if ((r.flags & FR_VALID) && cx0 <= cx1 && cy0 <= cy1) {
-        const int w = cx1 - cx0 + 1;
-        np = w * (cy1 - cy0 + 1);
-        meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 22);
+  for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+    const int4 U = P.units[u];
+    const int n = U.x / P.T, t = U.x - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int x0 = tx * MR_TS, y0 = ty * MR_TS;
+    if (lane < MR_TS) S.xs[lane] = col_ndc(x0 + lane < W ? x0 + lane : W - 1, H, W);
+    else if (lane < 2 * MR_TS) S.ys[lane - MR_TS] = row_ndc(y0 + lane - MR_TS < H ? y0 + lane - MR_TS : H - 1, H, W);
+    S.key[lane] = MR_KEY_EMPTY;
+    S.mark[lane] = -1;
+    const bool ovf = U.y < 0;
+    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
+    wave_lds_sync();
+#pragma unroll 1
+    for (int eb = 0; eb < U.z; eb += 64) {
+      const int e = eb + lane;
+      int np = 0, meta = 0;
+      if (e < U.z) {
+        const int id = ovf ? (int)(vfirst + e) : P.list[U.y + e];
+        const FaceRec r = P.recs[id];
+        int cx0, cx1, cy0, cy1;
+        ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
+        ndc_range_to_pix(r.ymin - pad, r.ymax + pad, H, W, cy0, cy1);
+        cx0 = cx0 > x0 ? cx0 : x0;
+        cx1 = cx1 < x0 + MR_TS - 1 ? cx1 : x0 + MR_TS - 1;
+        cy0 = cy0 > y0 ? cy0 : y0;
+        cy1 = cy1 < y0 + MR_TS - 1 ? cy1 : y0 + MR_TS - 1;
+        if ((r.flags & FR_VALID) && cx0 <= cx1 && cy0 <= cy1) {
+          const int w = cx1 - cx0 + 1;
+          np = w * (cy1 - cy0 + 1);
+          meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
+        }
+        S.rec[lane] = r;
+        S.id[lane] = id;
       }
-      S.rec[lane] = r;
-      S.id[lane] = id;
-    }
-    // (2) pair numbering
-    const int pincl = wave_incl_sum(np);
-    const int pexcl = pincl - np;
-    const int NP = __builtin_amdgcn_readlane(pincl, 63);
-    S.meta[lane] = meta | pexcl;
+      // pair numbering
+      const int pincl = wave_incl_sum(np);
+      const int pexcl = pincl - np;
+      const int NP = __builtin_amdgcn_readlane(pincl, 63);
+      S.meta[lane] = meta | pexcl;
 #pragma unroll 1
-    for (int pb = 0; pb < NP; pb += 64) {
-#ifdef MR_PROF
-      ++prof_passes;
-#endif
-      wave_lds_sync();
-      // entry starting inside this pass marks its first slot; slot 0 belongs to the entry
-      // straddling pb (the last non-empty entry starting at or before it)
-      if (np > 0 && pexcl > pb && pexcl < pb + 64) S.mark[pexcl - pb] = lane;
-      const unsigned long long own = __ballot(np > 0 && pexcl <= pb);
-      const int straddle = 63 - __builtin_clzll(own);
-      wave_lds_sync();
-      int m = S.mark[lane];
-      S.mark[lane] = -1;
-      if (lane == 0) m = straddle;
-      m = wave_incl_max(m);
-      const int q = pb + lane;
-      if (q < NP) {
-        // (3) one (face, pixel) pair per lane
-        const int mt = S.meta[m];
-        const int loc = q - (mt & 0x1fff);
-        const int w = ((mt >> 13) & 7) + 1;
+      for (int pb = 0; pb < NP; pb += 64) {
+        wave_lds_sync();
+        // the entry starting inside this pass marks its first slot; slot 0 belongs to the
+        // entry straddling pb (the last non-empty entry starting at or before it)
+        if (np > 0 && pexcl > pb && pexcl < pb + 64) S.mark[pexcl - pb] = lane;
+        const unsigned long long own = __ballot(np > 0 && pexcl <= pb);
+        const int straddle = 63 - __builtin_clzll(own);
+        wave_lds_sync();
+        int m = S.mark[lane];
+        S.mark[lane] = -1;
+        if (lane == 0) m = straddle;
+        m = wave_incl_max(m);
+        const int q = pb + lane;
+        if (q < NP) {
+          // one (face, pixel) pair per lane
+          const int mt = S.meta[m];
+          const int loc = q - (mt & 0x1fff);
+          const int w = ((mt >> 13) & 7) + 1;
 #ifdef MR_DBG_IDIV
-        const int ly = loc / w;
+          const int ly = loc / w;
 #else
-        const int ly = (int)((float)loc * __builtin_amdgcn_rcpf((float)w) + 1e-3f);
+          const int ly = (int)((float)loc * __builtin_amdgcn_rcpf((float)w) + 1e-3f);
 #endif
-        const int lx = loc - ly * w;
-        const int sx = ((mt >> 16) & 63) + lx, sy = ((mt >> 22) & 7) + ly;
-        const FaceRec r = S.rec[m];
-        float pz;
-        if (frag_keep(r, sm.xs[sx], sm.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
-          atomicMin(&sm.key[sy * 64 + sx], frag_key(pz, S.id[m]));
+          const int lx = loc - ly * w;
+          const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
+          const FaceRec r = S.rec[m];
+          float pz;
+          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
+            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, S.id[m]));
+        }
+      }
+      wave_lds_sync();  // the stage is rewritten by the next batch
+    }
+    unsigned long long k = S.key[lane];
+    bool emit = true;
+    if (U.w < 0) {  // tile shared by several units
+      const int slot = U.w & 0x7fffffff;
+      unsigned long long* dst = P.tkey + (int64_t)slot * 64 + lane;
+      // Device-scope atomics are performed at the memory side (never cached in an XCD's L2),
+      // so agent atomics on both sides hand the keys over: this wave's 64 atomicMin are
+      // acknowledged (vmcnt) before its count-down, and the last unit reads the merged keys
+      // with returning atomics issued after it observed the count-down reach it.
+      atomicMin(dst, k);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int left = 0;
+      if (lane == 0) left = __hip_atomic_fetch_add(&P.tdone[slot], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      left = __builtin_amdgcn_readfirstlane(left);
+      emit = left == 0;  // the last unit of the tile
+      if (emit) k = atomicMin(dst, MR_KEY_EMPTY);
+    }
+    if (emit) {
+      const int f = (int)(unsigned)(k & 0xffffffffull);
+      const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
+      const bool hit = f != MR_NONE && px < W && py < H;
+      const unsigned long long msk = __ballot(hit);
+      if (msk) {
+        int base = 0;
+        if (lane == 0) base = atomicAdd(&P.pcnt[n], __popcll(msk));
+        base = __shfl(base, 0, 64);
+        if (hit) P.plist[(int64_t)n * H * W + base + __popcll(msk & ((1ull << lane) - 1ull))] = make_int2(py * W + px, f);
       }
     }
-    wave_lds_sync();  // the stage is rewritten by the next batch
-  }
-  PROF_T(3);
-  __syncthreads();
-  PROF_T(4);
-
-  // (4) wave k finalises tile k of the strip
-  const int ly = lane >> 3, lx = wave * MR_TS + (lane & 7);
-  const int px = x0 + lx, py = y0 + ly;
-  const unsigned long long key = sm.key[ly * 64 + lx];
-  const int f = (int)(unsigned)(key & 0xffffffffull);
-  FragEval ev;
-  FaceRec r;
-  bool hit = f != MR_NONE && px < W && py < H;
-  if (hit) {
-    r = recs[f];
-    hit = eval_face(r, sm.xs[lx], sm.ys[ly], P.bbox_pad, P.blur, P.persp, P.clipb, ev);
-  }
-  stage_pixel<MODE>(P, sm.out, n, strip_slot(ly, lx), hit, f, r, ev);
-  if (MODE == 1) {  // compact list of covered pixels for the backward (one atomic per wave)
-    const unsigned long long msk = __ballot(hit);
-    if (msk) {
-      int base = 0;
-      if (lane == 0) base = atomicAdd(&P.pcnt[n], __popcll(msk));
-      base = __shfl(base, 0, 64);
-      if (hit) {
-        const int rank = __popcll(msk & ((1ull << lane) - 1ull));
-        P.plist[(int64_t)n * H * W + base + rank] = py * W + px;
-      }
-    }
-  }
-  PROF_T(5);
-  __syncthreads();
-  write_strip<MODE, CH>(P, &sm.out, n, x0, y0);
-  PROF_T(6);
-  PROF_AT(9, __builtin_amdgcn_s_memrealtime());
-#ifdef MR_PROF
-  PROF_AT(7, ((unsigned long long)E << 32) | (unsigned)prof_passes);
-#endif
-}
-
-// Persistent raster: a grid sized to the resident capacity (CUs x workgroups per CU) pulls
-// non-empty strips from the three work buckets (heaviest first) through one atomic counter;
-// background strips never reach this kernel (k_bg writes them). Every workgroup leaves
-// when the counter passes the total, so the grid always drains.
-template <int MODE, int CH>
-__global__ void __launch_bounds__(512, 6) k_raster(RasterParams P, const FaceRec* __restrict__ recs,
-                                                const int* __restrict__ list, const int* __restrict__ cnt,
-                                                const int* __restrict__ start, const int* __restrict__ vbase,
-                                                const int* __restrict__ work, int* __restrict__ wctr, int64_t NS,
-                                                int S, int GX) {
-  __shared__ RasterSmem sm;
-  __shared__ int s_item;
-  const int c0 = wctr[0], c1 = wctr[1], c2 = wctr[2];
-  const int total = c0 + c1 + c2;
-  for (;;) {
-    if (threadIdx.x == 0) s_item = atomicAdd(&wctr[3], 1);
-    __syncthreads();  // also orders the previous strip's LDS reads before this strip's writes
-    const int item = s_item;
-    if (item >= total) break;
-    const int sid = item < c0 ? work[item] : item < c0 + c1 ? work[NS + (item - c0)] : work[2 * NS + (item - c0 - c1)];
-    const int n = sid / S, r = sid - n * S;
-    const int ty = r / GX, gx = r - ty * GX;
-    raster_strip<MODE, CH>(P, sm, recs, list, cnt, start, vbase, n, gx, ty, sid);
+    wave_lds_sync();
   }
 }
 
-// Background for every strip without entries: streaming vector stores, one workgroup per
-// strip row (8 image rows) of one view; strips holding faces are skipped (k_raster writes them).
+// ---- outputs: background fill (every pixel) + shading of the covered-pixel list ----
+struct OutParams {
+  int N, H, W;
+  float blur, bbox_pad;
+  int persp, clipb;
+  const FaceRec* recs;
+  const int* pcnt;
+  const int2* plist;
+  // MODE 0 outputs (PyTorch3D Fragments, K = 1)
+  int64_t* p2f;
+  float* zbuf;
+  float* bary;
+  float* dists;
+  // MODE 1
+  ShadeParams S;
+  const ShadeRec* srec;
+  int64_t F;  // faces of the shared mesh (record id = n*F + face)
+  int out_flags;
+  float* depth;
+  float* sil;
+  float* rgb;
+  int32_t* p2f32;  // optional
+};
+
+// Per-face shading records of the shared mesh (one thread per face).
+__global__ void __launch_bounds__(256) k_shade_rec(ShadeParams S, int64_t F, ShadeRec* __restrict__ out) {
+  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= F) return;
+  ShadeRec R;
+  make_shade_rec(S, (uint32_t)f, R);
+  out[f] = R;
+}
+
+// Background of every pixel (the covered ones are overwritten by k_shade afterwards):
+// a pure store stream, 4 pixels per thread and 16-B vector stores when W % 4 == 0.
 template <int MODE, int CH>
-__global__ void __launch_bounds__(256) k_bg(RasterParams P, const int* __restrict__ scount, int S, int GX) {
-  const int n = blockIdx.y, ty = blockIdx.x;
+__global__ void __launch_bounds__(256) k_fill_bg(OutParams P) {
+  const int n = blockIdx.y;
   float bgd = -1.0f, bgs = -1.0f, bgv[4] = {-1.0f, -1.0f, -1.0f, -1.0f};
   if (MODE == 1) {
     PixGeom G;
@@ -881,90 +865,142 @@ __global__ void __launch_bounds__(256) k_bg(RasterParams P, const int* __restric
     bgs = o.sil;
     bgv[0] = o.rgb[0]; bgv[1] = o.rgb[1]; bgv[2] = o.rgb[2]; bgv[3] = o.alpha;
   }
-  const int* sc = scount + (int64_t)n * S + (int64_t)ty * GX;
-  const int W = P.W, H = P.H;
-  const bool vec = (W & 3) == 0;
-  const int W4 = (W + 3) >> 2;
-  const bool rgb = MODE == 1 && (P.out_flags & MR_OUT_RGB);
-  for (int rr = threadIdx.x >> 7; rr < MR_TS; rr += 2) {
-    const int y = ty * MR_TS + rr;
-    if (y >= H) break;
-    for (int x4 = threadIdx.x & 127; x4 < W4; x4 += 128) {
-      if (sc[x4 >> 4] != 0) continue;  // 16 groups of 4 pixels per 64-pixel strip
-      const int x = x4 * 4;
-      const int64_t pix = ((int64_t)n * H + y) * W + x;
-      if (vec) {
-        if (MODE == 0) {
-          longlong2* q = (longlong2*)(P.p2f + pix);
-          q[0] = make_longlong2(-1ll, -1ll);
-          q[1] = make_longlong2(-1ll, -1ll);
-          const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
-          *(float4*)(P.zbuf + pix) = m1;
-          *(float4*)(P.dists + pix) = m1;
-          float4* b = (float4*)(P.bary + pix * 3);
-          b[0] = m1; b[1] = m1; b[2] = m1;
-        } else {
-          if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = make_float4(bgd, bgd, bgd, bgd);
-          if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = make_float4(bgs, bgs, bgs, bgs);
-          *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
-          if (rgb) {
-            float4* c = (float4*)(P.rgb + pix * CH);
-            if (CH == 4) {
-              const float4 v = make_float4(bgv[0], bgv[1], bgv[2], bgv[3]);
-              c[0] = v; c[1] = v; c[2] = v; c[3] = v;
-            } else {
-              c[0] = make_float4(bgv[0], bgv[1], bgv[2], bgv[0]);
-              c[1] = make_float4(bgv[1], bgv[2], bgv[0], bgv[1]);
-              c[2] = make_float4(bgv[2], bgv[0], bgv[1], bgv[2]);
-            }
-          }
-        }
+  const int64_t HW = (int64_t)P.H * P.W;
+  const int64_t base = (int64_t)n * HW;
+  if ((P.W & 3) == 0) {
+    const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+    const float4 dv = make_float4(bgd, bgd, bgd, bgd), sv = make_float4(bgs, bgs, bgs, bgs);
+    const float4 c4 = make_float4(bgv[0], bgv[1], bgv[2], bgv[3]);
+    const float4 c0 = make_float4(bgv[0], bgv[1], bgv[2], bgv[0]), c1 = make_float4(bgv[1], bgv[2], bgv[0], bgv[1]),
+                 c2 = make_float4(bgv[2], bgv[0], bgv[1], bgv[2]);
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < HW / 4; i += (int64_t)gridDim.x * 256) {
+      const int64_t pix = base + 4 * i;
+      if (MODE == 0) {
+        longlong2* q = (longlong2*)(P.p2f + pix);
+        q[0] = make_longlong2(-1ll, -1ll);
+        q[1] = make_longlong2(-1ll, -1ll);
+        *(float4*)(P.zbuf + pix) = m1;
+        *(float4*)(P.dists + pix) = m1;
+        float4* b = (float4*)(P.bary + pix * 3);
+        b[0] = m1; b[1] = m1; b[2] = m1;
       } else {
-        for (int k = 0; k < 4 && x + k < W; ++k) {
-          const int64_t q = pix + k;
-          if (MODE == 0) {
-            P.p2f[q] = -1ll;
-            P.zbuf[q] = -1.0f;
-            P.dists[q] = -1.0f;
-            for (int c = 0; c < 3; ++c) P.bary[q * 3 + c] = -1.0f;
+        if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = dv;
+        if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = sv;
+        if (P.p2f32) *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
+        if (P.out_flags & MR_OUT_RGB) {
+          float4* c = (float4*)(P.rgb + pix * CH);
+          if (CH == 4) {
+            c[0] = c4; c[1] = c4; c[2] = c4; c[3] = c4;
           } else {
-            if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = bgd;
-            if (P.out_flags & MR_OUT_SIL) P.sil[q] = bgs;
-            P.p2f32[q] = -1;
-            if (rgb)
-              for (int c = 0; c < CH; ++c) P.rgb[q * CH + c] = bgv[c];
+            c[0] = c0; c[1] = c1; c[2] = c2;
           }
         }
+      }
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < HW; i += (int64_t)gridDim.x * 256) {
+      const int64_t q = base + i;
+      if (MODE == 0) {
+        P.p2f[q] = -1ll;
+        P.zbuf[q] = -1.0f;
+        P.dists[q] = -1.0f;
+        for (int c = 0; c < 3; ++c) P.bary[q * 3 + c] = -1.0f;
+      } else {
+        if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = bgd;
+        if (P.out_flags & MR_OUT_SIL) P.sil[q] = bgs;
+        if (P.p2f32) P.p2f32[q] = -1;
+        if (P.out_flags & MR_OUT_RGB)
+          for (int c = 0; c < CH; ++c) P.rgb[q * CH + c] = bgv[c];
       }
     }
   }
 }
 
-// Resident workgroups of k_raster<MODE,CH> on the current device (persistent grid size).
+// One covered pixel per thread (grid (NB, N), striding over view n's list): recompute the
+// winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade (M = 1).
 template <int MODE, int CH>
-static int raster_grid(int64_t strips_total) {
-  static int cached = 0;
-  if (!cached) {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_raster<MODE, CH>, 512, 0) != hipSuccess || per <= 0)
-      per = 2;
-    cached = cus * per;
+__global__ void __launch_bounds__(256) k_shade(OutParams P) {
+  const int n = blockIdx.y;
+  const int cntp = P.pcnt[n];
+  const int64_t HW = (int64_t)P.H * P.W;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < cntp; i += gridDim.x * 256) {
+    const int2 e = P.plist[n * HW + i];
+    const int px = e.x % P.W, py = e.x / P.W;
+    const int64_t q = n * HW + e.x;
+    const FaceRec r = P.recs[e.y];
+    PixGeom G;
+    if (MODE == 1) load_geom(P.srec, (uint32_t)(e.y - n * P.F), G);  // in parallel with the record
+    FragEval ev;
+    const bool hit = eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp,
+                               P.clipb, ev);  // true by construction (same test that kept it)
+    if (!hit) continue;
+    if (MODE == 0) {
+      P.p2f[q] = (int64_t)e.y;
+      P.zbuf[q] = ev.pz;
+      P.dists[q] = ev.sdist;
+      P.bary[3 * q + 0] = ev.b0;
+      P.bary[3 * q + 1] = ev.b1;
+      P.bary[3 * q + 2] = ev.b2;
+    } else {
+      ShadeOut o;
+      ShadeCache C;
+      shade_fwd(P.S, n, true, G, ev.b0, ev.b1, ev.b2, ev.pz, ev.sdist, o, C);
+      if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = o.depth;
+      if (P.out_flags & MR_OUT_SIL) P.sil[q] = o.sil;
+      if (P.out_flags & MR_OUT_RGB) {
+        P.rgb[q * CH + 0] = o.rgb[0];
+        P.rgb[q * CH + 1] = o.rgb[1];
+        P.rgb[q * CH + 2] = o.rgb[2];
+        if (CH == 4) P.rgb[q * CH + 3] = o.alpha;
+      }
+      if (P.p2f32) P.p2f32[q] = e.y;
+    }
   }
-  return (int)(strips_total < cached ? (strips_total > 0 ? strips_total : 1) : cached);
 }
 
-template <int MODE, int CH>
-static int launch_raster(const RasterParams& P, const RasterWS& w, const BinGeom& g, int64_t N, int kid,
-                         hipStream_t st) {
-  dim3 bgrid((unsigned)g.TY, (unsigned)N);
-  MR_TIMED(KID_BG, st, (k_bg<MODE, CH><<<bgrid, 256, 0, st>>>(P, w.scount, g.S, g.GX)));
-  MR_CHECK_LAUNCH("k_bg");
-  const int grid = raster_grid<MODE, CH>(N * g.S);
-  MR_TIMED(kid, st, (k_raster<MODE, CH><<<grid, 512, 0, st>>>(P, w.recs, w.list, w.cnt, w.start, w.vbase, w.work,
-                                                                w.wctr, N * g.S, g.S, g.GX)));
-  MR_CHECK_LAUNCH("k_raster");
+// Per-view workgroups for a view-strided grid: ~`total` workgroups overall, at most `cap` per view.
+static int blocks_per_view(int64_t N, int total, int64_t cap) {
+  int nb = ceil_div(total, N);
+  if (nb > cap) nb = (int)cap;
+  return nb < 1 ? 1 : nb;
+}
+
+// Resident workgroups of a kernel on the current device (persistent grid size).
+template <typename K>
+static int resident_grid(K kernel, int threads, int fallback_per_cu) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, threads, 0) != hipSuccess || per <= 0)
+    per = fallback_per_cu;
+  return cus * per;
+}
+
+struct RasterCfg {  // what launch_raster needs besides the workspace
+  int H, W;
+  float blur, bbox_pad;
+  int persp, clipb;
+  const int64_t* view_first;
+  int64_t F;
+};
+
+static TileParams make_tile(const RasterCfg& c, const BinGeom& g, const RasterWS& w) {
+  TileParams P;
+  P.H = c.H; P.W = c.W; P.TX = g.TX; P.T = g.T;
+  P.blur = c.blur; P.bbox_pad = c.bbox_pad;
+  P.persp = c.persp; P.clipb = c.clipb;
+  P.view_first = c.view_first; P.F = c.F;
+  P.recs = w.recs; P.list = w.list; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
+  P.tdone = w.tdone; P.pcnt = w.pcnt; P.plist = w.plist;
+  return P;
+}
+
+static int launch_tile_raster(const TileParams& P, int64_t unit_cap, hipStream_t st) {
+  static int grid = 0;
+  if (!grid) grid = resident_grid(k_tile_raster, 256, 7);
+  const int gb = (int)(unit_cap / 4 + 1 < grid ? unit_cap / 4 + 1 : grid);
+  MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<<<gb, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_tile_raster");
   return MR_OK;
 }
 
@@ -1063,119 +1099,194 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   acc_flush(L, P.gfv);
 }
 
-// Fused render backward over the compact per-view list of covered pixels written by
-// k_raster<1>: workgroup (b, n) handles entries [1024 b, 1024 b + 1024) of view n.
+// Sum ACC-float rows over runs of equal `key` in lane order (segmented shuffle scan; the
+// covered-pixel list is row-major, so a face's pixels along a row are consecutive lanes).
+// The run totals are staged in the wave's LDS rows and added with float atomics whose
+// lanes cover consecutive components of consecutive runs (contiguous 4*ACC-byte rows per
+// run instead of one scattered dword per lane and instruction). Lanes with key < 0 carry
+// zero rows. Uniform call (full EXEC).
+template <int ACC>
+MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float* lrow, int* lkey) {
+  const int lane = threadIdx.x & 63;
+  const int prev = __shfl_up(key, 1, 64);
+  const bool head = lane == 0 || key != prev;
+  const int d = lane - wave_incl_max(head ? lane : 0);  // distance to the run's first lane
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) {
+    float x = v[i];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float y = __shfl_up(x, o, 64);
+      if (d >= o) x += y;
+    }
+    v[i] = x;
+  }
+  const int next = __shfl_down(key, 1, 64);
+  const bool emit = (lane == 63 || key != next) && key >= 0;
+  const unsigned long long m = __ballot(emit);
+  if (emit) {
+    const int slot = __popcll(m & ((1ull << lane) - 1ull));
+    lkey[slot] = key;
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
+  }
+  wave_lds_sync();
+  const int nt = __popcll(m);
+  for (int j = lane; j < nt * ACC; j += 64) {
+    const int r = j / ACC;
+    const float x = lrow[j];
+    if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
+  }
+  wave_lds_sync();
+}
+
+// Fused render backward over the compact per-view (pixel, face record) list written by
+// k_tile_raster, in two kernels so that each stays small enough (VGPRs) to keep several
+// waves per SIMD hiding its load latency:
+//   k_bwd_shade: per covered pixel, recompute fragment + shading and differentiate the
+//                blends / Phong / texture -> 20-float record (grads of z, signed dist,
+//                barycentrics, interpolated point / normal / texel, and the barycentrics);
+//   k_bwd_geom : per covered pixel, rasterizer backward (edge functions, perspective
+//                correction, distances) + projection backward -> per-face rows summed over
+//                runs (seg_scatter) and per-view R/T partial sums (one slot per wave).
+// Workgroup (b, n) takes 256-entry chunks b, b + NB, ... of view n's list.
+#define MR_BWD_REC 5  // float4s per pixel record
 struct RenderBwdParams {
   int N, H, W, NB;
   float blur, bbox_pad;
   int persp, clipb;
   const FaceRec* recs;
-  const int32_t* p2f32;
   const int* pcnt;
-  const int* plist;
+  const int2* plist;
   const float* gD;
   const float* gS;
   const float* gRGB;
   int rgb_ch;
   ShadeParams S;
+  const ShadeRec* srec;
+  int64_t F;     // faces of the shared mesh: record id rid = n*F + face
   const ViewRec* views;
-  float* gface;   // (F, ACC)
-  float* rt_part; // (N*NB, 12)
+  float4* prec;  // (N, H*W, MR_BWD_REC) per covered pixel
+  float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
+  float* rt_part;  // (N, NB*4, 12) per-wave R/T partial sums
 };
 
-template <int ACC>
-__global__ void __launch_bounds__(256) k_render_bwd(RenderBwdParams P) {
-  __shared__ LdsAcc<ACC> L;
-  __shared__ float red[4][12];
+__global__ void __launch_bounds__(256) k_bwd_shade(RenderBwdParams P) {
   const int n = blockIdx.y;
   const int cntp = P.pcnt[n];
+  const int64_t HW = (int64_t)P.H * P.W;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < cntp; i += P.NB * 256) {
+    const int2 q = P.plist[n * HW + i];
+    const int px = q.x % P.W, py = q.x / P.W;
+    const int64_t pix = n * HW + q.x;
+    // every load that depends only on the list entry is issued here, together
+    const FaceRec r = P.recs[q.y];
+    PixGeom G;
+    load_geom(P.srec, (uint32_t)(q.y - n * P.F), G);
+    const float gD = P.gD ? P.gD[pix] : 0.0f;
+    const float gS = P.gS ? P.gS[pix] : 0.0f;
+    float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
+    if (P.gRGB) {
+      const float* g = P.gRGB + pix * P.rgb_ch;
+      gC[0] = g[0];
+      gC[1] = g[1];
+      gC[2] = g[2];
+      if (P.rgb_ch == 4) gA = g[3];
+    }
+    FragEval e;
+    float4* o4 = P.prec + (n * HW + i) * MR_BWD_REC;
+    if (!eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
+      // unreachable (the list holds kept fragments); a zero record contributes nothing
+      for (int k = 0; k < MR_BWD_REC; ++k) o4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      continue;
+    }
+    ShadeOut o;
+    ShadeCache C;
+    shade_fwd(P.S, n, true, G, e.b0, e.b1, e.b2, e.pz, e.sdist, o, C);
+    ShadeGrad SG;
+    shade_bwd(P.S, G, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
+    o4[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
+    o4[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
+    o4[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
+    o4[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
+    o4[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
+  }
+}
+
+template <int ACC>
+__global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
+  __shared__ float lrow[4][64 * ACC];
+  __shared__ int lkey[4][64];
+  const int n = blockIdx.y;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cntp = P.pcnt[n];
+  const int64_t HW = (int64_t)P.H * P.W;
   float gR[9], gT[3];
   for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
   for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
-  if ((int64_t)blockIdx.x * 256 >= cntp) {  // uniform over the workgroup: nothing to do
-    if (threadIdx.x < 12) P.rt_part[((int64_t)n * P.NB + blockIdx.x) * 12 + threadIdx.x] = 0.0f;
-    return;
-  }
-  acc_init(L);
-  __syncthreads();
-  const ViewRec V = P.views[n];
-  const int64_t HW = (int64_t)P.H * P.W;
-  // grid-stride over 256-pixel chunks of view n's compact covered-pixel list (one pixel per thread)
-  for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < cntp; c0 += (int64_t)gridDim.x * 256) {
-    {
-      const int64_t idx = c0 + threadIdx.x;
-      if (idx >= cntp) continue;
-      const int q = P.plist[n * HW + idx];
-      const int px = q % P.W, py = q / P.W;
-      const int64_t pix = n * HW + q;
-      const int rid = P.p2f32[pix];
-      if (rid < 0) continue;
-      const FaceRec r = P.recs[rid];
-      const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
-      FragEval e;
-      if (!eval_face(r, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e)) continue;
-      PixGeom G;
-      gather_geom(P.S, r.face, G);
-      ShadeOut o;
-      ShadeCache C;
-      shade_fwd(P.S, n, true, G, e.b0, e.b1, e.b2, e.pz, e.sdist, o, C);
-      const float gD = P.gD ? P.gD[pix] : 0.0f;
-      const float gS = P.gS ? P.gS[pix] : 0.0f;
-      float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
-      if (P.gRGB) {
-        const float* g = P.gRGB + pix * P.rgb_ch;
-        gC[0] = g[0];
-        gC[1] = g[1];
-        gC[2] = g[2];
-        if (P.rgb_ch == 4) gA = g[3];
-      }
-      ShadeGrad SG;
-      shade_bwd(P.S, G, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
-      float gfv[3][3];
-      raster_bwd_pixel(r, xf, yf, P.persp, P.clipb, SG.gz, SG.gb, SG.gsd, gfv);
+  if (blockIdx.x * 256 < cntp) {  // uniform over the workgroup
+    const ViewRec V = P.views[n];
+    for (int c0 = blockIdx.x * 256; c0 < cntp; c0 += P.NB * 256) {
+      const int i = c0 + threadIdx.x;
       float row[ACC];
-      for (int c = 0; c < 3; ++c) {
-        float gX[3];
-        project_bwd(V, G.X[c], gfv[c], gX, gR, gT);
-        for (int a = 0; a < 3; ++a) {
-          row[3 * c + a] = SG.gX[c][a] + gX[a];
-          row[9 + 3 * c + a] = SG.gN[c][a];
-          if (ACC == 27) row[18 + 3 * c + a] = SG.gC[c][a];
+#pragma unroll
+      for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
+      int key = -1;
+      if (i < cntp) {
+        const int2 q = P.plist[n * HW + i];
+        const int px = q.x % P.W, py = q.x / P.W;
+        const int face = (int)(q.y - n * P.F);
+        const FaceRec r = P.recs[q.y];
+        const float4* p4 = P.prec + (n * HW + i) * MR_BWD_REC;
+        const float4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
+        const float4 a4 = ACC == 27 ? p4[4] : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
+        const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
+        const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+        const float gb[3] = {a0.z, a0.w, a1.x};
+        const float gP[3] = {a1.y, a1.z, a1.w};
+        const float gNn[3] = {a2.x, a2.y, a2.z};
+        const float b[3] = {a2.w, a3.x, a3.y};
+        const float gt[3] = {a3.z, a3.w, a4.x};
+        float gfv[3][3];
+        raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+        key = face;
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+          float gX[3];
+          project_bwd(V, X[c], gfv[c], gX, gR, gT);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            row[3 * c + k] = b[c] * gP[k] + gX[k];
+            row[9 + 3 * c + k] = b[c] * gNn[k];
+            if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt[k];
+          }
         }
       }
-      acc_add<ACC>(L, P.gface, (int)r.face, row);
+      seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     }
   }
-  // per-view R/T partial sums: wave shuffle + LDS across the 4 waves
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // per-view R/T: wave reduction into this wave's partial slot (no atomics; k_rt_reduce sums)
+#pragma unroll
   for (int i = 0; i < 12; ++i) {
     float v = i < 9 ? gR[i] : gT[i - 9];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) red[wave][i] = v;
+    if (lane == i) P.rt_part[((int64_t)n * P.NB * 4 + blockIdx.x * 4 + wave) * 12 + i] = v;
   }
-  __syncthreads();
-  if (threadIdx.x < 12) {
-    const int i = threadIdx.x;
-    P.rt_part[((int64_t)n * P.NB + blockIdx.x) * 12 + i] = ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i];
-  }
-  acc_flush(L, P.gface);
 }
 
+// grad_views[n] = sum of view n's NST partial rows (fixed order: deterministic).
 __global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, int NST, float* __restrict__ out) {
-  __shared__ float s[256];
-  const int n = blockIdx.x;
+  __shared__ float s[12][4];
+  const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int i = 0; i < 12; ++i) {
     float v = 0.0f;
     for (int t = threadIdx.x; t < NST; t += 256) v += part[((int64_t)n * NST + t) * 12 + i];
-    s[threadIdx.x] = v;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) out[n * 12 + i] = s[0];
-    __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) s[i][wave] = v;
   }
+  __syncthreads();
+  if (threadIdx.x < 12) out[n * 12 + threadIdx.x] = ((s[threadIdx.x][0] + s[threadIdx.x][1]) + s[threadIdx.x][2]) + s[threadIdx.x][3];
 }
 
 // ---------------------------------------------------------------------------
@@ -1338,11 +1449,11 @@ extern "C" {
 const char* mr_last_error(void) { return g_err; }
 
 #ifdef MR_PROF
-// Debug-only (MR_PROF builds): device buffer of N*strips*8*16 u64 for k_raster phase stamps.
 int32_t mr_debug_set_prof(void* buf) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), &buf, sizeof(buf)) == hipSuccess ? MR_OK : MR_ELAUNCH;
 }
 #endif
+
 int32_t mr_version(void) { return 1; }
 
 static int check_settings(const mr_raster_settings_t* s) {
@@ -1360,7 +1471,7 @@ size_t mr_rasterize_meshes_workspace(int64_t num_meshes, int64_t total_faces, in
                                      int32_t max_faces_per_bin) {
   const int64_t Ftot = total_faces > 0 ? total_faces : 1;
   BinGeom g = bin_geom(H, W, num_meshes, Ftot, max_faces_per_bin);
-  return carve_raster_ws(nullptr, num_meshes, Ftot, H, W, g, false).bytes;
+  return carve_raster_ws(nullptr, num_meshes, Ftot, H, W, g).bytes;
 }
 
 static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, const RasterWS& w) {
@@ -1374,31 +1485,62 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.cnt = w.cnt;
   P.cur = w.cur;
   P.list = w.list;
+  P.vtot = w.vtot;
   P.vbase = w.vbase;
   return P;
 }
 
-static RasterParams make_raster(const mr_raster_settings_t* s, const BinGeom& g, int64_t N) {
-  RasterParams P;
+static RasterCfg make_cfg(const mr_raster_settings_t* s, const int64_t* view_first, int64_t F) {
+  RasterCfg c;
+  c.H = s->H; c.W = s->W;
+  c.blur = s->blur_radius;
+  c.bbox_pad = sqrtf(s->blur_radius);
+  c.persp = s->perspective_correct;
+  c.clipb = s->clip_barycentric_coords;
+  c.view_first = view_first;
+  c.F = F;
+  return c;
+}
+
+static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, const int64_t* view_count, int64_t F,
+                       hipStream_t st) {
+  ScanParams P;
+  P.T = g.T; P.list_cap = g.list_cap;
+  P.cnt = w.cnt; P.vtot = w.vtot; P.start = w.start; P.cur = w.cur; P.vbase = w.vbase;
+  P.tdone = w.tdone; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
+  P.view_count = view_count; P.F = F;
+  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan<<<(unsigned)N, 1024, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_bin_scan");
+  return MR_OK;
+}
+
+static OutParams make_out(const RasterCfg& c, const RasterWS& w, int64_t N) {
+  OutParams P;
   memset(&P, 0, sizeof(P));
-  P.N = (int)N; P.H = s->H; P.W = s->W;
-  P.TX = g.TX; P.TY = g.TY; P.T = g.T;
-  P.list_cap = g.list_cap;
-  P.blur = s->blur_radius;
-  P.bbox_pad = sqrtf(s->blur_radius);
-  P.persp = s->perspective_correct;
-  P.clipb = s->clip_barycentric_coords;
+  P.N = (int)N; P.H = c.H; P.W = c.W;
+  P.blur = c.blur; P.bbox_pad = c.bbox_pad;
+  P.persp = c.persp; P.clipb = c.clipb;
+  P.recs = w.recs; P.pcnt = w.pcnt; P.plist = w.plist;
   return P;
 }
 
-static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, hipStream_t st) {
-  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_views<<<(unsigned)N, 1024, 0, st>>>(w.cnt, g.T, w.start, w.cur, w.vtot, g.TX, g.GX, g.S,
-                                                                   N * g.S, w.scount, w.work, w.wctr)));
-  MR_CHECK_LAUNCH("k_bin_scan_views");
-  MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan_base<<<1, 64, 0, st>>>(w.vtot, (int)N, w.vbase)));
-  MR_CHECK_LAUNCH("k_bin_scan_base");
+extern "C++" {
+// Output stage shared by both entry points, in stream order: k_fill_bg (every pixel gets
+// the background), `geometry` (binning + raster, a callable), k_shade (covered pixels).
+template <int MODE, int CH, typename Geo>
+static int run_with_outputs(const OutParams& P, int64_t N, hipStream_t st, Geo geometry) {
+  const int64_t HW = (int64_t)P.H * P.W;
+  const dim3 fgrid(blocks_per_view(N, 4096, ceil_div(HW, 1024)), (unsigned)N);
+  MR_TIMED(MODE == 0 ? KID_FILL_FRAG : KID_FILL_RENDER, st, (k_fill_bg<MODE, CH><<<fgrid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_fill_bg");
+  const int rc = geometry();
+  if (rc) return rc;
+  const dim3 sgrid(blocks_per_view(N, 4096, ceil_div(HW, 256)), (unsigned)N);
+  MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sgrid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_shade");
   return MR_OK;
 }
+}  // extern "C++"
 
 int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const int64_t* count, int64_t N,
                             int64_t Ftot, const mr_raster_settings_t* s, int64_t* p2f, float* zbuf, float* bary,
@@ -1407,30 +1549,36 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   if (rc) return rc;
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "num_meshes must be in [1, 65535] (got %lld)", (long long)N);
   if (Ftot < 0 || Ftot >= (1ll << 31)) return set_err(MR_EINVAL, "total_faces out of range");
+  if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
   if (!p2f || !zbuf || !bary || !dists || !first || !count || (Ftot > 0 && !face_verts))
     return set_err(MR_EINVAL, "NULL tensor argument");
   hipStream_t st = (hipStream_t)stream;
   const int64_t Fb = Ftot > 0 ? Ftot : 1;
   BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g, false);
+  RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
-  if (Ftot > 0) {
-    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
-    MR_CHECK_LAUNCH("k_bin_count_fv");
-  }
-  if ((rc = launch_scan(w, N, g, st))) return rc;
-  if (Ftot > 0) {
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
-    MR_CHECK_LAUNCH("k_bin_fill_fv");
-  }
-  RasterParams P = make_raster(s, g, N);
-  P.view_first = first;
-  P.view_count = count;
+  const RasterCfg cfg = make_cfg(s, first, 0);
+  OutParams P = make_out(cfg, w, N);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
-  if ((rc = launch_raster<0, 3>(P, w, g, N, KID_RASTER_FRAG, st))) return rc;
-  return MR_OK;
+  return run_with_outputs<0, 3>(P, N, st, [&]() -> int {
+    int rc2;
+    const bool lds = g.T <= MR_LDS_HIST;
+    const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+    if (Ftot > 0) {
+      if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
+      else MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
+      MR_CHECK_LAUNCH("k_bin_count_fv");
+    }
+    if ((rc2 = launch_scan(w, N, g, count, 0, st))) return rc2;
+    if (Ftot > 0) {
+      if (lds) MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, Ftot, first, N)));
+      else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
+      MR_CHECK_LAUNCH("k_bin_fill_fv");
+    }
+    return launch_tile_raster(make_tile(cfg, g, w), g.unit_cap, st);
+  });
 }
 
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
@@ -1541,7 +1689,7 @@ static int check_mesh(const mr_mesh_t* m, const mr_shade_params_t* sp) {
 
 size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin) {
   BinGeom g = bin_geom(H, W, N, N * F, max_faces_per_bin);
-  return carve_raster_ws(nullptr, N, N * F, H, W, g, true).bytes;
+  return carve_raster_ws(nullptr, N, N * F, H, W, g, F).bytes;
 }
 
 int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
@@ -1554,46 +1702,49 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if ((int64_t)N * m->F >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
   if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
-  if (!p2f32 || !views) return set_err(MR_EINVAL, "NULL output");
+  if (!views) return set_err(MR_EINVAL, "NULL views");
   if ((sp->out_flags & MR_OUT_DEPTH) && !depth) return set_err(MR_EINVAL, "depth output NULL");
   if ((sp->out_flags & MR_OUT_SIL) && !sil) return set_err(MR_EINVAL, "silhouette output NULL");
   if ((sp->out_flags & MR_OUT_RGB) && !rgb) return set_err(MR_EINVAL, "rgb output NULL");
   if (sp->light_kind == 0 && (!cc || (ncc != 1 && ncc != N))) return set_err(MR_EINVAL, "camera centres");
   hipStream_t st = (hipStream_t)stream;
   BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, true);
+  RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, m->F);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
-  dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
-  const bool lds = g.T <= MR_LDS_HIST;
-  const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
-  if (lds)
-    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
-  else
-    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
-  MR_CHECK_LAUNCH("k_bin_count_world");
-  if ((rc = launch_scan(w, N, g, st))) return rc;
-  if (lds)
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
-  else
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
-  MR_CHECK_LAUNCH("k_bin_fill_world");
-  RasterParams P = make_raster(s, g, N);
-  P.F = m->F;
+  const RasterCfg cfg = make_cfg(s, nullptr, m->F);
+  OutParams P = make_out(cfg, w, N);
   P.S = make_shade(m, sp, cc, ncc);
   P.out_flags = sp->out_flags;
-  P.rgb_ch = sp->rgb_channels;
   P.depth = depth;
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  P.pcnt = w.pcnt;
-  P.plist = w.plist;
-  if (P.rgb_ch == 4) rc = launch_raster<1, 4>(P, w, g, N, KID_RASTER_RENDER, st);
-  else rc = launch_raster<1, 3>(P, w, g, N, KID_RASTER_RENDER, st);
-  if (rc) return rc;
-  return MR_OK;
+  P.srec = w.srec;
+  P.F = m->F;
+  auto geometry = [&]() -> int {
+    MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
+    MR_CHECK_LAUNCH("k_shade_rec");
+    dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
+    const bool lds = g.T <= MR_LDS_HIST;
+    const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+    if (lds)
+      MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+    else
+      MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+    MR_CHECK_LAUNCH("k_bin_count_world");
+    int rc2;
+    if ((rc2 = launch_scan(w, N, g, nullptr, m->F, st))) return rc2;
+    if (lds)
+      MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
+    else
+      MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
+    MR_CHECK_LAUNCH("k_bin_fill_world");
+    return launch_tile_raster(make_tile(cfg, g, w), g.unit_cap, st);
+  };
+  if (sp->rgb_channels == 4) return run_with_outputs<1, 4>(P, N, st, geometry);
+  return run_with_outputs<1, 3>(P, N, st, geometry);
 }
 
 // Backward workgroups per view: ~4096 in total, never more than the view's 256-pixel chunks.
@@ -1606,38 +1757,41 @@ static int bwd_blocks_per_view(int64_t N, int H, int W) {
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
   const int NB = bwd_blocks_per_view(N, H, W);
-  size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB, 256);
-  off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);
+  size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);        // gface
+  off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);           // gnu
+  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB * 4, 256); // rt_part
+  off = align_up(off + sizeof(float4) * MR_BWD_REC * (size_t)N * H * W, 256);  // prec
   return off;
 }
 
 int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_t* views, int64_t N, const float* cc,
                            int64_t ncc, const mr_raster_settings_t* s, const mr_shade_params_t* sp,
-                           const int32_t* p2f32, const float* gD, const float* gS, const float* gRGB,
-                           const void* fws, void* bws, size_t bws_bytes, float* gverts, float* gviews, float* gcol,
-                           void* stream) {
+                           const float* gD, const float* gS, const float* gRGB, const void* fws, void* bws,
+                           size_t bws_bytes, float* gverts, float* gviews, float* gcol, void* stream) {
   int rc = check_settings(s);
   if (rc) return rc;
   rc = check_mesh(m, sp);
   if (rc) return rc;
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
-  if (!p2f32 || !fws || !bws || !gverts || !gviews) return set_err(MR_EINVAL, "NULL argument");
+  if (!fws || !bws || !gverts || !gviews) return set_err(MR_EINVAL, "NULL argument");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
   const size_t need = mr_render_backward_workspace(N, m->V, m->F, s->H, s->W);
   if (bws_bytes < need) return set_err(MR_EWORKSPACE, "backward workspace too small");
   hipStream_t st = (hipStream_t)stream;
   BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, s->H, s->W, g, true);
+  RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, s->H, s->W, g, m->F);
   const bool vcol = m->tex_kind == 1;
   const int ACC = vcol ? 27 : 18;
   const int NB = bwd_blocks_per_view(N, s->H, s->W);
   char* b = (char*)bws;
-  float* gface = (float*)b;
-  size_t off = align_up(sizeof(float) * 27 * (size_t)m->F, 256);
-  float* rt_part = (float*)(b + off);
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB, 256);
+  size_t off = 0;
+  float* gface = (float*)(b + off);
+  off = align_up(sizeof(float) * 27 * (size_t)m->F, 256);
   float* gnu = (float*)(b + off);
+  off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
+  float* rt_part = (float*)(b + off);
+  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB * 4, 256);
+  float4* prec = (float4*)(b + off);
   if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
@@ -1646,7 +1800,6 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
   P.recs = w.recs;
-  P.p2f32 = p2f32;
   P.pcnt = w.pcnt;
   P.plist = w.plist;
   P.gD = (sp->out_flags & MR_OUT_DEPTH) ? gD : nullptr;
@@ -1654,14 +1807,19 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   P.gRGB = (sp->out_flags & MR_OUT_RGB) ? gRGB : nullptr;
   P.rgb_ch = sp->rgb_channels;
   P.S = make_shade(m, sp, cc, ncc);
+  P.srec = w.srec;
+  P.F = m->F;
   P.views = (const ViewRec*)views;
+  P.prec = prec;
   P.gface = gface;
   P.rt_part = rt_part;
   dim3 grid(NB, (unsigned)N);
-  if (vcol) MR_TIMED(KID_RENDER_BWD, st, (k_render_bwd<27><<<grid, 256, 0, st>>>(P)));
-  else MR_TIMED(KID_RENDER_BWD, st, (k_render_bwd<18><<<grid, 256, 0, st>>>(P)));
-  MR_CHECK_LAUNCH("k_render_bwd");
-  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, NB, gviews)));
+  MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<grid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_bwd_shade");
+  if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<grid, 256, 0, st>>>(P)));
+  else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<grid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_bwd_geom");
+  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, NB * 4, gviews)));
   MR_CHECK_LAUNCH("k_rt_reduce");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V, 256);

@@ -119,28 +119,69 @@ struct PixGeom {
   float Nv[3][3];  // vertex normals
   float uv[3][2];
   float col[3][3];
-  int32_t vi[3];
+};
+
+// Per-face shading inputs gathered once per call (k_shade_rec) so that per-pixel shading
+// reads them with one 144-B record load indexed by the face id, instead of the dependent
+// faces[f] -> verts / normals / uvs chain. A = uv (x, y, 0) or vertex colour per corner.
+struct __attribute__((aligned(16))) ShadeRec {
+  float X[9], N[9], A[9], pad[3];
 };
 
 MR_DEV void gather_geom(const ShadeParams& S, uint32_t face, PixGeom& G) {
+  // Every field is written on every path and every loop is unrolled: a conditionally
+  // initialised array element is otherwise demoted to scratch memory.
   const int32_t* fv = S.faces + 3 * (int64_t)face;
+  const int32_t* fu = S.faces_uvs + 3 * (int64_t)face;
+#pragma unroll
   for (int c = 0; c < 3; ++c) {
     const int32_t v = fv[c];
-    G.vi[c] = v;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
       G.X[c][k] = S.verts[3 * (int64_t)v + k];
       G.Nv[c][k] = S.light_kind == 0 ? S.vnormals[3 * (int64_t)v + k] : 0.0f;
+      G.col[c][k] = S.tex_kind == 1 ? S.vcolors[3 * (int64_t)v + k] : 0.0f;
     }
+    const int32_t t = S.tex_kind == 2 ? fu[c] : 0;
+    G.uv[c][0] = S.tex_kind == 2 ? S.verts_uvs[2 * (int64_t)t] : 0.0f;
+    G.uv[c][1] = S.tex_kind == 2 ? S.verts_uvs[2 * (int64_t)t + 1] : 0.0f;
   }
-  if (S.tex_kind == 2) {
-    const int32_t* fu = S.faces_uvs + 3 * (int64_t)face;
-    for (int c = 0; c < 3; ++c) {
-      G.uv[c][0] = S.verts_uvs[2 * (int64_t)fu[c]];
-      G.uv[c][1] = S.verts_uvs[2 * (int64_t)fu[c] + 1];
+}
+
+MR_DEV void make_shade_rec(const ShadeParams& S, uint32_t face, ShadeRec& R) {
+  PixGeom G;
+  gather_geom(S, face, G);
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      R.X[3 * c + k] = G.X[c][k];
+      R.N[3 * c + k] = G.Nv[c][k];
+      R.A[3 * c + k] = S.tex_kind == 1 ? G.col[c][k] : k < 2 ? G.uv[c][k] : 0.0f;
     }
-  } else if (S.tex_kind == 1) {
-    for (int c = 0; c < 3; ++c)
-      for (int k = 0; k < 3; ++k) G.col[c][k] = S.vcolors[3 * (int64_t)G.vi[c] + k];
+  R.pad[0] = R.pad[1] = R.pad[2] = 0.0f;
+}
+
+MR_DEV void load_geom(const ShadeRec* __restrict__ recs, uint32_t face, PixGeom& G) {
+  const float4* q = (const float4*)(recs + face);
+  float v[36];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const float4 x = q[i];
+    v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      G.X[c][k] = v[3 * c + k];
+      G.Nv[c][k] = v[9 + 3 * c + k];
+      G.col[c][k] = v[18 + 3 * c + k];
+    }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    G.uv[c][0] = v[18 + 3 * c];
+    G.uv[c][1] = v[18 + 3 * c + 1];
   }
 }
 
@@ -227,7 +268,8 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
 // dist, bary (b0..b2), per-corner world positions / normals / vertex colours.
 struct ShadeGrad {
   float gz, gsd, gb[3];
-  float gX[3][3], gN[3][3], gC[3][3];
+  float gX[3][3], gN[3][3], gC[3][3];  // per corner: b[c] * gP, b[c] * gNn, b[c] * gtex
+  float gP[3], gNn[3], gtex[3];        // grads of the interpolated point, normal, texel
 };
 
 MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1, float b2, float z,
@@ -309,6 +351,11 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
     normalize3_bwd(C.l, C.llen, C.lden, glh, gl);
     normalize3_bwd(C.v, C.vlen, C.vden, gvh, gvv);
     for (int k = 0; k < 3; ++k) gP[k] = -gl[k] - gvv[k];
+  }
+  for (int k = 0; k < 3; ++k) {
+    R.gP[k] = gP[k];
+    R.gNn[k] = gNn[k];
+    R.gtex[k] = S.tex_kind == 1 ? gtex[k] : 0.0f;
   }
   for (int c = 0; c < 3; ++c) {
     R.gb[c] += dot3(G.X[c], gP);

@@ -198,6 +198,7 @@ class ShadeConfig:
     want_sil: bool = True
     want_rgb: bool = True
     rgb_channels: int = 3
+    want_p2f: bool = False  # also return the (N,H,W) int32 packed face ids (tests / tools)
 
     def raster_struct(self):
         return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,
@@ -279,23 +280,25 @@ class RenderViews(torch.autograd.Function):
         depth = torch.empty((N, H, W), device=dev) if cfg.want_depth else None
         sil = torch.empty((N, H, W), device=dev) if cfg.want_sil else None
         rgb = torch.empty((N, H, W, cfg.rgb_channels), device=dev) if cfg.want_rgb else None
-        p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32)
+        p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
         wsb = L.mr_render_workspace(N, f.shape[0], H, W, rs.max_faces_per_bin)
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
         check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
                                   ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
                                   _lib.stream_handle(dev)))
-        ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, p2f, ws,
+        ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
                               vn if vn is not None else torch.empty(0, device=dev),
                               raw if raw is not None else torch.empty(0, device=dev))
         ctx.cfg, ctx.tex, ctx.has_vcol = cfg, tex, vcolors is not None
-        ctx.mark_non_differentiable(p2f)
         outs = [x for x in (depth, sil, rgb) if x is not None]
-        return (*outs, p2f)
+        if p2f is not None:
+            ctx.mark_non_differentiable(p2f)
+            outs.append(p2f)
+        return tuple(outs)
 
     @staticmethod
     def backward(ctx, *grads):
-        v, f, vcol, views, cc, p2f, ws, vn, raw = ctx.saved_tensors
+        v, f, vcol, views, cc, ws, vn, raw = ctx.saved_tensors
         cfg, tex = ctx.cfg, ctx.tex
         L = _lib.load()
         dev = v.device
@@ -326,7 +329,7 @@ class RenderViews(torch.autograd.Function):
         bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
         c = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
         check(L.mr_render_backward(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N, ptr(cc),
-                                   cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(p2f), ptr(c(gD)),
+                                   cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
                                    ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gviews),
                                    ptr(gcol), _lib.stream_handle(dev)))
         return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None)
@@ -334,7 +337,7 @@ class RenderViews(torch.autograd.Function):
 
 def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs | None = None,
                  vcolors=None):
-    """Functional entry: returns dict(depth, sil, rgb, pix_to_face32)."""
+    """Functional entry: returns dict(depth, sil, rgb[, pix_to_face32 when cfg.want_p2f])."""
     tex = tex or TextureArgs()
     outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex)
     res = {}
@@ -343,5 +346,6 @@ def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: T
         if want:
             res[name] = outs[i]
             i += 1
-    res["pix_to_face32"] = outs[i]
+    if cfg.want_p2f:
+        res["pix_to_face32"] = outs[i]
     return res

@@ -42,7 +42,7 @@ def texture_args(meshes: Meshes, need_color: bool):
 
 def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfig, cam_center=None):
     """Render every view of `meshes` (shared mesh or per-view meshes) with the fused kernels.
-    Returns dict(depth, sil, rgb, pix_to_face32) with tensors of batch N."""
+    Returns dict(depth, sil, rgb[, pix_to_face32 if cfg.want_p2f]) with tensors of batch N."""
     H, W = image_size
     n = max(len(meshes), R.reshape(-1, 3, 3).shape[0], T.reshape(-1, 3).shape[0])
     Rb, Tb, intr = view_batch(cameras, (H, W), R, T, n_views=n)

@@ -85,17 +85,29 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
                       f"torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
 
 
-# Algorithmic bytes per launch for each kernel that may dominate. `covered` =
-# covered pixels of the launch's batch (measured once, outside the timed region).
-def algorithmic_bytes(kernel, H, W, F, views, covered):
-    HW = H * W
-    if kernel == "k_resolve<1>":    # fused output stream: depth + sil + rgb (3 ch) = 20 B/px
-        return 20 * HW * views
-    if kernel == "k_resolve<0>":    # PyTorch3D fragments: p2f i64 + zbuf + bary + dists = 28 B/px
-        return 28 * HW * views
-    if kernel == "k_render_bwd":    # per covered pixel: upstream grads 20 B + list entry 8 B; face rows 72 B
-        return 28 * covered + 72 * F
-    return None
+# Algorithmic bytes per launch: what each kernel must move at minimum for the
+# launch's batch, from the forward's own work counters (kernels.render_stats: list entries,
+# covered pixels). Device-side caches may serve part of it; rocprof FETCH/WRITE is reported
+# beside it as roofline.traffic.
+def algorithmic_bytes(kernel, H, W, F, views, st):
+    HW, cov, ent = H * W, st["covered"], st["entries"]
+    table = {
+        "k_fill_bg<1>": 20 * HW * views,                   # depth + silhouette + rgb(3) of every pixel
+        "k_fill_bg<0>": 28 * HW * views,                   # p2f i64 + zbuf + bary(3) + dists
+        "k_tile_raster": 4 * ent + 64 * F * views + 8 * cov,  # list ids, each face record once, covered list
+        "k_shade<1>": 28 * cov,                            # list entry + 20 B of outputs per covered pixel
+        "k_bwd_shade": (8 + 20 + 80) * cov,                # list + upstream grads, 80-B gradient record out
+        "k_bwd_geom": (8 + 80) * cov + 72 * F,             # list + gradient record in, per-face rows out
+        "k_bin_count": 64 * F * views + 24 * F,            # face records out, mesh in
+        "k_bin_fill": 64 * F * views + 4 * ent,            # face records in, list ids out
+    }
+    return table.get(kernel)
+
+
+# Forward fragment pass (everything from projected geometry to the three images): API-minimum
+# bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
+FORWARD_KERNELS = ("k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
+                   "k_fill_bg<1>", "k_shade<1>")
 
 
 # SURVEY.md §8d API-minimum traffic of the whole fwd+bwd path per frame
@@ -113,6 +125,8 @@ def main():
     ap.add_argument("--mesh", default="cow")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-views", type=int, default=2)
+    ap.add_argument("--eager", action="store_true",
+                    help="enqueue every step from Python instead of replaying one captured HIP graph")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,23 +163,57 @@ def main():
     gS = (torch.rand(nv, H, W, generator=gen) * 2 - 1).to(dev)
     gC = (torch.rand(nv, H, W, 3, generator=gen) * 2 - 1).to(dev)
 
-    def step():
+    def fwd_bwd():
+        depth, sil, rgb = renderer.render(bmesh, R_cv, t_cv)
+        torch.autograd.backward([depth, sil, rgb], [gD, gS, gC])
+
+    def eager_step():
         verts.grad = None
         R_cv.grad = None
         t_cv.grad = None
-        depth, sil, rgb = renderer.render(bmesh, R_cv, t_cv)
-        torch.autograd.backward([depth, sil, rgb], [gD, gS, gC])
+        fwd_bwd()
+
+    for _ in range(args.warmup):
+        eager_step()
+        if world > 1:
+            D.allreduce_grads([verts])
+    from torch_renderer_amd.kernels import render_stats
+    _keep = renderer.render(bmesh, R_cv, t_cv)  # autograd keeps the forward workspace alive
+    wstats = render_stats()  # work counters of this rank's batch (bytes of data-dependent kernels)
+    del _keep
+    torch.cuda.synchronize()
+
+    # One step = fwd+bwd of the rank's views (+ the shared-vertex-gradient all-reduce when N > 1).
+    # Default: the fwd+bwd kernels are captured once into a HIP graph and replayed (every kernel
+    # of the step runs each replay; only the Python/launch enqueue work is removed). The
+    # collective stays outside the graph.
+    if args.eager:
+        run_fwd_bwd = eager_step
+    else:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                eager_step()
+        torch.cuda.current_stream().wait_stream(side)
+        verts.grad = None
+        R_cv.grad = None
+        t_cv.grad = None
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd_bwd()
+        run_fwd_bwd = graph.replay
+
+    def step():
+        run_fwd_bwd()
         if world > 1:
             D.allreduce_grads([verts])  # the step's only exchange: shared vertex grads
 
-    for _ in range(args.warmup):
+    for _ in range(2):
         step()
-    with torch.no_grad():  # covered pixels of this rank's batch (roofline bytes of the backward)
-        covered = int((renderer.render(bmesh, R_cv, t_cv)[0] > 0).sum().item())
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    _lib.timing_enable(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -173,12 +221,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kt = _lib.timing_read()
-    _lib.timing_enable(False)
     if world > 1:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
+    # per-kernel device times: HIP events around every launch of a few eager steps (same kernels)
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    for _ in range(min(args.steps, 20)):
+        eager_step()
+    torch.cuda.synchronize()
+    kt = _lib.timing_read()
+    _lib.timing_enable(False)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -189,23 +243,28 @@ def main():
     # dominant kernel (by summed device time) and its roofline point
     dom = max(kt.items(), key=lambda kv: kv[1][1]) if kt else None
     roof = None
+    pmc = {}
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as fh:
+            pmc = json.load(fh)
     if dom is not None:
         name, (launches, total_ms) = dom
         avg_s = total_ms / launches / 1e3
-        b = algorithmic_bytes(name, H, W, Fn, nv, covered)
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as fh:
-                pmc = json.load(fh)
-            ent = pmc.get(name)
-            if ent and ent.get("config") == f"{args.mesh}-{H}x{W}-{nv}":
-                traffic = ent.get("hbm_bytes_per_launch")
+        b = algorithmic_bytes(name, H, W, Fn, nv, wstats)
+        ent = pmc.get(name)
+        traffic = ent.get("hbm_bytes_per_launch") if ent and ent.get("config") == f"{args.mesh}-{H}x{W}-{nv}" else None
         if b is not None:
             gbs = b / avg_s / 1e9
             roof = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": name,
                     "avg_launch_us": round(avg_s * 1e6, 2), "algorithmic_bytes_per_launch": b}
+    fwd_us = sum(kt[k][1] / kt[k][0] * 1e3 for k in FORWARD_KERNELS if k in kt)
+    fwd_bytes = (20 * H * W + 36 * Fn) * nv
+    fwd_roof = {"kernels": [k for k in FORWARD_KERNELS if k in kt], "us_per_launch": round(fwd_us, 2),
+                "algorithmic_bytes": fwd_bytes, "achieved": round(fwd_bytes / (fwd_us * 1e-6) / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)} if fwd_us > 0 else None
     kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2),
                    "share": round(v[1] / sum(x[1] for x in kt.values()), 3)} for k, v in kt.items()}
     pb = path_bytes_per_frame(H, W, Fn, d["texture_u8"].shape[0] * d["texture_u8"].shape[1], nv)
@@ -218,12 +277,14 @@ def main():
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "launch": "eager" if args.eager else "hipgraph",
         "data": "synthetic camera poses on the reference's cow mesh + texture (assets/cow.npz from data/cow_mesh)",
         "config": {"workload": f"{args.mesh} (F={Fn}, V={verts0.shape[0]}), {H}x{W}, {nv} views/GPU, fwd+bwd: "
                                "depth+silhouette+Phong RGB from one raster pass, grads to verts and per-view R,t",
                    "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "global_views": nv * world,
                    "parallelism": f"view-sharded x{world}"},
-        "roofline": roof, "path_roofline": path_roof, "cpu_baseline": cpu, "kernels": kernels,
+        "roofline": roof, "forward_roofline": fwd_roof, "path_roofline": path_roof, "cpu_baseline": cpu,
+        "work": wstats, "kernels": kernels,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

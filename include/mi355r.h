@@ -142,6 +142,13 @@ int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, con
                            float* grad_vcolors, void* stream);
 
 /* ---------------- instrumentation ---------------- */
+/* Work counters left in `workspace` by the last mr_render_forward / mr_rasterize_meshes that used it
+ * (same N, total faces, H, W, max_faces_per_bin). Synchronises `stream`; for benchmarks and tools.
+ * out[0] = (tile, face) list entries, out[1] = raster work units, out[2] = non-empty 8x8 tiles,
+ * out[3] = covered pixels. */
+int32_t mr_workspace_stats(const void* workspace, int64_t N, int64_t total_faces, int32_t H, int32_t W,
+                           int32_t max_faces_per_bin, int64_t* out, void* stream);
+
 /* Per-kernel timing with HIP events recorded on each launch's stream (bench.py).
  * enable=1 clears and starts collection; mr_timing_read synchronizes on the
  * recorded events and returns, per kernel id, launches and summed ms. */

@@ -30,6 +30,7 @@
 #include <stdio.h>
 #include <string.h>
 #include <stdarg.h>
+#include <stdlib.h>
 
 #include "../../include/mi355r.h"
 #include "mr_common.h"
@@ -243,6 +244,18 @@ MR_DEV int wave_incl_max(int v) {
 }
 MR_DEV int wave_sum(int v) { return __builtin_amdgcn_readlane(wave_incl_sum(v), 63); }
 
+// Sum of v over a 256-thread workgroup added to *dst with ONE atomic (thread 0). Uniform call.
+MR_DEV void block_add_256(int v, int* dst) {
+  __shared__ int part[4];
+  const int w = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = w;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int t = ((part[0] + part[1]) + part[2]) + part[3];
+    if (t) atomicAdd(dst, t);
+  }
+}
+
 // Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
 MR_DEV void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -360,10 +373,8 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
         }
     }
   }
-  const int tot = wave_sum(mine);
-  if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&P.vtot[n], tot);
+  block_add_256(mine, &P.vtot[n]);  // also the barrier before the histogram flush
   if (LDS) {
-    __syncthreads();
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
       if (hist[i]) atomicAdd(&P.cnt[(int64_t)n * P.T + i], hist[i]);
   }
@@ -454,9 +465,7 @@ __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float
     }
   }
   if (lds) {
-    const int tot = wave_sum(mine);
-    if ((threadIdx.x & 63) == 0 && tot) atomicAdd(&P.vtot[n0], tot);
-    __syncthreads();
+    block_add_256(mine, &P.vtot[n0]);
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
       if (hist[i]) atomicAdd(&P.cnt[(int64_t)n0 * P.T + i], hist[i]);
   } else if (mine) {
@@ -1831,6 +1840,33 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");
+  return MR_OK;
+}
+
+int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, int32_t W, int32_t mfpb, int64_t* out,
+                           void* stream) {
+  if (!ws || !out || N <= 0 || N > 65535) return set_err(MR_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  BinGeom g = bin_geom(H, W, N, Ftot > 0 ? Ftot : 1, mfpb);
+  RasterWS w = carve_raster_ws((void*)ws, N, Ftot > 0 ? Ftot : 1, H, W, g);
+  const size_t n = 2 * (size_t)N + CTR_COUNT;  // pcnt, vtot, ctr are contiguous
+  int* h = (int*)malloc(sizeof(int) * n);
+  if (!h) return set_err(MR_EINVAL, "out of host memory");
+  if (hipMemcpyAsync(h, w.pcnt, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess) {
+    free(h);
+    return set_err(MR_ELAUNCH, "stats copy failed");
+  }
+  int64_t cov = 0, ent = 0;
+  for (int64_t i = 0; i < N; ++i) {
+    cov += h[i];
+    ent += h[N + i];
+  }
+  out[0] = ent;
+  out[1] = h[2 * N + CTR_UNITS];
+  out[2] = h[2 * N + CTR_SLOTS];
+  out[3] = cov;
+  free(h);
   return MR_OK;
 }
 

@@ -7,6 +7,7 @@ path: CPU tensors raise.
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass
 
 import numpy as np
@@ -16,6 +17,7 @@ from . import _lib
 from ._lib import MrMesh, MrRasterSettings, MrShadeParams, check, ptr
 
 _ADJ_CACHE: dict = {}
+_LAST_RENDER = None  # (weakref to the last fused forward's workspace, its geometry) for render_stats()
 
 
 def _require_cuda(*ts):
@@ -24,13 +26,7 @@ def _require_cuda(*ts):
             raise RuntimeError("mi355r: the MI355X path needs HIP device tensors (no CPU fallback)")
 
 
-def vertex_adjacency(faces: torch.Tensor, V: int):
-    """CSR vertex -> (face << 2 | corner) entries sorted by (corner, face): the
-    summation order of Meshes.verts_normals_packed's three index_add calls."""
-    key = (faces.data_ptr(), tuple(faces.shape), int(V), faces.device, getattr(faces, "_version", 0))
-    hit = _ADJ_CACHE.get(key)
-    if hit is not None:
-        return hit
+def _build_adjacency(faces: torch.Tensor, V: int):
     f = faces.detach().to("cpu", torch.int64).numpy()
     Fn = f.shape[0]
     vert = f.reshape(-1)
@@ -41,11 +37,31 @@ def vertex_adjacency(faces: torch.Tensor, V: int):
     ptr_ = np.zeros(V + 1, dtype=np.int32)
     np.cumsum(counts, out=ptr_[1:])
     adj = ((face[order] << 2) | corner[order]).astype(np.int32)
-    out = (torch.from_numpy(ptr_).to(faces.device), torch.from_numpy(adj).to(faces.device))
+    return torch.from_numpy(ptr_).to(faces.device), torch.from_numpy(adj).to(faces.device)
+
+
+def mesh_topology(faces: torch.Tensor, V: int):
+    """(faces int32 (F,3), vadj_ptr (V+1), vadj) of a faces tensor, built once per tensor.
+
+    The CSR lists vertex -> (face << 2 | corner) entries sorted by (corner, face): the
+    summation order of Meshes.verts_normals_packed's three index_add calls. Cached on the
+    identity and version of the caller's faces tensor (not on a data pointer), so a
+    captured HIP graph or a steady-state step does no host work and no host sync here."""
+    key = (id(faces), int(V))
+    hit = _ADJ_CACHE.get(key)
+    if hit is not None and hit[0]() is faces and hit[1] == faces._version:
+        return hit[2]
+    f32 = faces.detach().to(torch.int32).contiguous()
+    vptr, vadj = _build_adjacency(f32, V)
     if len(_ADJ_CACHE) > 64:
         _ADJ_CACHE.clear()
-    _ADJ_CACHE[key] = out
-    return out
+    _ADJ_CACHE[key] = (weakref.ref(faces), faces._version, (f32, vptr, vadj))
+    return f32, vptr, vadj
+
+
+def vertex_adjacency(faces: torch.Tensor, V: int):
+    """CSR vertex -> (face << 2 | corner) adjacency (see mesh_topology)."""
+    return mesh_topology(faces, V)[1:]
 
 
 def raster_settings_struct(H, W, K=1, blur=0.0, persp=True, clip=False, cull=False, max_faces_per_bin=None):
@@ -131,21 +147,20 @@ class ProjectFaces(torch.autograd.Function):
         _require_cuda(verts, R, T, faces)
         L = _lib.load()
         v = verts.detach().float().contiguous()
-        f = faces.to(torch.int32).contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
         views = make_views(R.detach(), T.detach(), intr)
         N = views.shape[0]
         out = torch.empty((N * f.shape[0], 3, 3), device=v.device, dtype=torch.float32)
         check(L.mr_project_faces(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(views), N, ptr(out),
                                  _lib.stream_handle(v.device)))
-        ctx.save_for_backward(v, f, views)
+        ctx.save_for_backward(v, f, views, vptr, vadj)
         return out
 
     @staticmethod
     def backward(ctx, g):
-        v, f, views = ctx.saved_tensors
+        v, f, views, vptr, vadj = ctx.saved_tensors
         L = _lib.load()
         N = views.shape[0]
-        vptr, vadj = vertex_adjacency(f, v.shape[0])
         gv = torch.empty_like(v)
         gviews = torch.empty((N, 12), device=v.device)
         check(L.mr_project_faces_backward(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(vptr), ptr(vadj), ptr(views),
@@ -157,10 +172,13 @@ class ProjectFaces(torch.autograd.Function):
 def vertex_normals(verts, faces):
     """(normals, raw sums) — Meshes.verts_normals_packed on the GPU (no autograd)."""
     _require_cuda(verts, faces)
-    L = _lib.load()
     v = verts.detach().float().contiguous()
-    f = faces.to(torch.int32).contiguous()
-    vptr, vadj = vertex_adjacency(f, v.shape[0])
+    f, vptr, vadj = mesh_topology(faces, v.shape[0])
+    return _vertex_normals(v, f, vptr, vadj)
+
+
+def _vertex_normals(v, f, vptr, vadj):
+    L = _lib.load()
     vn = torch.empty_like(v)
     raw = torch.empty_like(v)
     check(L.mr_vertex_normals(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(vptr), ptr(vadj), ptr(vn), ptr(raw),
@@ -264,15 +282,14 @@ class RenderViews(torch.autograd.Function):
         L = _lib.load()
         dev = verts.device
         v = verts.detach().float().contiguous()
-        f = faces.to(torch.int32).contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
         vcol = vcolors.detach().float().contiguous() if vcolors is not None else None
         views = make_views(R.detach(), T.detach(), intr)
         N = views.shape[0]
         H, W = cfg.H, cfg.W
-        vptr, vadj = vertex_adjacency(f, v.shape[0])
         vn = raw = None
         if cfg.light_kind == 0:
-            vn, raw = vertex_normals(v, f)
+            vn, raw = _vertex_normals(v, f, vptr, vadj)
         cc = cam_centers.float().contiguous().reshape(-1, 3)
         rs = cfg.raster_struct()
         sp = cfg.shade_struct()
@@ -283,12 +300,14 @@ class RenderViews(torch.autograd.Function):
         p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
         wsb = L.mr_render_workspace(N, f.shape[0], H, W, rs.max_faces_per_bin)
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        global _LAST_RENDER
+        _LAST_RENDER = (weakref.ref(ws), (N, N * f.shape[0], H, W, rs.max_faces_per_bin))
         check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
                                   ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
                                   _lib.stream_handle(dev)))
         ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
                               vn if vn is not None else torch.empty(0, device=dev),
-                              raw if raw is not None else torch.empty(0, device=dev))
+                              raw if raw is not None else torch.empty(0, device=dev), vptr, vadj)
         ctx.cfg, ctx.tex, ctx.has_vcol = cfg, tex, vcolors is not None
         outs = [x for x in (depth, sil, rgb) if x is not None]
         if p2f is not None:
@@ -298,7 +317,7 @@ class RenderViews(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        v, f, vcol, views, cc, ws, vn, raw = ctx.saved_tensors
+        v, f, vcol, views, cc, ws, vn, raw, vptr, vadj = ctx.saved_tensors
         cfg, tex = ctx.cfg, ctx.tex
         L = _lib.load()
         dev = v.device
@@ -318,7 +337,6 @@ class RenderViews(torch.autograd.Function):
         cfg2.want_depth = gD is not None
         cfg2.want_sil = gS is not None
         cfg2.want_rgb = gC is not None
-        vptr, vadj = vertex_adjacency(f, v.shape[0])
         mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None)
         rs = cfg2.raster_struct()
         sp = cfg2.shade_struct()
@@ -349,3 +367,16 @@ def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: T
     if cfg.want_p2f:
         res["pix_to_face32"] = outs[i]
     return res
+
+
+def render_stats():
+    """Work counters of the most recent fused forward whose workspace is still alive (kept by
+    autograd until backward): dict(entries, units, tiles, covered). Synchronises; for tools."""
+    if _LAST_RENDER is None or _LAST_RENDER[0]() is None:
+        raise RuntimeError("no live fused-render workspace")
+    ws = _LAST_RENDER[0]()
+    N, Ft, H, W, mfpb = _LAST_RENDER[1]
+    out = (ctypes.c_int64 * 4)()
+    check(_lib.load().mr_workspace_stats(ptr(ws), N, Ft, H, W, mfpb, ctypes.cast(out, ctypes.c_void_p),
+                                         _lib.stream_handle(ws.device)))
+    return {"entries": out[0], "units": out[1], "tiles": out[2], "covered": out[3]}

@@ -90,14 +90,14 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
 # covered pixels). Device-side caches may serve part of it; rocprof FETCH/WRITE is reported
 # beside it as roofline.traffic.
 def algorithmic_bytes(kernel, H, W, F, views, st):
-    HW, cov, ent = H * W, st["covered"], st["entries"]
+    HW, cov, ent, slots = H * W, st["covered"], st["entries"], st["tiles"]
     table = {
-        "k_fill_bg<1>": 20 * HW * views,                   # depth + silhouette + rgb(3) of every pixel
-        "k_fill_bg<0>": 28 * HW * views,                   # p2f i64 + zbuf + bary(3) + dists
-        "k_tile_raster": 4 * ent + 64 * F * views + 8 * cov,  # list ids, each face record once, covered list
-        "k_shade<1>": 28 * cov,                            # list entry + 20 B of outputs per covered pixel
-        "k_bwd_shade": (8 + 20 + 80) * cov,                # list + upstream grads, 80-B gradient record out
-        "k_bwd_geom": (8 + 80) * cov + 72 * F,             # list + gradient record in, per-face rows out
+        # background of every pixel (depth + silhouette + rgb(3)), list ids, each face record once,
+        # 64 winners per non-empty tile
+        "k_tile_raster": 20 * HW * views + 4 * ent + 64 * F * views + 256 * slots,
+        "k_shade<1>": 256 * slots + 20 * cov,              # winners in, 20 B of outputs per covered pixel
+        "k_bwd_shade": 256 * slots + (20 + 80) * cov,      # winners + upstream grads, 80-B gradient record out
+        "k_bwd_geom": 256 * slots + 80 * cov + 72 * F,     # winners + gradient record in, per-face rows out
         "k_bin_count": 64 * F * views + 24 * F,            # face records out, mesh in
         "k_bin_fill": 64 * F * views + 4 * ent,            # face records in, list ids out
     }
@@ -107,7 +107,7 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
 # Forward fragment pass (everything from projected geometry to the three images): API-minimum
 # bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
 FORWARD_KERNELS = ("k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
-                   "k_fill_bg<1>", "k_shade<1>")
+                   "k_shade<1>")
 
 
 # SURVEY.md §8d API-minimum traffic of the whole fwd+bwd path per frame

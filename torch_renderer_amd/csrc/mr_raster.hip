@@ -59,12 +59,11 @@ static int set_err(int code, const char* fmt, ...) {
 // Optional per-kernel timing: HIP events recorded on the launch stream around
 // every kernel while enabled (bench.py reads them to price the dominant kernel).
 // ---------------------------------------------------------------------------
-enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_FILL_FRAG, KID_FILL_RENDER,
-                KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
+enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
-                                              "k_fill_bg<0>", "k_fill_bg<1>", "k_shade<0>", "k_shade<1>",
+                                              "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
@@ -121,7 +120,7 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // per-view list of covered (pixel, face) pairs.
 // ---------------------------------------------------------------------------
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
-enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COUNT = 4 };
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_COUNT = 4 };
 
 struct BinGeom {
   int TX, TY, T;
@@ -145,23 +144,25 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
 
 struct RasterWS {
   FaceRec* recs;
-  int* cnt;    // (N*T) entries per tile; zeroed per call together with pcnt, vtot, ctr
-  int* pcnt;   // (N) covered pixels per view (fused path)
+  int* cnt;    // (N*T) entries per tile; zeroed per call together with vtot and ctr
   int* vtot;   // (N) list entries per view
-  int* ctr;    // (CTR_COUNT) units / slots emitted by the scan
+  int* ctr;    // (CTR_COUNT) units / slots emitted by the scan, covered pixels
   int* start;  // (N*T) entry offset of each tile inside its view's region
   int* cur;    // (N*T) fill cursors
   int* vbase;  // (N) first list entry of each view (saturating)
-  int* tdone;  // (N*T) per slot: units of a shared slot still to finish (count-down; the last appends)
+  int* tdone;  // (N*T) per slot: units of a shared slot still to finish (count-down; the last writes)
+  int* vslot;  // (2N) first slot and number of slots of each view
+  int* stile;  // (N*T) per slot: view * T + tile
   int4* units; // (unit_cap) {view*T + tile, first list entry (-1: every face of the view), entries, slot | multi<<31}
   int* list;   // list_cap
   unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
-  int2* plist; // (N*H*W) covered (pixel, face record) pairs, view-major regions
+  int* sface;  // (N*T*64) per slot, per tile pixel (row-major 8x8): winning face record or -1
   ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
   size_t bytes;
 };
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
                                 int64_t Fshade = 0) {
+  (void)H; (void)W;
   RasterWS w;
   size_t off = 0;
   char* b = (char*)base;
@@ -169,10 +170,9 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   w.recs = (FaceRec*)(b + off);
   off = align_up(off + sizeof(FaceRec) * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.cnt = (int*)(b + off);
-  w.pcnt = w.cnt + NT;
-  w.vtot = w.pcnt + N;
+  w.vtot = w.cnt + NT;
   w.ctr = w.vtot + N;
-  off = align_up(off + sizeof(int) * (NT + 2 * (size_t)N + CTR_COUNT), 256);
+  off = align_up(off + sizeof(int) * (NT + (size_t)N + CTR_COUNT), 256);
   w.start = (int*)(b + off);
   off = align_up(off + sizeof(int) * NT, 256);
   w.cur = (int*)(b + off);
@@ -181,21 +181,25 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * (size_t)N, 256);
   w.tdone = (int*)(b + off);
   off = align_up(off + sizeof(int) * NT, 256);
+  w.vslot = (int*)(b + off);
+  off = align_up(off + sizeof(int) * 2 * (size_t)N, 256);
+  w.stile = (int*)(b + off);
+  off = align_up(off + sizeof(int) * NT, 256);
   w.units = (int4*)(b + off);
   off = align_up(off + sizeof(int4) * (size_t)g.unit_cap, 256);
   w.list = (int*)(b + off);
   off = align_up(off + sizeof(int) * (size_t)g.list_cap, 256);
   w.tkey = (unsigned long long*)(b + off);
   off = align_up(off + sizeof(unsigned long long) * 64 * NT, 256);
-  w.plist = (int2*)(b + off);
-  off = align_up(off + sizeof(int2) * (size_t)N * H * W, 256);
+  w.sface = (int*)(b + off);
+  off = align_up(off + sizeof(int) * 64 * NT, 256);
   w.srec = (ShadeRec*)(b + off);
   off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
   w.bytes = off;
   return w;
 }
 static size_t zero_bytes(int64_t N, const BinGeom& g) {
-  return sizeof(int) * ((size_t)N * g.T + 2 * (size_t)N + CTR_COUNT);
+  return sizeof(int) * ((size_t)N * g.T + (size_t)N + CTR_COUNT);
 }
 
 // ---------------------------------------------------------------------------
@@ -256,9 +260,12 @@ MR_DEV void block_add_256(int v, int* dst) {
   }
 }
 
-// Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads).
+// Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads). A wave's
+// LDS operations execute in program order, so a wavefront-scope fence (no instructions, a
+// compiler barrier) is all the ordering needed. A workgroup-scope fence here would emit
+// s_waitcnt vmcnt(0) and stall on the wave's outstanding global stores every time.
 MR_DEV void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -525,6 +532,8 @@ struct ScanParams {
   int* cur;
   int* vbase;
   int* tdone;
+  int* vslot;
+  int* stile;
   int4* units;
   int* ctr;
   unsigned long long* tkey;
@@ -585,6 +594,8 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
       for (int k = 0; k < 16; ++k) { au += part[k]; as += (int)red[k]; }
       base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
       base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
+      P.vslot[n] = base[1];
+      P.vslot[gridDim.x + n] = as;
     }
     __syncthreads();
   }
@@ -604,6 +615,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
     run_u += tu;
     run_s += ts;
     const int gt = n * P.T + tt;
+    if (ns) P.stile[slot] = gt;
     const int multi = nu > 1 ? (int)0x80000000u : 0;
     for (int k = 0; k < nu; ++k) {
       int4 U;
@@ -665,20 +677,34 @@ MR_DEV unsigned long long frag_key(float z, int f) {
   return ((unsigned long long)zb << 32) | (unsigned)f;
 }
 
-struct TileParams {
-  int H, W, TX, T;
+// Everything the forward kernels read and write (geometry, work lists, outputs).
+struct FwdParams {
+  int N, H, W, TX, T;
   float blur, bbox_pad;
   int persp, clipb;
   const int64_t* view_first;  // NULL: shared mode (overflow units scan faces n*F ..)
-  int64_t F;
+  int64_t F;                  // faces per view in shared mode (record id = n*F + face)
   const FaceRec* recs;
   const int* list;
   const int4* units;
-  const int* ctr;
+  int* ctr;
   unsigned long long* tkey;
   int* tdone;
-  int* pcnt;    // (N) covered pixels per view
-  int2* plist;  // (N, H*W) covered (pixel, face record) pairs
+  int* sface;       // (slots, 64) winning face record per tile pixel or -1
+  const int* stile; // (slots) view * T + tile
+  // MODE 0 outputs (PyTorch3D Fragments, K = 1)
+  int64_t* p2f;
+  float* zbuf;
+  float* bary;
+  float* dists;
+  // MODE 1 outputs
+  ShadeParams S;
+  const ShadeRec* srec;
+  int out_flags;
+  float* depth;
+  float* sil;
+  float* rgb;
+  int32_t* p2f32;  // optional
 };
 
 // One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).
@@ -691,6 +717,86 @@ struct WaveStage {
   float xs[MR_TS], ys[MR_TS];
 };
 
+// Background values of every output (view-independent: a pixel without a face has zero
+// blend weight, so depth = relu(-1) = 0, silhouette = 0, rgb = background, alpha = 0).
+struct Bg {
+  float d, s, c[4];
+};
+template <int MODE>
+MR_DEV Bg background(const FwdParams& P) {
+  Bg b;
+  b.d = b.s = -1.0f;
+  b.c[0] = b.c[1] = b.c[2] = b.c[3] = -1.0f;
+  if (MODE == 1) {
+    PixGeom G;
+    ShadeOut o;
+    ShadeCache C;
+    shade_fwd(P.S, 0, false, G, 0.f, 0.f, 0.f, 0.f, 0.f, o, C);
+    b.d = o.depth;
+    b.s = o.sil;
+    b.c[0] = o.rgb[0]; b.c[1] = o.rgb[1]; b.c[2] = o.rgb[2]; b.c[3] = o.alpha;
+  }
+  return b;
+}
+
+// Background of one 64-lane chunk of view n: 4 pixels per lane and 16-B vector stores when
+// W % 4 == 0 (every row then starts 16-B aligned), else one pixel per lane.
+template <int MODE, int CH>
+MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) {
+  const int lane = threadIdx.x & 63;
+  const int64_t HW = (int64_t)P.H * P.W;
+  if (vec) {
+    const int64_t g = (int64_t)c * 64 + lane;
+    if (g >= HW / 4) return;
+    const int64_t pix = (int64_t)n * HW + 4 * g;
+    if (MODE == 0) {
+      const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+      longlong2* q = (longlong2*)(P.p2f + pix);
+      q[0] = make_longlong2(-1ll, -1ll);
+      q[1] = make_longlong2(-1ll, -1ll);
+      *(float4*)(P.zbuf + pix) = m1;
+      *(float4*)(P.dists + pix) = m1;
+      float4* q3 = (float4*)(P.bary + pix * 3);
+      q3[0] = m1; q3[1] = m1; q3[2] = m1;
+    } else {
+      if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = make_float4(b.d, b.d, b.d, b.d);
+      if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = make_float4(b.s, b.s, b.s, b.s);
+      if (P.p2f32) *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
+      if (P.out_flags & MR_OUT_RGB) {
+        float4* q = (float4*)(P.rgb + pix * CH);
+        if (CH == 4) {
+          const float4 v = make_float4(b.c[0], b.c[1], b.c[2], b.c[3]);
+          q[0] = v; q[1] = v; q[2] = v; q[3] = v;
+        } else {
+          // 4 pixels x 3 channels = 3 aligned 16-B stores. Opaque copies keep the compiler from
+          // re-splitting the period-3 pattern into four unaligned 12-B stores.
+          float r0 = b.c[0], g0 = b.c[1], b0 = b.c[2], r1 = r0, g1 = g0, b1 = b0, r2 = r0, g2 = g0, b2 = b0;
+          asm volatile("" : "+v"(r1), "+v"(g1), "+v"(b1), "+v"(r2), "+v"(g2), "+v"(b2));
+          q[0] = make_float4(r0, g0, b0, r1);
+          q[1] = make_float4(g1, b1, r2, g2);
+          q[2] = make_float4(b2, r0, g0, b0);
+        }
+      }
+    }
+  } else {
+    const int64_t i = (int64_t)c * 64 + lane;
+    if (i >= HW) return;
+    const int64_t q = (int64_t)n * HW + i;
+    if (MODE == 0) {
+      P.p2f[q] = -1ll;
+      P.zbuf[q] = -1.0f;
+      P.dists[q] = -1.0f;
+      for (int k = 0; k < 3; ++k) P.bary[q * 3 + k] = -1.0f;
+    } else {
+      if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = b.d;
+      if (P.out_flags & MR_OUT_SIL) P.sil[q] = b.s;
+      if (P.p2f32) P.p2f32[q] = -1;
+      if (P.out_flags & MR_OUT_RGB)
+        for (int k = 0; k < CH; ++k) P.rgb[q * CH + k] = b.c[k];
+    }
+  }
+}
+
 // Persistent grid of independent waves (4 per workgroup, no workgroup barriers): wave g
 // takes units g, g + G, ... of the list k_bin_scan emitted (G = resident waves). Per unit:
 //  (1) one entry per lane: load its face record, clip the face's padded pixel bbox to the
@@ -700,12 +806,15 @@ struct WaveStage {
 //      face costs ~3 lanes, not a wave;
 //  (3) kept fragments meet in a per-pixel ds_min_u64 on the packed (z, face) key, which is
 //      order-independent and equals the CPU's "strictly nearer, earlier face wins";
-//  (4) a tile that is a single unit appends its covered pixels (pixel, winning face record)
-//      to the view's list straight from LDS (one atomic per wave); units sharing a tile
-//      merge their keys with global u64 atomicMin, and the last of them to finish (a
-//      count-down with agent-scope release/acquire) reads the merged keys back with
-//      returning atomics and appends.
-__global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
+//  (4) a tile that is a single unit writes its 64 winners (face record or -1) to its slot
+//      of sface straight from LDS; units sharing a tile merge their keys with global u64
+//      atomicMin, and the last of them to finish (an atomic count-down) reads the merged
+//      keys back with returning atomics and writes the slot.
+// The background of every pixel (k_shade later overwrites the covered ones) is written by
+// the same waves, a share of 64-lane chunks after each unit: the stores stream to HBM while
+// the raster work, which is latency-bound, leaves it idle.
+template <int MODE, int CH>
+__global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
   __shared__ WaveStage stage[4];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -719,8 +828,27 @@ __global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
   const bool fast_ok = !(blur > 0.0f);
 #endif
   const int H = P.H, W = P.W;
+  // background chunks of this wave: c = gw, gw + G, ... < N * cpv, spread over its units
+  const int gw = blockIdx.x * 4 + wave, G = gridDim.x * 4;
+  const bool vec = (W & 3) == 0;
+  const int64_t HW = (int64_t)H * W;
+  const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
+  const int nchunks = P.N * cpv;
+  const int my_chunks = gw < nchunks ? (nchunks - gw + G - 1) / G : 0;
+  const int my_units = gw < nunits ? (nunits - gw + G - 1) / G : 0;
+  const int per_unit = my_units > 0 ? (my_chunks + my_units - 1) / my_units : my_chunks;
+  const Bg bg = background<MODE>(P);
+  int chunk = gw;
+#ifdef MR_PROF
+  unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, npass = 0, nunit = 0;
+  unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long tstart = tp0;
+#define ACC(v) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); v += _t - tp0; tp0 = _t; } while (0)
+#else
+#define ACC(v) do {} while (0)
+#endif
 #pragma unroll 1
-  for (int u = blockIdx.x * 4 + wave; u < nunits; u += gridDim.x * 4) {
+  for (int u = gw; u < nunits; u += G) {
     const int4 U = P.units[u];
     const int n = U.x / P.T, t = U.x - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
@@ -755,12 +883,22 @@ __global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
         S.id[lane] = id;
       }
       // pair numbering
+      ACC(acc_load);
+      if (eb == 0) {  // this unit's share of background chunks: they drain during the passes
+#pragma unroll 1
+        for (int j = 0; j < per_unit && chunk < nchunks; ++j, chunk += G)
+          fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
+        ACC(acc_fill);
+      }
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
       S.meta[lane] = meta | pexcl;
 #pragma unroll 1
       for (int pb = 0; pb < NP; pb += 64) {
+#ifdef MR_PROF
+        ++npass;
+#endif
         wave_lds_sync();
         // the entry starting inside this pass marks its first slot; slot 0 belongs to the
         // entry straddling pb (the last non-empty entry starting at or before it)
@@ -792,11 +930,12 @@ __global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
         }
       }
       wave_lds_sync();  // the stage is rewritten by the next batch
+      ACC(acc_pass);
     }
     unsigned long long k = S.key[lane];
+    const int slot = U.w & 0x7fffffff;
     bool emit = true;
     if (U.w < 0) {  // tile shared by several units
-      const int slot = U.w & 0x7fffffff;
       unsigned long long* dst = P.tkey + (int64_t)slot * 64 + lane;
       // Device-scope atomics are performed at the memory side (never cached in an XCD's L2),
       // so agent atomics on both sides hand the keys over: this wave's 64 atomicMin are
@@ -814,41 +953,28 @@ __global__ void __launch_bounds__(256) k_tile_raster(TileParams P) {
       const int f = (int)(unsigned)(k & 0xffffffffull);
       const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
       const bool hit = f != MR_NONE && px < W && py < H;
-      const unsigned long long msk = __ballot(hit);
-      if (msk) {
-        int base = 0;
-        if (lane == 0) base = atomicAdd(&P.pcnt[n], __popcll(msk));
-        base = __shfl(base, 0, 64);
-        if (hit) P.plist[(int64_t)n * H * W + base + __popcll(msk & ((1ull << lane) - 1ull))] = make_int2(py * W + px, f);
-      }
+      P.sface[(int64_t)slot * 64 + lane] = hit ? f : -1;
+      const int nh = __popcll(__ballot(hit));
+      if (lane == 0 && nh) atomicAdd(&P.ctr[CTR_COVERED], nh);
     }
     wave_lds_sync();
+    ACC(acc_emit);
+#ifdef MR_PROF
+    ++nunit;
+#endif
   }
+#pragma unroll 1
+  for (; chunk < nchunks; chunk += G) fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
+  ACC(acc_fill);
+#ifdef MR_PROF
+  if (g_prof && lane == 0) {
+    unsigned long long* o = g_prof + (size_t)gw * 8;
+    o[0] = acc_load; o[1] = acc_pass; o[2] = acc_emit; o[3] = acc_fill;
+    o[4] = npass; o[5] = nunit; o[6] = __builtin_amdgcn_s_memtime() - tstart; o[7] = 1;
+  }
+#endif
+#undef ACC
 }
-
-// ---- outputs: background fill (every pixel) + shading of the covered-pixel list ----
-struct OutParams {
-  int N, H, W;
-  float blur, bbox_pad;
-  int persp, clipb;
-  const FaceRec* recs;
-  const int* pcnt;
-  const int2* plist;
-  // MODE 0 outputs (PyTorch3D Fragments, K = 1)
-  int64_t* p2f;
-  float* zbuf;
-  float* bary;
-  float* dists;
-  // MODE 1
-  ShadeParams S;
-  const ShadeRec* srec;
-  int64_t F;  // faces of the shared mesh (record id = n*F + face)
-  int out_flags;
-  float* depth;
-  float* sil;
-  float* rgb;
-  int32_t* p2f32;  // optional
-};
 
 // Per-face shading records of the shared mesh (one thread per face).
 __global__ void __launch_bounds__(256) k_shade_rec(ShadeParams S, int64_t F, ShadeRec* __restrict__ out) {
@@ -859,92 +985,32 @@ __global__ void __launch_bounds__(256) k_shade_rec(ShadeParams S, int64_t F, Sha
   out[f] = R;
 }
 
-// Background of every pixel (the covered ones are overwritten by k_shade afterwards):
-// a pure store stream, 4 pixels per thread and 16-B vector stores when W % 4 == 0.
+// Covered pixels: waves stride over the non-empty tiles' slots, one tile pixel per lane:
+// recompute the winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade
+// (M = 1) over the background k_tile_raster wrote.
 template <int MODE, int CH>
-__global__ void __launch_bounds__(256) k_fill_bg(OutParams P) {
-  const int n = blockIdx.y;
-  float bgd = -1.0f, bgs = -1.0f, bgv[4] = {-1.0f, -1.0f, -1.0f, -1.0f};
-  if (MODE == 1) {
-    PixGeom G;
-    ShadeOut o;
-    ShadeCache C;
-    shade_fwd(P.S, n, false, G, 0.f, 0.f, 0.f, 0.f, 0.f, o, C);
-    bgd = o.depth;
-    bgs = o.sil;
-    bgv[0] = o.rgb[0]; bgv[1] = o.rgb[1]; bgv[2] = o.rgb[2]; bgv[3] = o.alpha;
-  }
+__global__ void __launch_bounds__(256) k_shade(FwdParams P) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
   const int64_t HW = (int64_t)P.H * P.W;
-  const int64_t base = (int64_t)n * HW;
-  if ((P.W & 3) == 0) {
-    const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
-    const float4 dv = make_float4(bgd, bgd, bgd, bgd), sv = make_float4(bgs, bgs, bgs, bgs);
-    const float4 c4 = make_float4(bgv[0], bgv[1], bgv[2], bgv[3]);
-    const float4 c0 = make_float4(bgv[0], bgv[1], bgv[2], bgv[0]), c1 = make_float4(bgv[1], bgv[2], bgv[0], bgv[1]),
-                 c2 = make_float4(bgv[2], bgv[0], bgv[1], bgv[2]);
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < HW / 4; i += (int64_t)gridDim.x * 256) {
-      const int64_t pix = base + 4 * i;
-      if (MODE == 0) {
-        longlong2* q = (longlong2*)(P.p2f + pix);
-        q[0] = make_longlong2(-1ll, -1ll);
-        q[1] = make_longlong2(-1ll, -1ll);
-        *(float4*)(P.zbuf + pix) = m1;
-        *(float4*)(P.dists + pix) = m1;
-        float4* b = (float4*)(P.bary + pix * 3);
-        b[0] = m1; b[1] = m1; b[2] = m1;
-      } else {
-        if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = dv;
-        if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = sv;
-        if (P.p2f32) *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
-        if (P.out_flags & MR_OUT_RGB) {
-          float4* c = (float4*)(P.rgb + pix * CH);
-          if (CH == 4) {
-            c[0] = c4; c[1] = c4; c[2] = c4; c[3] = c4;
-          } else {
-            c[0] = c0; c[1] = c1; c[2] = c2;
-          }
-        }
-      }
-    }
-  } else {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < HW; i += (int64_t)gridDim.x * 256) {
-      const int64_t q = base + i;
-      if (MODE == 0) {
-        P.p2f[q] = -1ll;
-        P.zbuf[q] = -1.0f;
-        P.dists[q] = -1.0f;
-        for (int c = 0; c < 3; ++c) P.bary[q * 3 + c] = -1.0f;
-      } else {
-        if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = bgd;
-        if (P.out_flags & MR_OUT_SIL) P.sil[q] = bgs;
-        if (P.p2f32) P.p2f32[q] = -1;
-        if (P.out_flags & MR_OUT_RGB)
-          for (int c = 0; c < CH; ++c) P.rgb[q * CH + c] = bgv[c];
-      }
-    }
-  }
-}
-
-// One covered pixel per thread (grid (NB, N), striding over view n's list): recompute the
-// winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade (M = 1).
-template <int MODE, int CH>
-__global__ void __launch_bounds__(256) k_shade(OutParams P) {
-  const int n = blockIdx.y;
-  const int cntp = P.pcnt[n];
-  const int64_t HW = (int64_t)P.H * P.W;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < cntp; i += gridDim.x * 256) {
-    const int2 e = P.plist[n * HW + i];
-    const int px = e.x % P.W, py = e.x / P.W;
-    const int64_t q = n * HW + e.x;
-    const FaceRec r = P.recs[e.y];
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
+    const int gt = P.stile[s];
+    const int f = P.sface[(int64_t)s * 64 + lane];
+    if (f < 0) continue;
+    const int n = gt / P.T, t = gt - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
+    const int64_t q = n * HW + (int64_t)py * P.W + px;
+    const FaceRec r = P.recs[f];
     PixGeom G;
-    if (MODE == 1) load_geom(P.srec, (uint32_t)(e.y - n * P.F), G);  // in parallel with the record
+    if (MODE == 1) load_geom(P.srec, (uint32_t)(f - n * P.F), G);  // in parallel with the record
     FragEval ev;
     const bool hit = eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp,
                                P.clipb, ev);  // true by construction (same test that kept it)
     if (!hit) continue;
     if (MODE == 0) {
-      P.p2f[q] = (int64_t)e.y;
+      P.p2f[q] = (int64_t)f;
       P.zbuf[q] = ev.pz;
       P.dists[q] = ev.sdist;
       P.bary[3 * q + 0] = ev.b0;
@@ -962,16 +1028,9 @@ __global__ void __launch_bounds__(256) k_shade(OutParams P) {
         P.rgb[q * CH + 2] = o.rgb[2];
         if (CH == 4) P.rgb[q * CH + 3] = o.alpha;
       }
-      if (P.p2f32) P.p2f32[q] = e.y;
+      if (P.p2f32) P.p2f32[q] = f;
     }
   }
-}
-
-// Per-view workgroups for a view-strided grid: ~`total` workgroups overall, at most `cap` per view.
-static int blocks_per_view(int64_t N, int total, int64_t cap) {
-  int nb = ceil_div(total, N);
-  if (nb > cap) nb = (int)cap;
-  return nb < 1 ? 1 : nb;
 }
 
 // Resident workgroups of a kernel on the current device (persistent grid size).
@@ -985,31 +1044,34 @@ static int resident_grid(K kernel, int threads, int fallback_per_cu) {
   return cus * per;
 }
 
-struct RasterCfg {  // what launch_raster needs besides the workspace
-  int H, W;
-  float blur, bbox_pad;
-  int persp, clipb;
-  const int64_t* view_first;
-  int64_t F;
-};
-
-static TileParams make_tile(const RasterCfg& c, const BinGeom& g, const RasterWS& w) {
-  TileParams P;
-  P.H = c.H; P.W = c.W; P.TX = g.TX; P.T = g.T;
-  P.blur = c.blur; P.bbox_pad = c.bbox_pad;
-  P.persp = c.persp; P.clipb = c.clipb;
-  P.view_first = c.view_first; P.F = c.F;
+// Static forward parameters from the settings; the workspace pointers from the carve.
+static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const RasterWS& w, int64_t N,
+                          const int64_t* view_first, int64_t F) {
+  FwdParams P;
+  memset(&P, 0, sizeof(P));
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.TX = g.TX; P.T = g.T;
+  P.blur = s->blur_radius;
+  P.bbox_pad = sqrtf(s->blur_radius);
+  P.persp = s->perspective_correct;
+  P.clipb = s->clip_barycentric_coords;
+  P.view_first = view_first; P.F = F;
   P.recs = w.recs; P.list = w.list; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
-  P.tdone = w.tdone; P.pcnt = w.pcnt; P.plist = w.plist;
+  P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
   return P;
 }
 
-static int launch_tile_raster(const TileParams& P, int64_t unit_cap, hipStream_t st) {
-  static int grid = 0;
-  if (!grid) grid = resident_grid(k_tile_raster, 256, 7);
-  const int gb = (int)(unit_cap / 4 + 1 < grid ? unit_cap / 4 + 1 : grid);
-  MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<<<gb, 256, 0, st>>>(P)));
+// Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
+template <int MODE, int CH>
+static int launch_raster_and_shade(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+  static int rgrid = 0, sgrid = 0;
+  if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH>, 256, 7);
+  if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
+  MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
+  const int64_t slots_cap = N * (int64_t)g.T;
+  const int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
+  MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sg, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_shade");
   return MR_OK;
 }
 
@@ -1149,24 +1211,26 @@ MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float
   wave_lds_sync();
 }
 
-// Fused render backward over the compact per-view (pixel, face record) list written by
-// k_tile_raster, in two kernels so that each stays small enough (VGPRs) to keep several
-// waves per SIMD hiding its load latency:
+// Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
+// tile pixel the winning face record or -1; the pixel is implied by slot and lane), in two
+// kernels so that each stays small enough (VGPRs) to keep several waves per SIMD:
 //   k_bwd_shade: per covered pixel, recompute fragment + shading and differentiate the
 //                blends / Phong / texture -> 20-float record (grads of z, signed dist,
 //                barycentrics, interpolated point / normal / texel, and the barycentrics);
 //   k_bwd_geom : per covered pixel, rasterizer backward (edge functions, perspective
 //                correction, distances) + projection backward -> per-face rows summed over
-//                runs (seg_scatter) and per-view R/T partial sums (one slot per wave).
-// Workgroup (b, n) takes 256-entry chunks b, b + NB, ... of view n's list.
+//                runs of equal faces (seg_scatter), and the slot's R/T partial sums.
+// Waves stride over slots (one 8x8 tile, one view each).
 #define MR_BWD_REC 5  // float4s per pixel record
 struct RenderBwdParams {
-  int N, H, W, NB;
+  int N, H, W, TX, T;
   float blur, bbox_pad;
   int persp, clipb;
   const FaceRec* recs;
-  const int* pcnt;
-  const int2* plist;
+  const int* ctr;
+  const int* sface;
+  const int* stile;
+  const int* vslot;
   const float* gD;
   const float* gS;
   const float* gRGB;
@@ -1175,23 +1239,35 @@ struct RenderBwdParams {
   const ShadeRec* srec;
   int64_t F;     // faces of the shared mesh: record id rid = n*F + face
   const ViewRec* views;
-  float4* prec;  // (N, H*W, MR_BWD_REC) per covered pixel
+  float4* prec;  // (slots, 64, MR_BWD_REC) per covered pixel
   float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
-  float* rt_part;  // (N, NB*4, 12) per-wave R/T partial sums
+  float* rt_part;  // (slots, 12) per-slot R/T partial sums
 };
 
+MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& px, int& py) {
+  n = gt / P.T;
+  const int t = gt - n * P.T;
+  const int ty = t / P.TX, tx = t - ty * P.TX;
+  px = tx * MR_TS + (lane & 7);
+  py = ty * MR_TS + (lane >> 3);
+}
+
 __global__ void __launch_bounds__(256) k_bwd_shade(RenderBwdParams P) {
-  const int n = blockIdx.y;
-  const int cntp = P.pcnt[n];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
   const int64_t HW = (int64_t)P.H * P.W;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < cntp; i += P.NB * 256) {
-    const int2 q = P.plist[n * HW + i];
-    const int px = q.x % P.W, py = q.x / P.W;
-    const int64_t pix = n * HW + q.x;
-    // every load that depends only on the list entry is issued here, together
-    const FaceRec r = P.recs[q.y];
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
+    const int gt = P.stile[s];
+    const int f = P.sface[(int64_t)s * 64 + lane];
+    if (f < 0) continue;
+    int n, px, py;
+    slot_pixel(P, gt, lane, n, px, py);
+    const int64_t pix = n * HW + (int64_t)py * P.W + px;
+    // every load that depends only on the slot entry is issued here, together
+    const FaceRec r = P.recs[f];
     PixGeom G;
-    load_geom(P.srec, (uint32_t)(q.y - n * P.F), G);
+    load_geom(P.srec, (uint32_t)(f - n * P.F), G);
     const float gD = P.gD ? P.gD[pix] : 0.0f;
     const float gS = P.gS ? P.gS[pix] : 0.0f;
     float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
@@ -1203,9 +1279,9 @@ __global__ void __launch_bounds__(256) k_bwd_shade(RenderBwdParams P) {
       if (P.rgb_ch == 4) gA = g[3];
     }
     FragEval e;
-    float4* o4 = P.prec + (n * HW + i) * MR_BWD_REC;
+    float4* o4 = P.prec + ((int64_t)s * 64 + lane) * MR_BWD_REC;
     if (!eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
-      // unreachable (the list holds kept fragments); a zero record contributes nothing
+      // unreachable (slots hold kept fragments); a zero record contributes nothing
       for (int k = 0; k < MR_BWD_REC; ++k) o4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       continue;
     }
@@ -1226,76 +1302,78 @@ template <int ACC>
 __global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
-  const int n = blockIdx.y;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cntp = P.pcnt[n];
-  const int64_t HW = (int64_t)P.H * P.W;
-  float gR[9], gT[3];
-  for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
-  for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
-  if (blockIdx.x * 256 < cntp) {  // uniform over the workgroup
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
+    const int gt = P.stile[s];
+    const int f = P.sface[(int64_t)s * 64 + lane];
+    int n, px, py;
+    slot_pixel(P, gt, lane, n, px, py);
     const ViewRec V = P.views[n];
-    for (int c0 = blockIdx.x * 256; c0 < cntp; c0 += P.NB * 256) {
-      const int i = c0 + threadIdx.x;
-      float row[ACC];
+    float gR[9], gT[3];
 #pragma unroll
-      for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
-      int key = -1;
-      if (i < cntp) {
-        const int2 q = P.plist[n * HW + i];
-        const int px = q.x % P.W, py = q.x / P.W;
-        const int face = (int)(q.y - n * P.F);
-        const FaceRec r = P.recs[q.y];
-        const float4* p4 = P.prec + (n * HW + i) * MR_BWD_REC;
-        const float4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
-        const float4 a4 = ACC == 27 ? p4[4] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
-        const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
-        const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
-        const float gb[3] = {a0.z, a0.w, a1.x};
-        const float gP[3] = {a1.y, a1.z, a1.w};
-        const float gNn[3] = {a2.x, a2.y, a2.z};
-        const float b[3] = {a2.w, a3.x, a3.y};
-        const float gt[3] = {a3.z, a3.w, a4.x};
-        float gfv[3][3];
-        raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
-        key = face;
+    for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-          float gX[3];
-          project_bwd(V, X[c], gfv[c], gX, gR, gT);
+    for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
+    float row[ACC];
 #pragma unroll
-          for (int k = 0; k < 3; ++k) {
-            row[3 * c + k] = b[c] * gP[k] + gX[k];
-            row[9 + 3 * c + k] = b[c] * gNn[k];
-            if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt[k];
-          }
+    for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
+    int key = -1;
+    if (f >= 0) {
+      const int face = (int)(f - n * P.F);
+      const FaceRec r = P.recs[f];
+      const float4* p4 = P.prec + ((int64_t)s * 64 + lane) * MR_BWD_REC;
+      const float4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
+      const float4 a4 = ACC == 27 ? p4[4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
+      const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
+      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+      const float gb[3] = {a0.z, a0.w, a1.x};
+      const float gP[3] = {a1.y, a1.z, a1.w};
+      const float gNn[3] = {a2.x, a2.y, a2.z};
+      const float b[3] = {a2.w, a3.x, a3.y};
+      const float gt3[3] = {a3.z, a3.w, a4.x};
+      float gfv[3][3];
+      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+      key = face;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float gX[3];
+        project_bwd(V, X[c], gfv[c], gX, gR, gT);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          row[3 * c + k] = b[c] * gP[k] + gX[k];
+          row[9 + 3 * c + k] = b[c] * gNn[k];
+          if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
         }
       }
-      seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     }
-  }
-  // per-view R/T: wave reduction into this wave's partial slot (no atomics; k_rt_reduce sums)
+    seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
+    // the slot's R/T partial sums (a slot is one view): wave reduction, no atomics
 #pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    float v = i < 9 ? gR[i] : gT[i - 9];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == i) P.rt_part[((int64_t)n * P.NB * 4 + blockIdx.x * 4 + wave) * 12 + i] = v;
+    for (int i = 0; i < 12; ++i) {
+      float v = i < 9 ? gR[i] : gT[i - 9];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == i) P.rt_part[(int64_t)s * 12 + i] = v;
+    }
   }
 }
 
-// grad_views[n] = sum of view n's NST partial rows (fixed order: deterministic).
-__global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, int NST, float* __restrict__ out) {
-  __shared__ float s[12][4];
+// grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
+__global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
+                                                   int N, float* __restrict__ out) {
+  __shared__ float sm[12][4];
   const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s0 = vslot[n], ns = vslot[N + n];
   for (int i = 0; i < 12; ++i) {
     float v = 0.0f;
-    for (int t = threadIdx.x; t < NST; t += 256) v += part[((int64_t)n * NST + t) * 12 + i];
+    for (int t = threadIdx.x; t < ns; t += 256) v += part[((int64_t)s0 + t) * 12 + i];
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) s[i][wave] = v;
+    if (lane == 0) sm[i][wave] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 12) out[n * 12 + threadIdx.x] = ((s[threadIdx.x][0] + s[threadIdx.x][1]) + s[threadIdx.x][2]) + s[threadIdx.x][3];
+  if (threadIdx.x < 12) out[n * 12 + threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + sm[threadIdx.x][2]) + sm[threadIdx.x][3];
 }
 
 // ---------------------------------------------------------------------------
@@ -1499,57 +1577,17 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   return P;
 }
 
-static RasterCfg make_cfg(const mr_raster_settings_t* s, const int64_t* view_first, int64_t F) {
-  RasterCfg c;
-  c.H = s->H; c.W = s->W;
-  c.blur = s->blur_radius;
-  c.bbox_pad = sqrtf(s->blur_radius);
-  c.persp = s->perspective_correct;
-  c.clipb = s->clip_barycentric_coords;
-  c.view_first = view_first;
-  c.F = F;
-  return c;
-}
-
 static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, const int64_t* view_count, int64_t F,
                        hipStream_t st) {
   ScanParams P;
   P.T = g.T; P.list_cap = g.list_cap;
   P.cnt = w.cnt; P.vtot = w.vtot; P.start = w.start; P.cur = w.cur; P.vbase = w.vbase;
-  P.tdone = w.tdone; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
+  P.tdone = w.tdone; P.vslot = w.vslot; P.stile = w.stile; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
   P.view_count = view_count; P.F = F;
   MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan<<<(unsigned)N, 1024, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_bin_scan");
   return MR_OK;
 }
-
-static OutParams make_out(const RasterCfg& c, const RasterWS& w, int64_t N) {
-  OutParams P;
-  memset(&P, 0, sizeof(P));
-  P.N = (int)N; P.H = c.H; P.W = c.W;
-  P.blur = c.blur; P.bbox_pad = c.bbox_pad;
-  P.persp = c.persp; P.clipb = c.clipb;
-  P.recs = w.recs; P.pcnt = w.pcnt; P.plist = w.plist;
-  return P;
-}
-
-extern "C++" {
-// Output stage shared by both entry points, in stream order: k_fill_bg (every pixel gets
-// the background), `geometry` (binning + raster, a callable), k_shade (covered pixels).
-template <int MODE, int CH, typename Geo>
-static int run_with_outputs(const OutParams& P, int64_t N, hipStream_t st, Geo geometry) {
-  const int64_t HW = (int64_t)P.H * P.W;
-  const dim3 fgrid(blocks_per_view(N, 4096, ceil_div(HW, 1024)), (unsigned)N);
-  MR_TIMED(MODE == 0 ? KID_FILL_FRAG : KID_FILL_RENDER, st, (k_fill_bg<MODE, CH><<<fgrid, 256, 0, st>>>(P)));
-  MR_CHECK_LAUNCH("k_fill_bg");
-  const int rc = geometry();
-  if (rc) return rc;
-  const dim3 sgrid(blocks_per_view(N, 4096, ceil_div(HW, 256)), (unsigned)N);
-  MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sgrid, 256, 0, st>>>(P)));
-  MR_CHECK_LAUNCH("k_shade");
-  return MR_OK;
-}
-}  // extern "C++"
 
 int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const int64_t* count, int64_t N,
                             int64_t Ftot, const mr_raster_settings_t* s, int64_t* p2f, float* zbuf, float* bary,
@@ -1568,26 +1606,22 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
-  const RasterCfg cfg = make_cfg(s, first, 0);
-  OutParams P = make_out(cfg, w, N);
+  const bool lds = g.T <= MR_LDS_HIST;
+  const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+  if (Ftot > 0) {
+    if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
+    else MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
+    MR_CHECK_LAUNCH("k_bin_count_fv");
+  }
+  if ((rc = launch_scan(w, N, g, count, 0, st))) return rc;
+  if (Ftot > 0) {
+    if (lds) MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, Ftot, first, N)));
+    else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
+    MR_CHECK_LAUNCH("k_bin_fill_fv");
+  }
+  FwdParams P = make_fwd(s, g, w, N, first, 0);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
-  return run_with_outputs<0, 3>(P, N, st, [&]() -> int {
-    int rc2;
-    const bool lds = g.T <= MR_LDS_HIST;
-    const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
-    if (Ftot > 0) {
-      if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
-      else MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
-      MR_CHECK_LAUNCH("k_bin_count_fv");
-    }
-    if ((rc2 = launch_scan(w, N, g, count, 0, st))) return rc2;
-    if (Ftot > 0) {
-      if (lds) MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, Ftot, first, N)));
-      else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
-      MR_CHECK_LAUNCH("k_bin_fill_fv");
-    }
-    return launch_tile_raster(make_tile(cfg, g, w), g.unit_cap, st);
-  });
+  return launch_raster_and_shade<0, 3>(P, g, N, st);
 }
 
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
@@ -1722,54 +1756,40 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
-  const RasterCfg cfg = make_cfg(s, nullptr, m->F);
-  OutParams P = make_out(cfg, w, N);
+  FwdParams P = make_fwd(s, g, w, N, nullptr, m->F);
   P.S = make_shade(m, sp, cc, ncc);
+  P.srec = w.srec;
   P.out_flags = sp->out_flags;
   P.depth = depth;
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  P.srec = w.srec;
-  P.F = m->F;
-  auto geometry = [&]() -> int {
-    MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
-    MR_CHECK_LAUNCH("k_shade_rec");
-    dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
-    const bool lds = g.T <= MR_LDS_HIST;
-    const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
-    if (lds)
-      MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
-    else
-      MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
-    MR_CHECK_LAUNCH("k_bin_count_world");
-    int rc2;
-    if ((rc2 = launch_scan(w, N, g, nullptr, m->F, st))) return rc2;
-    if (lds)
-      MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
-    else
-      MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
-    MR_CHECK_LAUNCH("k_bin_fill_world");
-    return launch_tile_raster(make_tile(cfg, g, w), g.unit_cap, st);
-  };
-  if (sp->rgb_channels == 4) return run_with_outputs<1, 4>(P, N, st, geometry);
-  return run_with_outputs<1, 3>(P, N, st, geometry);
-}
-
-// Backward workgroups per view: ~4096 in total, never more than the view's 256-pixel chunks.
-static int bwd_blocks_per_view(int64_t N, int H, int W) {
-  const int chunks = ceil_div((int64_t)H * W, 256);
-  int nb = ceil_div(4096, N);
-  if (nb > chunks) nb = chunks;
-  return nb < 1 ? 1 : nb;
+  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
+  MR_CHECK_LAUNCH("k_shade_rec");
+  dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
+  const bool lds = g.T <= MR_LDS_HIST;
+  const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+  if (lds)
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+  else
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+  MR_CHECK_LAUNCH("k_bin_count_world");
+  if ((rc = launch_scan(w, N, g, nullptr, m->F, st))) return rc;
+  if (lds)
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
+  else
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
+  MR_CHECK_LAUNCH("k_bin_fill_world");
+  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st);
+  return launch_raster_and_shade<1, 3>(P, g, N, st);
 }
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
-  const int NB = bwd_blocks_per_view(N, H, W);
-  size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);        // gface
-  off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);           // gnu
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB * 4, 256); // rt_part
-  off = align_up(off + sizeof(float4) * MR_BWD_REC * (size_t)N * H * W, 256);  // prec
+  const int64_t NT = N * (int64_t)ceil_div(W, MR_TS) * ceil_div(H, MR_TS);
+  size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);                 // gface
+  off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);                    // gnu
+  off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);                  // rt_part
+  off = align_up(off + sizeof(float4) * MR_BWD_REC * 64 * (size_t)NT, 256);    // prec
   return off;
 }
 
@@ -1791,7 +1811,7 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, s->H, s->W, g, m->F);
   const bool vcol = m->tex_kind == 1;
   const int ACC = vcol ? 27 : 18;
-  const int NB = bwd_blocks_per_view(N, s->H, s->W);
+  const int64_t NT = N * (int64_t)g.T;
   char* b = (char*)bws;
   size_t off = 0;
   float* gface = (float*)(b + off);
@@ -1799,18 +1819,20 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   float* gnu = (float*)(b + off);
   off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
   float* rt_part = (float*)(b + off);
-  off = align_up(off + sizeof(float) * 12 * (size_t)N * NB * 4, 256);
+  off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);
   float4* prec = (float4*)(b + off);
   if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
   memset(&P, 0, sizeof(P));
-  P.N = (int)N; P.H = s->H; P.W = s->W; P.NB = NB;
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.TX = g.TX; P.T = g.T;
   P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
   P.recs = w.recs;
-  P.pcnt = w.pcnt;
-  P.plist = w.plist;
+  P.ctr = w.ctr;
+  P.sface = w.sface;
+  P.stile = w.stile;
+  P.vslot = w.vslot;
   P.gD = (sp->out_flags & MR_OUT_DEPTH) ? gD : nullptr;
   P.gS = (sp->out_flags & MR_OUT_SIL) ? gS : nullptr;
   P.gRGB = (sp->out_flags & MR_OUT_RGB) ? gRGB : nullptr;
@@ -1822,13 +1844,17 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   P.prec = prec;
   P.gface = gface;
   P.rt_part = rt_part;
-  dim3 grid(NB, (unsigned)N);
-  MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<grid, 256, 0, st>>>(P)));
+  static int g1 = 0, g2 = 0, g3 = 0;
+  if (!g1) g1 = resident_grid(k_bwd_shade, 256, 3);
+  if (!g2) g2 = resident_grid(k_bwd_geom<18>, 256, 3);
+  if (!g3) g3 = resident_grid(k_bwd_geom<27>, 256, 3);
+  auto cap = [&](int gr) { return (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr); };
+  MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<cap(g1), 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_bwd_shade");
-  if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<grid, 256, 0, st>>>(P)));
-  else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<grid, 256, 0, st>>>(P)));
+  if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<cap(g3), 256, 0, st>>>(P)));
+  else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<cap(g2), 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_bwd_geom");
-  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, NB * 4, gviews)));
+  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
   MR_CHECK_LAUNCH("k_rt_reduce");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V, 256);
@@ -1849,23 +1875,20 @@ int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, i
   hipStream_t st = (hipStream_t)stream;
   BinGeom g = bin_geom(H, W, N, Ftot > 0 ? Ftot : 1, mfpb);
   RasterWS w = carve_raster_ws((void*)ws, N, Ftot > 0 ? Ftot : 1, H, W, g);
-  const size_t n = 2 * (size_t)N + CTR_COUNT;  // pcnt, vtot, ctr are contiguous
+  const size_t n = (size_t)N + CTR_COUNT;  // vtot and ctr are contiguous
   int* h = (int*)malloc(sizeof(int) * n);
   if (!h) return set_err(MR_EINVAL, "out of host memory");
-  if (hipMemcpyAsync(h, w.pcnt, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+  if (hipMemcpyAsync(h, w.vtot, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess) {
     free(h);
     return set_err(MR_ELAUNCH, "stats copy failed");
   }
-  int64_t cov = 0, ent = 0;
-  for (int64_t i = 0; i < N; ++i) {
-    cov += h[i];
-    ent += h[N + i];
-  }
+  int64_t ent = 0;
+  for (int64_t i = 0; i < N; ++i) ent += h[i];
   out[0] = ent;
-  out[1] = h[2 * N + CTR_UNITS];
-  out[2] = h[2 * N + CTR_SLOTS];
-  out[3] = cov;
+  out[1] = h[N + CTR_UNITS];
+  out[2] = h[N + CTR_SLOTS];
+  out[3] = h[N + CTR_COVERED];
   free(h);
   return MR_OK;
 }

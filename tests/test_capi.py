@@ -45,7 +45,7 @@ def test_version_and_workspace_queries(lib):
 
 def test_invalid_arguments_fail_loudly_without_touching_the_gpu(lib):
     s = _lib.MrRasterSettings()
-    s.H, s.W, s.faces_per_pixel, s.blur_radius = 64, 64, 4, 0.0
+    s.H, s.W, s.faces_per_pixel, s.blur_radius = 64, 64, 129, 0.0  # K in [1, 128]
     rc = lib.mr_rasterize_meshes(None, None, None, 1, 10, ctypes.byref(s), None, None, None, None, None, 0, None)
     assert rc == 3 and b"faces_per_pixel" in lib.mr_last_error()
     with pytest.raises(NotImplementedError):

@@ -100,3 +100,47 @@ def test_empty_views_and_background():
     ref = O.raster_fwd(fv, torch.zeros(1, dtype=torch.int64), torch.full((1,), F), 32, 32)
     assert torch.equal(got[0].cpu(), ref[0])
     assert (ref[0] == -1).all() and (got[1].cpu() == -1).all()
+
+
+@pytest.mark.parametrize("name,H,W,N,K,blur,clip,cap", [
+    ("cow", 96, 128, 2, 3, 0.0, False, None),
+    ("teapot", 64, 64, 2, 8, 0.0, False, None),
+    # soft rasterization as deform_mesh_with_color.py:153-159 configures it (blur > 0 => clip)
+    ("sphere", 64, 64, 1, 6, 2e-3, True, None),
+    ("cow", 64, 64, 2, 4, 0.0, False, 5),  # overflowing tile lists: whole-view scan
+])
+def test_raster_k_nearest_matches_oracle(name, H, W, N, K, blur, clip, cap):
+    """faces_per_pixel > 1: the K nearest faces per pixel in ascending
+    (z, face) order, with their zbuf / bary / dists, bit-exact against the C oracle."""
+    verts, faces, views = _inputs(name, H, W, N)
+    fv = O.project_faces_c(verts, faces, views)
+    F = faces.shape[0]
+    first, count = torch.arange(N) * F, torch.full((N,), F)
+    ref = O.raster_fwd(fv, first, count, H, W, K, blur, True, clip)
+    dev = torch.device("cuda:0")
+    got = Kn.rasterize_meshes_fwd(fv.to(dev), first.to(dev), count.to(dev), H, W, K, blur, True, clip,
+                                  max_faces_per_bin=cap)
+    got = [t.cpu() for t in got]
+    assert got[0].shape == (N, H, W, K)
+    assert (ref[0][..., 1] >= 0).sum() > 0, "degenerate test: no pixel has a second face"
+    assert torch.equal(got[0], ref[0]), f"pix_to_face mismatch at {(got[0] != ref[0]).sum()} entries"
+    for a, b, nm in zip(got[1:], ref[1:], ("zbuf", "bary", "dists")):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32)), f"{nm}: max diff {(a - b).abs().max()}"
+
+
+def test_raster_k_backward_matches_oracle():
+    name, H, W, N, K = "cow", 64, 80, 2, 3
+    verts, faces, views = _inputs(name, H, W, N)
+    fv = O.project_faces_c(verts, faces, views)
+    F = faces.shape[0]
+    first, count = torch.arange(N) * F, torch.full((N,), F)
+    p2f, zbuf, bary, dists = O.raster_fwd(fv, first, count, H, W, K)
+    g = torch.Generator().manual_seed(2)
+    gz = torch.rand(zbuf.shape, generator=g) * 2 - 1
+    gb = torch.rand(bary.shape, generator=g) * 2 - 1
+    gd = torch.rand(dists.shape, generator=g) * 2e-5 - 1e-5
+    ref = O.raster_bwd(fv, p2f, gz, gb, gd)
+    dev = torch.device("cuda:0")
+    got = Kn.rasterize_meshes_bwd(fv.to(dev), p2f.to(dev), gz.to(dev), gb.to(dev), gd.to(dev), H, W, K).cpu()
+    scale = max(1.0, ref.abs().max().item())
+    assert torch.allclose(got, ref, atol=1e-4 * scale, rtol=1e-4), (got - ref).abs().max()

@@ -32,6 +32,8 @@
 #include <stdarg.h>
 #include <stdlib.h>
 
+#include <mutex>
+
 #include "../../include/mi355r.h"
 #include "mr_common.h"
 #include "mr_shade.h"
@@ -61,13 +63,14 @@ static int set_err(int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
-                KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_COUNT };
+                KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG, KID_FILL_RENDER,
+                KID_RASTER_K, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
-                                              "k_shade_rec"};
+                                              "k_shade_rec", "k_fill<0>", "k_fill<1>", "k_raster_k"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -126,6 +129,7 @@ struct BinGeom {
   int TX, TY, T;
   int64_t list_cap;
   int64_t unit_cap;  // >= units the scan can emit: one per non-empty tile + list_cap / MR_UE
+  int mfpb;          // max_faces_per_bin (0: none): a longer tile list takes the whole-view path
 };
 static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   BinGeom g;
@@ -134,11 +138,12 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   g.T = g.TX * g.TY;
   // Expected entries: ~(1 + 2*edge/8)^2 tiles per face + large faces; tiles whose list would
   // overflow take the exact full-view path (one unit scanning every face of the view).
-  // max_faces_per_bin (if given) scales the reservation.
+  // max_faces_per_bin (if given) scales the reservation and caps each tile's list (PyTorch3D's per-bin cap).
   int64_t cap = 6 * Ftot + 2 * N * (int64_t)g.T + 65536;
   if (mfpb > 0) cap = (int64_t)mfpb * N * 16 + 65536;
   g.list_cap = cap;
   g.unit_cap = N * (int64_t)g.T + cap / MR_UE + 1;
+  g.mfpb = mfpb > 0 ? mfpb : 0;
   return g;
 }
 
@@ -524,7 +529,7 @@ __global__ void __launch_bounds__(256) k_bin_fill_fv(SetupParams P, int64_t Ftot
 }
 
 struct ScanParams {
-  int T;
+  int T, mfpb;
   int64_t list_cap;
   const int* cnt;
   const int* vtot;
@@ -580,7 +585,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
       P.start[(int64_t)n * P.T + tt] = ex;
       P.cur[(int64_t)n * P.T + tt] = ex;
     }
-    const bool ovf = cc > 0 && vb + ex + cc > P.list_cap;
+    const bool ovf = cc > 0 && (vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb));
     const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
     tot_u += nu;
     tot_s += cc > 0 ? 1 : 0;
@@ -605,7 +610,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
     const int tt = b0 + t;
     const int cc = tt < P.T ? c[tt] : 0;
     const int ex = tt < P.T ? P.start[(int64_t)n * P.T + tt] : 0;
-    const bool ovf = cc > 0 && vb + ex + cc > P.list_cap;
+    const bool ovf = cc > 0 && (vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb));
     const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
     const int ns = cc > 0 ? 1 : 0;
     int tu, ts;
@@ -679,7 +684,7 @@ MR_DEV unsigned long long frag_key(float z, int f) {
 
 // Everything the forward kernels read and write (geometry, work lists, outputs).
 struct FwdParams {
-  int N, H, W, TX, T;
+  int N, H, W, TX, T, K;
   float blur, bbox_pad;
   int persp, clipb;
   const int64_t* view_first;  // NULL: shared mode (overflow units scan faces n*F ..)
@@ -687,6 +692,12 @@ struct FwdParams {
   const FaceRec* recs;
   const int* list;
   const int4* units;
+  const int64_t* view_count;  // modular mode: faces per view (overflow tiles scan them all)
+  const int* cnt;             // per-tile entries, start inside the view, view bases (K > 1)
+  const int* start;
+  const int* vbase;
+  int64_t list_cap;
+  int mfpb;
   int* ctr;
   unsigned long long* tkey;
   int* tdone;
@@ -744,7 +755,7 @@ MR_DEV Bg background(const FwdParams& P) {
 template <int MODE, int CH>
 MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) {
   const int lane = threadIdx.x & 63;
-  const int64_t HW = (int64_t)P.H * P.W;
+  const int64_t HW = (int64_t)P.H * P.W * (MODE == 0 ? P.K : 1);  // MODE 0: every entry is -1
   if (vec) {
     const int64_t g = (int64_t)c * 64 + lane;
     if (g >= HW / 4) return;
@@ -810,9 +821,20 @@ MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) 
 //      of sface straight from LDS; units sharing a tile merge their keys with global u64
 //      atomicMin, and the last of them to finish (an atomic count-down) reads the merged
 //      keys back with returning atomics and writes the slot.
-// The background of every pixel (k_shade later overwrites the covered ones) is written by
-// the same waves, a share of 64-lane chunks after each unit: the stores stream to HBM while
-// the raster work, which is latency-bound, leaves it idle.
+// The background of every pixel is k_fill's (side stream, overlapping binning and this
+// kernel); k_shade then overwrites the covered pixels.
+template <int MODE, int CH>
+__global__ void __launch_bounds__(256) k_fill(FwdParams P) {
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), G = gridDim.x * 4;
+  const bool vec = (P.W & 3) == 0;
+  const int64_t HW = (int64_t)P.H * P.W * (MODE == 0 ? P.K : 1);
+  const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
+  const int nchunks = P.N * cpv;
+  const Bg bg = background<MODE>(P);
+#pragma unroll 1
+  for (int c = gw; c < nchunks; c += G) fill_chunk<MODE, CH>(P, bg, c / cpv, c - (c / cpv) * cpv, vec);
+}
+
 template <int MODE, int CH>
 __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
   __shared__ WaveStage stage[4];
@@ -828,17 +850,12 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
   const bool fast_ok = !(blur > 0.0f);
 #endif
   const int H = P.H, W = P.W;
-  // background chunks of this wave: c = gw, gw + G, ... < N * cpv, spread over its units
   const int gw = blockIdx.x * 4 + wave, G = gridDim.x * 4;
-  const bool vec = (W & 3) == 0;
-  const int64_t HW = (int64_t)H * W;
-  const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
-  const int nchunks = P.N * cpv;
-  const int my_chunks = gw < nchunks ? (nchunks - gw + G - 1) / G : 0;
-  const int my_units = gw < nunits ? (nunits - gw + G - 1) / G : 0;
-  const int per_unit = my_units > 0 ? (my_chunks + my_units - 1) / my_units : my_chunks;
-  const Bg bg = background<MODE>(P);
-  int chunk = gw;
+  // software pipeline: the next unit's record and this lane's entry of it are loaded while
+  // the current unit is rasterised, so a unit starts with one dependent load (its face
+  // records) instead of three (unit -> list entry -> record)
+  int4 Un = gw < nunits ? P.units[gw] : make_int4(0, 0, 0, 0);
+  int idn = gw < nunits && Un.y >= 0 && lane < Un.z ? P.list[Un.y + lane] : 0;
 #ifdef MR_PROF
   unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, npass = 0, nunit = 0;
   unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -849,7 +866,9 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
 #endif
 #pragma unroll 1
   for (int u = gw; u < nunits; u += G) {
-    const int4 U = P.units[u];
+    const int4 U = Un;
+    const int id0 = idn;
+    if (u + G < nunits) Un = P.units[u + G];
     const int n = U.x / P.T, t = U.x - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
     const int x0 = tx * MR_TS, y0 = ty * MR_TS;
@@ -865,7 +884,7 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
       const int e = eb + lane;
       int np = 0, meta = 0;
       if (e < U.z) {
-        const int id = ovf ? (int)(vfirst + e) : P.list[U.y + e];
+        const int id = ovf ? (int)(vfirst + e) : id0;  // a listed unit has <= 64 entries
         const FaceRec r = P.recs[id];
         int cx0, cx1, cy0, cy1;
         ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
@@ -882,14 +901,9 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
         S.rec[lane] = r;
         S.id[lane] = id;
       }
+      if (eb == 0 && u + G < nunits) idn = Un.y >= 0 && lane < Un.z ? P.list[Un.y + lane] : 0;
       // pair numbering
       ACC(acc_load);
-      if (eb == 0) {  // this unit's share of background chunks: they drain during the passes
-#pragma unroll 1
-        for (int j = 0; j < per_unit && chunk < nchunks; ++j, chunk += G)
-          fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
-        ACC(acc_fill);
-      }
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
@@ -963,9 +977,6 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
     ++nunit;
 #endif
   }
-#pragma unroll 1
-  for (; chunk < nchunks; chunk += G) fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
-  ACC(acc_fill);
 #ifdef MR_PROF
   if (g_prof && lane == 0) {
     unsigned long long* o = g_prof + (size_t)gw * 8;
@@ -1049,25 +1060,201 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
                           const int64_t* view_first, int64_t F) {
   FwdParams P;
   memset(&P, 0, sizeof(P));
-  P.N = (int)N; P.H = s->H; P.W = s->W; P.TX = g.TX; P.T = g.T;
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.TX = g.TX; P.T = g.T; P.K = s->faces_per_pixel;
   P.blur = s->blur_radius;
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
   P.clipb = s->clip_barycentric_coords;
   P.view_first = view_first; P.F = F;
   P.recs = w.recs; P.list = w.list; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
+  P.cnt = w.cnt; P.start = w.start; P.vbase = w.vbase; P.list_cap = g.list_cap; P.mfpb = g.mfpb;
   P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
   return P;
 }
 
-// Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
+// K > 1 (modular path, PyTorch3D faces_per_pixel): one wave per non-empty tile, one pixel per
+// lane. The tile's faces are staged 64 at a time in the wave's LDS (one record per lane, then
+// read as broadcasts) and each lane keeps the K smallest packed (z, face) keys of its pixel in
+// an ascending per-lane LDS list (insertion; lane-strided so the 64 lanes hit 64 banks). The
+// K smallest keys are exactly the CPU's K nearest with the earlier face winning depth ties,
+// already in output order (RasterizeMeshesNaiveCpu keeps the K smallest, then sorts).
+// LDS per wave: K * 512 B of keys + 4.25 KB of staged records.
+#define MR_KMAX 128
+MR_DEV size_t rk_wave_bytes(int K) { return (size_t)K * 64 * 8 + 64 * sizeof(FaceRec) + 64 * sizeof(int); }
+__global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char rk_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wpg = blockDim.x >> 6;
+  const int K = P.K;
+  unsigned char* base = rk_lds + (size_t)wave * rk_wave_bytes(K);
+  unsigned long long* q = (unsigned long long*)base + lane;  // q[k * 64]
+  FaceRec* rs = (FaceRec*)(base + (size_t)K * 64 * 8);
+  int* ids = (int*)(rs + 64);
+  const int nslots = P.ctr[CTR_SLOTS];
+  const float pad = P.bbox_pad, blur = P.blur;
+  const bool persp = P.persp != 0, clipb = P.clipb != 0;
+  const bool fast_ok = !(blur > 0.0f);
+  const int H = P.H, W = P.W;
+  const int64_t HW = (int64_t)H * W;
+#pragma unroll 1
+  for (int s = blockIdx.x * wpg + wave; s < nslots; s += gridDim.x * wpg) {
+    const int gt = P.stile[s];
+    const int n = gt / P.T, t = gt - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
+    const bool in_img = px < W && py < H;
+    const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
+    const int cc = P.cnt[gt], ex = P.start[gt];
+    const int64_t vb = P.vbase[n];
+    // the scan's overflow rule: scan the whole view
+    const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
+    const int64_t vfirst = P.view_first[n];
+    const int count = ovf ? (int)(P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : cc;
+    int nq = 0;
+#pragma unroll 1
+    for (int eb = 0; eb < count; eb += 64) {
+      const int e = eb + lane;
+      if (e < count) {
+        const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
+        rs[lane] = P.recs[id];
+        ids[lane] = id;
+      }
+      wave_lds_sync();
+      const int m = count - eb < 64 ? count - eb : 64;
+#pragma unroll 1
+      for (int j = 0; j < m; ++j) {
+        const FaceRec r = rs[j];
+        float pz;
+        if (in_img && (r.flags & FR_VALID) &&
+            frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz)) {
+          const unsigned long long key = frag_key(pz, ids[j]);
+          if (key < MR_KEY_EMPTY && (nq < K || key < q[(nq - 1) * 64])) {
+            int i = nq < K ? nq : K - 1;
+            while (i > 0 && q[(i - 1) * 64] > key) {
+              q[i * 64] = q[(i - 1) * 64];
+              --i;
+            }
+            q[i * 64] = key;
+            nq += nq < K ? 1 : 0;
+          }
+        }
+      }
+      wave_lds_sync();
+    }
+    if (!in_img) continue;
+    const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+      int64_t f = -1;
+      float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
+      if (k < nq) {
+        const int id = (int)(unsigned)(q[k * 64] & 0xffffffffull);
+        FragEval ev;
+        eval_face(P.recs[id], xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
+        f = id; z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
+      }
+      P.p2f[pix + k] = f;
+      P.zbuf[pix + k] = z;
+      P.dists[pix + k] = d;
+      P.bary[3 * (pix + k) + 0] = b0;
+      P.bary[3 * (pix + k) + 1] = b1;
+      P.bary[3 * (pix + k) + 2] = b2;
+    }
+  }
+}
+
+static int join_fill(hipStream_t st, bool forked);
+static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st, bool forked) {
+  int rc = join_fill(st, forked);
+  if (rc) return rc;
+  const int K = P.K;
+  const size_t wb = (size_t)K * 64 * 8 + 64 * sizeof(FaceRec) + 64 * sizeof(int);
+  const int wpg = wb * 4 <= 65536 ? 4 : wb * 2 <= 65536 ? 2 : 1;
+  const int64_t slots_cap = N * (int64_t)g.T;
+  const int64_t want = (slots_cap + wpg - 1) / wpg;
+  const int grid = (int)(want < 8192 ? want : 8192);
+  MR_TIMED(KID_RASTER_K, st, (k_raster_k<<<grid, 64 * wpg, wb * wpg, st>>>(P)));
+  MR_CHECK_LAUNCH("k_raster_k");
+  return MR_OK;
+}
+
+// Side stream of the background fill, one per device: k_fill is forked from the caller's
+// stream before binning and joined before the first kernel that overwrites its pixels, so
+// its streaming stores overlap the latency-bound binning and raster. Events record/wait
+// pairs are issued under one lock (re-entrant across threads; a join may also wait for
+// another caller's fill, which is only conservative). Inside a stream capture the fork
+// and join become graph edges; the stream itself is never created during a capture (the
+// fill then runs on the caller's stream).
+struct SideStream {
+  hipStream_t s;
+  hipEvent_t fork, join;
+  int ok;
+};
+static SideStream g_side[64];
+static std::mutex g_side_mu;
+
+static SideStream* side_stream_locked(hipStream_t st) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  SideStream& S = g_side[dev];
+  if (S.ok) return &S;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  int lo = 0, hi = 0;
+  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
+  if (hipStreamCreateWithPriority(&S.s, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
+  if (hipEventCreateWithFlags(&S.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&S.join, hipEventDisableTiming) != hipSuccess)
+    return nullptr;
+  S.ok = 1;
+  return &S;
+}
+
 template <int MODE, int CH>
-static int launch_raster_and_shade(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+static int fork_fill(const FwdParams& P, hipStream_t st, bool& forked) {
+  static int grid = 0;
+  if (!grid) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    grid = 2 * cus;
+  }
+  std::lock_guard<std::mutex> lk(g_side_mu);
+  forked = false;
+  hipStream_t fs = st;
+  SideStream* S = getenv("MR_NO_SIDE_STREAM") ? nullptr : side_stream_locked(st);
+  if (S && hipEventRecord(S->fork, st) == hipSuccess && hipStreamWaitEvent(S->s, S->fork, 0) == hipSuccess) {
+    fs = S->s;
+    forked = true;
+  }
+  MR_TIMED(MODE == 0 ? KID_FILL_FRAG : KID_FILL_RENDER, fs, (k_fill<MODE, CH><<<grid, 256, 0, fs>>>(P)));
+  MR_CHECK_LAUNCH("k_fill");
+  return MR_OK;
+}
+
+static int join_fill(hipStream_t st, bool forked) {
+  if (!forked) return MR_OK;
+  std::lock_guard<std::mutex> lk(g_side_mu);
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  SideStream& S = g_side[dev];
+  if (hipEventRecord(S.join, S.s) != hipSuccess || hipStreamWaitEvent(st, S.join, 0) != hipSuccess)
+    return set_err(MR_ELAUNCH, "background fill join failed");
+  return MR_OK;
+}
+
+// Raster then covered-pixel outputs (after the background fill has joined); grids sized
+// once per kernel instance.
+template <int MODE, int CH>
+static int launch_raster_and_shade(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st, bool forked) {
   static int rgrid = 0, sgrid = 0;
   if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH>, 256, 7);
   if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
   MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
+  int rc = join_fill(st, forked);
+  if (rc) return rc;
   const int64_t slots_cap = N * (int64_t)g.T;
   const int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
   MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sg, 256, 0, st>>>(P)));
@@ -1130,9 +1317,9 @@ MR_DEV void acc_flush(LdsAcc<ACC>& L, float* __restrict__ gdst) {
   }
 }
 
-// Modular backward (PyTorch3D _C.rasterize_meshes_backward), K = 1.
+// Modular backward (PyTorch3D _C.rasterize_meshes_backward), every one of the K faces per pixel.
 struct RasterBwdParams {
-  int N, H, W, NBX;
+  int N, H, W, NBX, K;
   int persp, clipb;
   const float* fv;
   const int64_t* p2f;
@@ -1152,19 +1339,22 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   for (int k = 0; k < 4; ++k) {
     const int py = bty * MR_BT + (threadIdx.x >> 5) + 8 * k;
     if (px >= P.W || py >= P.H) continue;
-    const int64_t pix = ((int64_t)n * P.H + py) * P.W + px;
-    const int64_t f = P.p2f[pix];
-    if (f < 0) continue;
-    FaceRec r;
-    const float* v = P.fv + 9 * f;
-    r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
-    r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
-    r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
-    r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
-    const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
-    float g[3][3];
-    raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
-    acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
+    const int64_t pix0 = (((int64_t)n * P.H + py) * P.W + px) * P.K;
+    for (int kk = 0; kk < P.K; ++kk) {
+      const int64_t pix = pix0 + kk;
+      const int64_t f = P.p2f[pix];
+      if (f < 0) continue;
+      FaceRec r;
+      const float* v = P.fv + 9 * f;
+      r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
+      r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
+      r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
+      r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
+      const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
+      float g[3][3];
+      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+      acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
+    }
   }
   __syncthreads();
   acc_flush(L, P.gfv);
@@ -1547,8 +1737,8 @@ static int check_settings(const mr_raster_settings_t* s) {
   if (!s) return set_err(MR_EINVAL, "settings is NULL");
   if (s->H <= 0 || s->W <= 0) return set_err(MR_EINVAL, "image size must be positive (got %d x %d)", s->H, s->W);
   if (s->H > 8192 || s->W > 8192) return set_err(MR_EUNSUPPORTED, "image size above 8192");
-  if (s->faces_per_pixel != 1)
-    return set_err(MR_EUNSUPPORTED, "faces_per_pixel=%d: only 1 is implemented on the MI355X path", s->faces_per_pixel);
+  if (s->faces_per_pixel < 1 || s->faces_per_pixel > MR_KMAX)
+    return set_err(MR_EUNSUPPORTED, "faces_per_pixel=%d: supported range is [1, %d]", s->faces_per_pixel, MR_KMAX);
   if (!(s->blur_radius >= 0.0f) || !__builtin_isfinite(s->blur_radius))
     return set_err(MR_EINVAL, "blur_radius must be finite and >= 0");
   return MR_OK;
@@ -1580,7 +1770,7 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
 static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, const int64_t* view_count, int64_t F,
                        hipStream_t st) {
   ScanParams P;
-  P.T = g.T; P.list_cap = g.list_cap;
+  P.T = g.T; P.mfpb = g.mfpb; P.list_cap = g.list_cap;
   P.cnt = w.cnt; P.vtot = w.vtot; P.start = w.start; P.cur = w.cur; P.vbase = w.vbase;
   P.tdone = w.tdone; P.vslot = w.vslot; P.stile = w.stile; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
   P.view_count = view_count; P.F = F;
@@ -1606,6 +1796,11 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
+  FwdParams P = make_fwd(s, g, w, N, first, 0);
+  P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
+  P.view_count = count;
+  bool forked = false;
+  if ((rc = fork_fill<0, 3>(P, st, forked))) return rc;
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   if (Ftot > 0) {
@@ -1619,9 +1814,8 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
     else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
     MR_CHECK_LAUNCH("k_bin_fill_fv");
   }
-  FwdParams P = make_fwd(s, g, w, N, first, 0);
-  P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
-  return launch_raster_and_shade<0, 3>(P, g, N, st);
+  if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st, forked);
+  return launch_raster_and_shade<0, 3>(P, g, N, st, forked);
 }
 
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
@@ -1636,7 +1830,7 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
     return set_err(MR_ELAUNCH, "memset failed");
   if (Ftot == 0) return MR_OK;
   RasterBwdParams P;
-  P.N = (int)N; P.H = s->H; P.W = s->W; P.NBX = ceil_div(s->W, MR_BT);
+  P.N = (int)N; P.H = s->H; P.W = s->W; P.NBX = ceil_div(s->W, MR_BT); P.K = s->faces_per_pixel;
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
   P.fv = fv; P.p2f = p2f; P.gz = gz; P.gb = gb; P.gd = gd; P.gfv = gfv;
   dim3 grid(P.NBX * ceil_div(s->H, MR_BT), (unsigned)N);
@@ -1742,6 +1936,7 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   if (rc) return rc;
   rc = check_mesh(m, sp);
   if (rc) return rc;
+  if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if ((int64_t)N * m->F >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
   if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
@@ -1764,6 +1959,10 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
+  bool forked = false;
+  if (sp->rgb_channels == 4) rc = fork_fill<1, 4>(P, st, forked);
+  else rc = fork_fill<1, 3>(P, st, forked);
+  if (rc) return rc;
   MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
   MR_CHECK_LAUNCH("k_shade_rec");
   dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
@@ -1780,8 +1979,8 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   else
     MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
-  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st);
-  return launch_raster_and_shade<1, 3>(P, g, N, st);
+  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, forked);
+  return launch_raster_and_shade<1, 3>(P, g, N, st, forked);
 }
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
@@ -1801,6 +2000,7 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   if (rc) return rc;
   rc = check_mesh(m, sp);
   if (rc) return rc;
+  if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if (!fws || !bws || !gverts || !gviews) return set_err(MR_EINVAL, "NULL argument");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");

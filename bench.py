@@ -92,9 +92,9 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
 def algorithmic_bytes(kernel, H, W, F, views, st):
     HW, cov, ent, slots = H * W, st["covered"], st["entries"], st["tiles"]
     table = {
-        # list ids, each face record once, 64 winners per non-empty tile
-        "k_tile_raster": 4 * ent + 64 * F * views + 256 * slots,
-        "k_fill<1>": 20 * HW * views,                     # background depth + silhouette + rgb(3)
+        # background of every pixel (depth + silhouette + rgb(3)), list ids, each face record once,
+        # 64 winners per non-empty tile
+        "k_tile_raster": 20 * HW * views + 4 * ent + 64 * F * views + 256 * slots,
         "k_shade<1>": 256 * slots + 20 * cov,              # winners in, 20 B of outputs per covered pixel
         "k_bwd_shade": 256 * slots + (20 + 80) * cov,      # winners + upstream grads, 80-B gradient record out
         "k_bwd_geom": 256 * slots + 80 * cov + 72 * F,     # winners + gradient record in, per-face rows out
@@ -108,8 +108,6 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
 # bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
 FORWARD_KERNELS = ("k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                    "k_shade<1>")
-# k_fill<1> (background stores) runs on the library's side stream, overlapped with the above
-FORWARD_SIDE_KERNELS = ("k_fill<1>",)
 
 
 # SURVEY.md §8d API-minimum traffic of the whole fwd+bwd path per frame
@@ -264,7 +262,6 @@ def main():
     fwd_us = sum(kt[k][1] / kt[k][0] * 1e3 for k in FORWARD_KERNELS if k in kt)
     fwd_bytes = (20 * H * W + 36 * Fn) * nv
     fwd_roof = {"kernels": [k for k in FORWARD_KERNELS if k in kt], "us_per_launch": round(fwd_us, 2),
-                "overlapped": [k for k in FORWARD_SIDE_KERNELS if k in kt],
                 "algorithmic_bytes": fwd_bytes, "achieved": round(fwd_bytes / (fwd_us * 1e-6) / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)} if fwd_us > 0 else None

@@ -32,8 +32,6 @@
 #include <stdarg.h>
 #include <stdlib.h>
 
-#include <mutex>
-
 #include "../../include/mi355r.h"
 #include "mr_common.h"
 #include "mr_shade.h"
@@ -63,14 +61,14 @@ static int set_err(int code, const char* fmt, ...) {
 // ---------------------------------------------------------------------------
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
-                KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG, KID_FILL_RENDER,
+                KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
                 KID_RASTER_K, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
-                                              "k_shade_rec", "k_fill<0>", "k_fill<1>", "k_raster_k"};
+                                              "k_shade_rec", "k_fill<0>", "k_raster_k"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -698,6 +696,7 @@ struct FwdParams {
   const int* vbase;
   int64_t list_cap;
   int mfpb;
+  int fill;  // k_tile_raster also writes the background
   int* ctr;
   unsigned long long* tkey;
   int* tdone;
@@ -821,8 +820,12 @@ MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) 
 //      of sface straight from LDS; units sharing a tile merge their keys with global u64
 //      atomicMin, and the last of them to finish (an atomic count-down) reads the merged
 //      keys back with returning atomics and writes the slot.
-// The background of every pixel is k_fill's (side stream, overlapping binning and this
-// kernel); k_shade then overwrites the covered pixels.
+// The background of every pixel (k_shade later overwrites the covered ones) is written by
+// the same waves, a share of 64-lane chunks after each unit: the stores stream to HBM while
+// the raster work, which is latency-bound, leaves it idle. (Measured: a separate fill kernel
+// on a forked stream overlapping binning was slower in the graph-replayed step, and the
+// raster's time barely drops without the fill.) k_fill is the stand-alone version, used
+// before k_raster_k (K > 1).
 template <int MODE, int CH>
 __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), G = gridDim.x * 4;
@@ -850,7 +853,17 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
   const bool fast_ok = !(blur > 0.0f);
 #endif
   const int H = P.H, W = P.W;
+  // background chunks of this wave: c = gw, gw + G, ... < N * cpv, spread over its units
   const int gw = blockIdx.x * 4 + wave, G = gridDim.x * 4;
+  const bool vec = (W & 3) == 0;
+  const int64_t HW = (int64_t)H * W * (MODE == 0 ? P.K : 1);
+  const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
+  const int nchunks = P.fill ? P.N * cpv : 0;
+  const int my_chunks = gw < nchunks ? (nchunks - gw + G - 1) / G : 0;
+  const int my_units = gw < nunits ? (nunits - gw + G - 1) / G : 0;
+  const int per_unit = my_units > 0 ? (my_chunks + my_units - 1) / my_units : my_chunks;
+  const Bg bg = background<MODE>(P);
+  int chunk = gw;
   // software pipeline: the next unit's record and this lane's entry of it are loaded while
   // the current unit is rasterised, so a unit starts with one dependent load (its face
   // records) instead of three (unit -> list entry -> record)
@@ -904,6 +917,12 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
       if (eb == 0 && u + G < nunits) idn = Un.y >= 0 && lane < Un.z ? P.list[Un.y + lane] : 0;
       // pair numbering
       ACC(acc_load);
+      if (eb == 0) {  // this unit's share of background chunks: they drain during the passes
+#pragma unroll 1
+        for (int j = 0; j < per_unit && chunk < nchunks; ++j, chunk += G)
+          fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
+        ACC(acc_fill);
+      }
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
@@ -977,6 +996,9 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
     ++nunit;
 #endif
   }
+#pragma unroll 1
+  for (; chunk < nchunks; chunk += G) fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
+  ACC(acc_fill);
 #ifdef MR_PROF
   if (g_prof && lane == 0) {
     unsigned long long* o = g_prof + (size_t)gw * 8;
@@ -1164,10 +1186,11 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
   }
 }
 
-static int join_fill(hipStream_t st, bool forked);
-static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st, bool forked) {
-  int rc = join_fill(st, forked);
-  if (rc) return rc;
+static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+  static int fgrid = 0;
+  if (!fgrid) fgrid = resident_grid(k_fill<0, 3>, 256, 8);
+  MR_TIMED(KID_FILL_FRAG, st, (k_fill<0, 3><<<fgrid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_fill");
   const int K = P.K;
   const size_t wb = (size_t)K * 64 * 8 + 64 * sizeof(FaceRec) + 64 * sizeof(int);
   const int wpg = wb * 4 <= 65536 ? 4 : wb * 2 <= 65536 ? 2 : 1;
@@ -1179,82 +1202,15 @@ static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipS
   return MR_OK;
 }
 
-// Side stream of the background fill, one per device: k_fill is forked from the caller's
-// stream before binning and joined before the first kernel that overwrites its pixels, so
-// its streaming stores overlap the latency-bound binning and raster. Events record/wait
-// pairs are issued under one lock (re-entrant across threads; a join may also wait for
-// another caller's fill, which is only conservative). Inside a stream capture the fork
-// and join become graph edges; the stream itself is never created during a capture (the
-// fill then runs on the caller's stream).
-struct SideStream {
-  hipStream_t s;
-  hipEvent_t fork, join;
-  int ok;
-};
-static SideStream g_side[64];
-static std::mutex g_side_mu;
-
-static SideStream* side_stream_locked(hipStream_t st) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  SideStream& S = g_side[dev];
-  if (S.ok) return &S;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  int lo = 0, hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = 0;
-  if (hipStreamCreateWithPriority(&S.s, hipStreamNonBlocking, lo) != hipSuccess) return nullptr;
-  if (hipEventCreateWithFlags(&S.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&S.join, hipEventDisableTiming) != hipSuccess)
-    return nullptr;
-  S.ok = 1;
-  return &S;
-}
-
+// Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
 template <int MODE, int CH>
-static int fork_fill(const FwdParams& P, hipStream_t st, bool& forked) {
-  static int grid = 0;
-  if (!grid) {
-    int dev = 0, cus = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    grid = 2 * cus;
-  }
-  std::lock_guard<std::mutex> lk(g_side_mu);
-  forked = false;
-  hipStream_t fs = st;
-  SideStream* S = getenv("MR_NO_SIDE_STREAM") ? nullptr : side_stream_locked(st);
-  if (S && hipEventRecord(S->fork, st) == hipSuccess && hipStreamWaitEvent(S->s, S->fork, 0) == hipSuccess) {
-    fs = S->s;
-    forked = true;
-  }
-  MR_TIMED(MODE == 0 ? KID_FILL_FRAG : KID_FILL_RENDER, fs, (k_fill<MODE, CH><<<grid, 256, 0, fs>>>(P)));
-  MR_CHECK_LAUNCH("k_fill");
-  return MR_OK;
-}
-
-static int join_fill(hipStream_t st, bool forked) {
-  if (!forked) return MR_OK;
-  std::lock_guard<std::mutex> lk(g_side_mu);
-  int dev = 0;
-  (void)hipGetDevice(&dev);
-  SideStream& S = g_side[dev];
-  if (hipEventRecord(S.join, S.s) != hipSuccess || hipStreamWaitEvent(st, S.join, 0) != hipSuccess)
-    return set_err(MR_ELAUNCH, "background fill join failed");
-  return MR_OK;
-}
-
-// Raster then covered-pixel outputs (after the background fill has joined); grids sized
-// once per kernel instance.
-template <int MODE, int CH>
-static int launch_raster_and_shade(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st, bool forked) {
+static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st) {
+  P.fill = 1;
   static int rgrid = 0, sgrid = 0;
   if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH>, 256, 7);
   if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
   MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
-  int rc = join_fill(st, forked);
-  if (rc) return rc;
   const int64_t slots_cap = N * (int64_t)g.T;
   const int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
   MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sg, 256, 0, st>>>(P)));
@@ -1799,8 +1755,6 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   FwdParams P = make_fwd(s, g, w, N, first, 0);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.view_count = count;
-  bool forked = false;
-  if ((rc = fork_fill<0, 3>(P, st, forked))) return rc;
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   if (Ftot > 0) {
@@ -1814,8 +1768,8 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
     else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
     MR_CHECK_LAUNCH("k_bin_fill_fv");
   }
-  if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st, forked);
-  return launch_raster_and_shade<0, 3>(P, g, N, st, forked);
+  if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
+  return launch_raster_and_shade<0, 3>(P, g, N, st);
 }
 
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
@@ -1959,10 +1913,6 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  bool forked = false;
-  if (sp->rgb_channels == 4) rc = fork_fill<1, 4>(P, st, forked);
-  else rc = fork_fill<1, 3>(P, st, forked);
-  if (rc) return rc;
   MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
   MR_CHECK_LAUNCH("k_shade_rec");
   dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
@@ -1979,8 +1929,8 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   else
     MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
-  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, forked);
-  return launch_raster_and_shade<1, 3>(P, g, N, st, forked);
+  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st);
+  return launch_raster_and_shade<1, 3>(P, g, N, st);
 }
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {

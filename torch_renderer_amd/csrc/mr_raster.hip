@@ -987,8 +987,6 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
       const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
       const bool hit = f != MR_NONE && px < W && py < H;
       P.sface[(int64_t)slot * 64 + lane] = hit ? f : -1;
-      const int nh = __popcll(__ballot(hit));
-      if (lane == 0 && nh) atomicAdd(&P.ctr[CTR_COVERED], nh);
     }
     wave_lds_sync();
     ACC(acc_emit);
@@ -2019,6 +2017,17 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   return MR_OK;
 }
 
+// Covered pixels of a forward (stats only; a same-address counter in the raster serialises).
+__global__ void __launch_bounds__(256) k_count_covered(const int* __restrict__ sface, const int* __restrict__ ctr,
+                                                       int* __restrict__ out) {
+  const int64_t n = (int64_t)ctr[CTR_SLOTS] * 64;
+  int c = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    c += sface[i] >= 0 ? 1 : 0;
+  c = wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, c);
+}
+
 int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, int32_t W, int32_t mfpb, int64_t* out,
                            void* stream) {
   if (!ws || !out || N <= 0 || N > 65535) return set_err(MR_EINVAL, "bad arguments");
@@ -2026,6 +2035,9 @@ int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, i
   BinGeom g = bin_geom(H, W, N, Ftot > 0 ? Ftot : 1, mfpb);
   RasterWS w = carve_raster_ws((void*)ws, N, Ftot > 0 ? Ftot : 1, H, W, g);
   const size_t n = (size_t)N + CTR_COUNT;  // vtot and ctr are contiguous
+  if (hipMemsetAsync(w.ctr + CTR_COVERED, 0, sizeof(int), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
+  k_count_covered<<<1024, 256, 0, st>>>(w.sface, w.ctr, w.ctr + CTR_COVERED);
+  MR_CHECK_LAUNCH("k_count_covered");
   int* h = (int*)malloc(sizeof(int) * n);
   if (!h) return set_err(MR_EINVAL, "out of host memory");
   if (hipMemcpyAsync(h, w.vtot, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||

@@ -838,8 +838,21 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
   for (int c = gw; c < nchunks; c += G) fill_chunk<MODE, CH>(P, bg, c / cpv, c - (c / cpv) * cpv, vec);
 }
 
+MR_DEV FaceRec load_rec_if(const FaceRec* __restrict__ recs, bool c, int id) {
+  FaceRec r;
+  if (c) {
+    r = recs[id];
+  } else {
+    r.x0 = r.y0 = r.z0 = r.x1 = r.y1 = r.z1 = r.x2 = r.y2 = r.z2 = 0.0f;
+    r.area = r.xmin = r.xmax = r.ymin = r.ymax = 0.0f;
+    r.flags = 0u;
+    r.face = 0u;
+  }
+  return r;
+}
+
 template <int MODE, int CH>
-__global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
+__global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 waves / SIMD: <= 96 VGPRs
   __shared__ WaveStage stage[4];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -860,15 +873,29 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
   const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
   const int nchunks = P.fill ? P.N * cpv : 0;
   const int my_chunks = gw < nchunks ? (nchunks - gw + G - 1) / G : 0;
-  const int my_units = gw < nunits ? (nunits - gw + G - 1) / G : 0;
+  // XCD-aware unit partition: workgroups are dispatched round-robin over the 8 XCDs, so
+  // blockIdx % 8 names this wave's XCD; each XCD's waves take a contiguous eighth of the
+  // (view-major) units, which keeps the face records they gather in that XCD's L2.
+  const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int jw = (blockIdx.x / parts) * 4 + wave, Gp = (gridDim.x / parts) * 4;
+  const int Cp = (nunits + parts - 1) / parts;
+  const int ub = (blockIdx.x % parts) * Cp, ue = ub + Cp < nunits ? ub + Cp : nunits;
+  const int my_units = ub + jw < ue ? (ue - ub - jw + Gp - 1) / Gp : 0;
   const int per_unit = my_units > 0 ? (my_chunks + my_units - 1) / my_units : my_chunks;
   const Bg bg = background<MODE>(P);
   int chunk = gw;
-  // software pipeline: the next unit's record and this lane's entry of it are loaded while
-  // the current unit is rasterised, so a unit starts with one dependent load (its face
-  // records) instead of three (unit -> list entry -> record)
-  int4 Un = gw < nunits ? P.units[gw] : make_int4(0, 0, 0, 0);
-  int idn = gw < nunits && Un.y >= 0 && lane < Un.z ? P.list[Un.y + lane] : 0;
+  // Software pipeline over the wave's units u, u + Gp, u + 2Gp, ...: while unit u is
+  // rasterised, the face records of u + Gp, the list entries of u + 2Gp and the unit record of
+  // u + 3Gp are in flight (unit records are wave-uniform scalar loads). Each link of the
+  // unit -> list entry -> record chain so gets a whole unit of work to land in, and a unit
+  // starts with its records in registers. (Overflow units fetch their records in the batch.)
+  const int4 z4 = make_int4(0, 0, 0, -1);
+  int4 U1 = ub + jw < ue ? P.units[ub + jw] : z4;
+  int4 U2 = ub + jw + Gp < ue ? P.units[ub + jw + Gp] : z4;
+  int4 U3 = ub + jw + 2 * Gp < ue ? P.units[ub + jw + 2 * Gp] : z4;
+  int id1 = ub + jw < ue && U1.y >= 0 && lane < U1.z ? P.list[U1.y + lane] : 0;
+  int id2 = ub + jw + Gp < ue && U2.y >= 0 && lane < U2.z ? P.list[U2.y + lane] : 0;
+  FaceRec r1 = load_rec_if(P.recs, ub + jw < ue && U1.y >= 0 && lane < U1.z, id1);
 #ifdef MR_PROF
   unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, npass = 0, nunit = 0;
   unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -878,10 +905,9 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
 #define ACC(v) do {} while (0)
 #endif
 #pragma unroll 1
-  for (int u = gw; u < nunits; u += G) {
-    const int4 U = Un;
-    const int id0 = idn;
-    if (u + G < nunits) Un = P.units[u + G];
+  for (int u = ub + jw; u < ue; u += Gp) {
+    const int4 U = U1;
+    const int id0 = id1;
     const int n = U.x / P.T, t = U.x - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
     const int x0 = tx * MR_TS, y0 = ty * MR_TS;
@@ -897,8 +923,15 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
       const int e = eb + lane;
       int np = 0, meta = 0;
       if (e < U.z) {
-        const int id = ovf ? (int)(vfirst + e) : id0;  // a listed unit has <= 64 entries
-        const FaceRec r = P.recs[id];
+        int id;
+        FaceRec r;
+        if (ovf) {
+          id = (int)(vfirst + e);
+          r = P.recs[id];
+        } else {  // a listed unit has <= 64 entries: its records are already here
+          id = id0;
+          r = r1;
+        }
         int cx0, cx1, cy0, cy1;
         ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
         ndc_range_to_pix(r.ymin - pad, r.ymax + pad, H, W, cy0, cy1);
@@ -914,7 +947,14 @@ __global__ void __launch_bounds__(256) k_tile_raster(FwdParams P) {
         S.rec[lane] = r;
         S.id[lane] = id;
       }
-      if (eb == 0 && u + G < nunits) idn = Un.y >= 0 && lane < Un.z ? P.list[Un.y + lane] : 0;
+      if (eb == 0) {  // advance the pipeline (after this unit's records are consumed)
+        r1 = load_rec_if(P.recs, u + Gp < ue && U2.y >= 0 && lane < U2.z, id2);
+        id1 = id2;
+        U1 = U2;
+        id2 = u + 2 * Gp < ue && U3.y >= 0 && lane < U3.z ? P.list[U3.y + lane] : 0;
+        U2 = U3;
+        U3 = u + 3 * Gp < ue ? P.units[u + 3 * Gp] : z4;
+      }
       // pair numbering
       ACC(acc_load);
       if (eb == 0) {  // this unit's share of background chunks: they drain during the passes

@@ -113,6 +113,16 @@ int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* 
                                   const int32_t* vadj_ptr, const int32_t* vadj, const mr_view_t* views, int64_t N,
                                   const float* grad_face_verts, float* grad_verts, float* grad_views, void* stream);
 
+/* ---------------- camera poses (DifferentiableRenderer._camera_pose_from_opencv_to_pytorch) ---------------- */
+/* torch_renderer.py:73-80: R_p3d = R_cv^T with columns 0,1 negated; T = t_cv with entries 0,1 negated.
+ * views[n] = {R_p3d row-major, T, intr[n]} (bitwise what the torch conversion + packing gives).
+ * *_stride = elements between consecutive views (0 broadcasts one pose / one intrinsics row). */
+int32_t mr_views_from_opencv(const float* R_cv, int64_t R_stride, const float* t_cv, int64_t t_stride,
+                             const float* intr, int64_t intr_stride, int64_t N, mr_view_t* views, void* stream);
+/* Chain rule of the conversion above: grad_views (N,12: dR_p3d row-major, dT) -> grad_R_cv (N,3,3),
+ * grad_t_cv (N,3), both overwritten. */
+int32_t mr_view_grads_to_opencv(const float* grad_views, int64_t N, float* grad_R_cv, float* grad_t_cv, void* stream);
+
 /* ---------------- mesh helpers ---------------- */
 /* Meshes.verts_normals_packed: n_f = (v2-v1) x (v0-v1), summed in (corner, face) order, normalized (eps 1e-6).
  * vnormals_raw (V,3) keeps the unnormalized sums for the backward. */

@@ -187,3 +187,38 @@ def test_renderer_class_matches_oracle():
     assert (ref["p2f"] >= 0).sum() > 50, "degenerate: the mesh is not in view"
     assert out.shape == (1, H, W, 4)
     _close(out, ref["rgba"])
+
+
+@pytest.mark.parametrize("broadcast", [False, True])
+def test_native_pose_conversion_is_bitwise_the_torch_one(broadcast):
+    """mr_views_from_opencv / mr_view_grads_to_opencv (the drop-in classes' camera conversion,
+    torch_renderer.py:73-80) give bitwise the images and pose gradients of the torch conversion."""
+    from torch_renderer_amd.kernels import ShadeConfig
+    from torch_renderer_amd.torch_renderer import render_mesh_batch
+    from torch_renderer_amd.transforms import opencv_to_pytorch3d
+    H = W = 64
+    N = 3
+    verts, faces, _, _, mesh = _cow_mesh(N)
+    _, _, _, (R, T, K) = canonical_views(verts, N, H, W)
+    r = DepthColorRender(K.to(DEV), (H, W), device=DEV)
+    if broadcast:
+        R, T = R[:1], T[:1]
+    outs, grads = [], []
+    for native in (True, False):
+        Rg = R.clone().to(DEV).requires_grad_(True)
+        tg = T.clone().to(DEV).requires_grad_(True)
+        Rin, tin = (Rg, tg) if native else opencv_to_pytorch3d(Rg, tg)
+        if broadcast:
+            Rin, tin = Rin.expand(N, 3, 3), tin.expand(N, 3)
+        cfg = ShadeConfig(H=H, W=W, light_location=(0.0, 0.0, -3.0))
+        o = render_mesh_batch(mesh, r._cameras, (H, W), Rin, tin, cfg, pose_cv=native)
+        g = torch.Generator().manual_seed(3)
+        loss = sum((o[k] * (torch.rand(o[k].shape, generator=g) * 2 - 1).to(DEV)).sum() for k in ("depth", "sil", "rgb"))
+        loss.backward()
+        outs.append([o[k].detach().cpu() for k in ("depth", "sil", "rgb")])
+        grads.append((Rg.grad.cpu(), tg.grad.cpu()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    for a, b in zip(*grads):
+        assert a.shape == b.shape
+        assert torch.allclose(a, b, rtol=0, atol=1e-6 * max(1.0, b.abs().max().item()))

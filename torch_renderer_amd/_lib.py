@@ -71,6 +71,8 @@ _SIGS = [
     ("mr_rasterize_meshes_backward", _I32, [_VP, _VP, _VP, _VP, _VP, _I64, _I64, ctypes.POINTER(MrRasterSettings),
                                             _VP, _VP]),
     ("mr_project_faces", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
+    ("mr_views_from_opencv", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _VP]),
+    ("mr_view_grads_to_opencv", _I32, [_VP, _I64, _VP, _VP, _VP]),
     ("mr_project_faces_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
     ("mr_vertex_normals", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _VP]),
     ("mr_render_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),

@@ -1859,6 +1859,67 @@ int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* 
   return MR_OK;
 }
 
+// OpenCV pose -> view records, and the conversion's chain rule (one thread per output float).
+__global__ void __launch_bounds__(256) k_views_from_opencv(const float* __restrict__ R, int64_t sR,
+                                                           const float* __restrict__ t, int64_t sT,
+                                                           const float* __restrict__ intr, int64_t sI, int64_t N,
+                                                           float* __restrict__ views) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * 16) return;
+  const int64_t n = i >> 4;
+  const int k = (int)(i & 15);
+  float v;
+  if (k < 9) {  // R_p3d[a][b] = R_cv[b][a] * s[b], s = (-1, -1, 1)
+    const int a = k / 3, b = k - 3 * a;
+    v = R[n * sR + 3 * b + a];
+    if (b < 2) v = -v;
+  } else if (k < 12) {
+    v = t[n * sT + (k - 9)];
+    if (k < 11) v = -v;
+  } else {
+    v = intr[n * sI + (k - 12)];
+  }
+  views[i] = v;
+}
+
+__global__ void __launch_bounds__(256) k_view_grads_to_opencv(const float* __restrict__ g, int64_t N,
+                                                              float* __restrict__ gR, float* __restrict__ gt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * 12) return;
+  const int64_t n = i / 12;
+  const int k = (int)(i - n * 12);
+  if (k < 9) {  // dL/dR_cv[b][a] = dL/dR_p3d[a][b] * s[b]
+    const int b = k / 3, a = k - 3 * b;
+    const float v = g[n * 12 + 3 * a + b];
+    gR[n * 9 + k] = b < 2 ? -v : v;
+  } else {
+    const float v = g[n * 12 + k];
+    gt[n * 3 + (k - 9)] = k < 11 ? -v : v;
+  }
+}
+
+int32_t mr_views_from_opencv(const float* R_cv, int64_t R_stride, const float* t_cv, int64_t t_stride,
+                             const float* intr, int64_t intr_stride, int64_t N, mr_view_t* views, void* stream) {
+  if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
+  if (!R_cv || !t_cv || !intr || !views) return set_err(MR_EINVAL, "NULL argument");
+  if (R_stride < 0 || t_stride < 0 || intr_stride < 0) return set_err(MR_EINVAL, "negative stride");
+  hipStream_t st = (hipStream_t)stream;
+  k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(R_cv, R_stride, t_cv, t_stride, intr, intr_stride, N,
+                                                            (float*)views);
+  MR_CHECK_LAUNCH("k_views_from_opencv");
+  return MR_OK;
+}
+
+int32_t mr_view_grads_to_opencv(const float* grad_views, int64_t N, float* grad_R_cv, float* grad_t_cv,
+                                void* stream) {
+  if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
+  if (!grad_views || !grad_R_cv || !grad_t_cv) return set_err(MR_EINVAL, "NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  k_view_grads_to_opencv<<<ceil_div(N * 12, 256), 256, 0, st>>>(grad_views, N, grad_R_cv, grad_t_cv);
+  MR_CHECK_LAUNCH("k_view_grads_to_opencv");
+  return MR_OK;
+}
+
 int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, int64_t F, const int32_t* ptr,
                           const int32_t* adj, float* vn, float* vraw, void* stream) {
   (void)F;

@@ -139,6 +139,26 @@ def make_views(R, T, intr):
     return torch.cat([R.reshape(-1, 9), T.reshape(-1, 3), intr.reshape(-1, 4)], dim=1).float().contiguous()
 
 
+def _batch_stride(t):
+    """(float tensor whose per-view rows are contiguous, elements between views; 0 = broadcast)."""
+    t = t.float()
+    if t.stride(-1) != 1 or (t.dim() == 3 and t.stride(-2) != 3):
+        t = t.contiguous()
+    return t, (t.stride(0) if t.shape[0] > 1 else 0)
+
+
+def views_from_opencv(R_cv, t_cv, intr, N):
+    """mr_views_from_opencv: (N,16) view records straight from OpenCV poses (one launch instead
+    of the transpose/sign multiplies and the packing concatenation)."""
+    R, sR = _batch_stride(R_cv.detach().reshape(-1, 3, 3))
+    t, sT = _batch_stride(t_cv.detach().reshape(-1, 3))
+    it, sI = _batch_stride(intr.reshape(-1, 4))
+    views = torch.empty((N, 16), device=R.device)
+    check(_lib.load().mr_views_from_opencv(ptr(R), sR, ptr(t), sT, ptr(it), sI, N, ptr(views),
+                                           _lib.stream_handle(R.device)))
+    return views
+
+
 class ProjectFaces(torch.autograd.Function):
     """MeshRasterizer.transform + verts_packed()[faces_packed] for one mesh shared by N views."""
 
@@ -276,7 +296,8 @@ class RenderViews(torch.autograd.Function):
     Differentiable inputs: verts (V,3), R (N,3,3), T (N,3), vcolors (V,3)."""
 
     @staticmethod
-    def forward(ctx, verts, R, T, vcolors, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs):
+    def forward(ctx, verts, R, T, vcolors, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs,
+                pose_cv=False):
         _require_cuda(verts, R, T, faces)
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled (N,H,W) grads
         L = _lib.load()
@@ -284,7 +305,10 @@ class RenderViews(torch.autograd.Function):
         v = verts.detach().float().contiguous()
         f, vptr, vadj = mesh_topology(faces, v.shape[0])
         vcol = vcolors.detach().float().contiguous() if vcolors is not None else None
-        views = make_views(R.detach(), T.detach(), intr)
+        if pose_cv:  # R, T are OpenCV poses (DifferentiableRenderer callers)
+            views = views_from_opencv(R, T, intr, max(R.shape[0], T.shape[0], intr.shape[0]))
+        else:
+            views = make_views(R.detach(), T.detach(), intr)
         N = views.shape[0]
         H, W = cfg.H, cfg.W
         vn = raw = None
@@ -308,7 +332,7 @@ class RenderViews(torch.autograd.Function):
         ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
                               vn if vn is not None else torch.empty(0, device=dev),
                               raw if raw is not None else torch.empty(0, device=dev), vptr, vadj)
-        ctx.cfg, ctx.tex, ctx.has_vcol = cfg, tex, vcolors is not None
+        ctx.cfg, ctx.tex, ctx.has_vcol, ctx.pose_cv = cfg, tex, vcolors is not None, pose_cv
         outs = [x for x in (depth, sil, rgb) if x is not None]
         if p2f is not None:
             ctx.mark_non_differentiable(p2f)
@@ -350,14 +374,20 @@ class RenderViews(torch.autograd.Function):
                                    cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
                                    ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gviews),
                                    ptr(gcol), _lib.stream_handle(dev)))
-        return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None)
+        if ctx.pose_cv:
+            gR = torch.empty((N, 3, 3), device=dev)
+            gt = torch.empty((N, 3), device=dev)
+            check(L.mr_view_grads_to_opencv(ptr(gviews), N, ptr(gR), ptr(gt), _lib.stream_handle(dev)))
+            return (gverts, gR, gt, gcol, None, None, None, None, None, None)
+        return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None, None)
 
 
 def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs | None = None,
-                 vcolors=None):
-    """Functional entry: returns dict(depth, sil, rgb[, pix_to_face32 when cfg.want_p2f])."""
+                 vcolors=None, pose_cv=False):
+    """Functional entry: returns dict(depth, sil, rgb[, pix_to_face32 when cfg.want_p2f]).
+    pose_cv: R, T are OpenCV camera poses (converted on the GPU, gradients returned in kind)."""
     tex = tex or TextureArgs()
-    outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex)
+    outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex, pose_cv)
     res = {}
     i = 0
     for name, want in (("depth", cfg.want_depth), ("sil", cfg.want_sil), ("rgb", cfg.want_rgb)):

@@ -40,9 +40,12 @@ def texture_args(meshes: Meshes, need_color: bool):
     raise NotImplementedError(f"textures of type {type(tex).__name__}")
 
 
-def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfig, cam_center=None):
+def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfig, cam_center=None,
+                      pose_cv=False):
     """Render every view of `meshes` (shared mesh or per-view meshes) with the fused kernels.
-    Returns dict(depth, sil, rgb[, pix_to_face32 if cfg.want_p2f]) with tensors of batch N."""
+    Returns dict(depth, sil, rgb[, pix_to_face32 if cfg.want_p2f]) with tensors of batch N.
+    pose_cv: R, T are OpenCV poses; the PyTorch3D conversion of torch_renderer.py:73-80 runs
+    on the GPU inside the render (mr_views_from_opencv) and gradients come back in kind."""
     H, W = image_size
     n = max(len(meshes), R.reshape(-1, 3, 3).shape[0], T.reshape(-1, 3).shape[0])
     Rb, Tb, intr = view_batch(cameras, (H, W), R, T, n_views=n)
@@ -52,7 +55,7 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
     if meshes.is_shared():
         tex, vcol = texture_args(meshes, need_color)
         return render_views(meshes.shared_verts(), Rb, Tb, meshes.shared_faces(), intr, cam_center,
-                            cfg, tex, vcolors=vcol)
+                            cfg, tex, vcolors=vcol, pose_cv=pose_cv)
     if len(meshes) != n:
         raise ValueError(f"Meshes batch ({len(meshes)}) and camera batch ({n}) differ")
     outs = []
@@ -61,7 +64,7 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
         tex, vcol = texture_args(mi, need_color)
         cc = cam_center[i:i + 1] if cam_center.shape[0] > 1 else cam_center
         outs.append(render_views(mi.shared_verts(), Rb[i:i + 1], Tb[i:i + 1], mi.shared_faces(),
-                                 intr[i:i + 1].contiguous(), cc, cfg, tex, vcolors=vcol))
+                                 intr[i:i + 1].contiguous(), cc, cfg, tex, vcolors=vcol, pose_cv=pose_cv))
     return {k: torch.cat([o[k] for o in outs], 0) for k in outs[0]}
 
 
@@ -108,10 +111,9 @@ class DepthRender(DifferentiableRenderer):
 
     def render(self, meshes, R, tvec, return_silhouette=False):
         self._check_meshes(meshes)
-        Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], want_depth=True,
                           want_sil=bool(return_silhouette), want_rgb=False)
-        out = render_mesh_batch(meshes, self._cameras, self._image_size, Rs, ts, cfg)
+        out = render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)
         if not return_silhouette:
             return out["depth"]
         return out["depth"], out["sil"]
@@ -133,10 +135,9 @@ class ColorRender(DifferentiableRenderer):
 
     def render(self, meshes, R, tvec):
         self._check_meshes(meshes)
-        Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location,
                           want_depth=False, want_sil=False, want_rgb=True)
-        return render_mesh_batch(meshes, self._cameras, self._image_size, Rs, ts, cfg)["rgb"]
+        return render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)["rgb"]
 
 
 class DepthColorRender(DifferentiableRenderer):
@@ -149,7 +150,6 @@ class DepthColorRender(DifferentiableRenderer):
 
     def render(self, meshes, R, tvec):
         self._check_meshes(meshes)
-        Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location)
-        out = render_mesh_batch(meshes, self._cameras, self._image_size, Rs, ts, cfg)
+        out = render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)
         return out["depth"], out["sil"], out["rgb"]

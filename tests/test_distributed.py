@@ -35,7 +35,10 @@ def _worker(rank, world, port, n_total, q):
         ((v * (rank + 1)).sum() + (c * (rank + 2)).sum()).backward()
         D.allreduce_grads([v, c, None])
         got = D.gather_to_root(local, n_total)
-        res = {"v": v.grad.clone(), "c": c.grad.clone(), "range": (s, e), "gather": got}
+        # numpy arrays pickle by value: torch tensors would travel as shared-memory fds that
+        # the parent may fail to receive once this worker has exited
+        res = {"v": v.grad.numpy().copy(), "c": c.grad.numpy().copy(), "range": (s, e),
+               "gather": None if got is None else got.numpy().copy()}
         q.put((rank, res))
     finally:
         dist.destroy_process_group()
@@ -60,9 +63,9 @@ def test_gloo_world2_shard_allreduce_gather(n_total):
     assert res[0]["range"][0] == 0 and res[0]["range"][1] == res[1]["range"][0] and res[1]["range"][1] == n_total
     # all_reduce(sum): 1 + 2 and 2 + 3
     for r in range(world):
-        assert torch.equal(res[r]["v"], torch.full((7, 3), 3.0))
-        assert torch.equal(res[r]["c"], torch.full((5,), 5.0))
-    assert torch.equal(res[0]["gather"], full * 2.0)
+        assert torch.equal(torch.from_numpy(res[r]["v"]), torch.full((7, 3), 3.0))
+        assert torch.equal(torch.from_numpy(res[r]["c"]), torch.full((5,), 5.0))
+    assert torch.equal(torch.from_numpy(res[0]["gather"]), full * 2.0)
     assert res[1]["gather"] is None
 
 

@@ -132,6 +132,12 @@ def ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def strided_ptr(t):
+    """Pointer of a tensor whose layout the callee takes as explicit strides (e.g. a broadcast
+    view with batch stride 0)."""
+    return ctypes.c_void_p(t.data_ptr())
+
+
 def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 

@@ -154,7 +154,8 @@ def views_from_opencv(R_cv, t_cv, intr, N):
     t, sT = _batch_stride(t_cv.detach().reshape(-1, 3))
     it, sI = _batch_stride(intr.reshape(-1, 4))
     views = torch.empty((N, 16), device=R.device)
-    check(_lib.load().mr_views_from_opencv(ptr(R), sR, ptr(t), sT, ptr(it), sI, N, ptr(views),
+    sp = _lib.strided_ptr
+    check(_lib.load().mr_views_from_opencv(sp(R), sR, sp(t), sT, sp(it), sI, N, ptr(views),
                                            _lib.stream_handle(R.device)))
     return views
 

@@ -62,13 +62,13 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
-                                              "k_shade_rec", "k_fill<0>", "k_raster_k"};
+                                              "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -1065,9 +1065,20 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
   const int64_t HW = (int64_t)P.H * P.W;
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
-    const int gt = P.stile[s];
-    const int f = P.sface[(int64_t)s * 64 + lane];
+  // slot s + G's tile and winners are loaded while slot s is processed
+  const int G = gridDim.x * 4;
+  int gt_n = 0, f_n = -1;
+  if (blockIdx.x * 4 + wave < nslots) {
+    gt_n = P.stile[blockIdx.x * 4 + wave];
+    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
+  }
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
+    const int gt = gt_n;
+    const int f = f_n;
+    if (s + G < nslots) {
+      gt_n = P.stile[s + G];
+      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
+    }
     if (f < 0) continue;
     const int n = gt / P.T, t = gt - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
@@ -1441,9 +1452,20 @@ __global__ void __launch_bounds__(256) k_bwd_shade(RenderBwdParams P) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
   const int64_t HW = (int64_t)P.H * P.W;
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
-    const int gt = P.stile[s];
-    const int f = P.sface[(int64_t)s * 64 + lane];
+  // slot s + G's tile and winners are loaded while slot s is processed
+  const int G = gridDim.x * 4;
+  int gt_n = 0, f_n = -1;
+  if (blockIdx.x * 4 + wave < nslots) {
+    gt_n = P.stile[blockIdx.x * 4 + wave];
+    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
+  }
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
+    const int gt = gt_n;
+    const int f = f_n;
+    if (s + G < nslots) {
+      gt_n = P.stile[s + G];
+      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
+    }
     if (f < 0) continue;
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
@@ -1489,9 +1511,20 @@ __global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
-    const int gt = P.stile[s];
-    const int f = P.sface[(int64_t)s * 64 + lane];
+  // slot s + G's tile and winners are loaded while slot s is processed
+  const int G = gridDim.x * 4;
+  int gt_n = 0, f_n = -1;
+  if (blockIdx.x * 4 + wave < nslots) {
+    gt_n = P.stile[blockIdx.x * 4 + wave];
+    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
+  }
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
+    const int gt = gt_n;
+    const int f = f_n;
+    if (s + G < nslots) {
+      gt_n = P.stile[s + G];
+      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
+    }
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
     const ViewRec V = P.views[n];
@@ -1535,6 +1568,113 @@ __global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
     }
     seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     // the slot's R/T partial sums (a slot is one view): wave reduction, no atomics
+#pragma unroll
+    for (int i = 0; i < 12; ++i) {
+      float v = i < 9 ? gR[i] : gT[i - 9];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if (lane == i) P.rt_part[(int64_t)s * 12 + i] = v;
+    }
+  }
+}
+
+// Both halves in one kernel (the default): the shade backward's 20-float record goes through
+// the wave's LDS instead of HBM (80 B written + 80 B read per covered pixel), and the slot,
+// winners and face record are fetched once. Peak VGPRs stay those of the larger half: the
+// LDS hand-off ends the first half's live ranges.
+template <int ACC>
+__global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
+  __shared__ float lrow[4][64 * ACC];
+  __shared__ int lkey[4][64];
+  __shared__ float4 lrec[4][MR_BWD_REC][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
+  const int G = gridDim.x * 4;
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
+    const int gt = P.stile[s];
+    const int f = P.sface[(int64_t)s * 64 + lane];
+    int n, px, py;
+    slot_pixel(P, gt, lane, n, px, py);
+    // ---- half 1: blends / Phong / texture backward -> lrec
+    if (f >= 0) {
+      const int64_t HW = (int64_t)P.H * P.W;
+      const int64_t pix = n * HW + (int64_t)py * P.W + px;
+      const FaceRec r = P.recs[f];
+      PixGeom Gm;
+      load_geom(P.srec, (uint32_t)(f - n * P.F), Gm);
+      const float gD = P.gD ? P.gD[pix] : 0.0f;
+      const float gS = P.gS ? P.gS[pix] : 0.0f;
+      float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
+      if (P.gRGB) {
+        const float* g = P.gRGB + pix * P.rgb_ch;
+        gC[0] = g[0];
+        gC[1] = g[1];
+        gC[2] = g[2];
+        if (P.rgb_ch == 4) gA = g[3];
+      }
+      FragEval e;
+      float4 o[MR_BWD_REC];
+      if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
+        ShadeOut so;
+        ShadeCache C;
+        shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C);
+        ShadeGrad SG;
+        shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
+        o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
+        o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
+        o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
+        o[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
+        o[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
+      } else {  // unreachable (slots hold kept fragments); a zero record contributes nothing
+#pragma unroll
+        for (int k = 0; k < MR_BWD_REC; ++k) o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][k][lane] = o[k];
+    }
+    wave_lds_sync();
+    __builtin_amdgcn_sched_barrier(0);  // keep half 2's loads out of half 1's register peak
+    // ---- half 2: raster + projection backward, per-face runs, R/T partials
+    const ViewRec V = P.views[n];
+    float gR[9], gT[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
+    float row[ACC];
+#pragma unroll
+    for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
+    int key = -1;
+    if (f >= 0) {
+      const int face = (int)(f - n * P.F);
+      const FaceRec r = P.recs[f];
+      const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
+      const float4 a3 = lrec[wave][3][lane];
+      const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
+      const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
+      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+      const float gb[3] = {a0.z, a0.w, a1.x};
+      const float gP[3] = {a1.y, a1.z, a1.w};
+      const float gNn[3] = {a2.x, a2.y, a2.z};
+      const float b[3] = {a2.w, a3.x, a3.y};
+      const float gt3[3] = {a3.z, a3.w, a4.x};
+      float gfv[3][3];
+      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+      key = face;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float gX[3];
+        project_bwd(V, X[c], gfv[c], gX, gR, gT);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          row[3 * c + k] = b[c] * gP[k] + gX[k];
+          row[9 + 3 * c + k] = b[c] * gNn[k];
+          if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
+        }
+      }
+    }
+    seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
 #pragma unroll
     for (int i = 0; i < 12; ++i) {
       float v = i < 9 ? gR[i] : gT[i - 9];
@@ -2098,11 +2238,21 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   if (!g2) g2 = resident_grid(k_bwd_geom<18>, 256, 3);
   if (!g3) g3 = resident_grid(k_bwd_geom<27>, 256, 3);
   auto cap = [&](int gr) { return (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr); };
-  MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<cap(g1), 256, 0, st>>>(P)));
-  MR_CHECK_LAUNCH("k_bwd_shade");
-  if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<cap(g3), 256, 0, st>>>(P)));
-  else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<cap(g2), 256, 0, st>>>(P)));
-  MR_CHECK_LAUNCH("k_bwd_geom");
+  static const bool split = getenv("MR_BWD_SPLIT") != nullptr;  // two-kernel variant, for comparison
+  if (split) {
+    MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<cap(g1), 256, 0, st>>>(P)));
+    MR_CHECK_LAUNCH("k_bwd_shade");
+    if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<cap(g3), 256, 0, st>>>(P)));
+    else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<cap(g2), 256, 0, st>>>(P)));
+    MR_CHECK_LAUNCH("k_bwd_geom");
+  } else {
+    static int f18 = 0, f27 = 0;
+    if (!f18) f18 = resident_grid(k_bwd_fused<18>, 256, 3);
+    if (!f27) f27 = resident_grid(k_bwd_fused<27>, 256, 2);
+    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27><<<cap(f27), 256, 0, st>>>(P)));
+    else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18><<<cap(f18), 256, 0, st>>>(P)));
+    MR_CHECK_LAUNCH("k_bwd_fused");
+  }
   MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
   MR_CHECK_LAUNCH("k_rt_reduce");
   const int use_n = sp->light_kind == 0;

@@ -6,24 +6,22 @@
 //                    through an LDS histogram) -> k_bin_scan (one workgroup per view:
 //                    entry offsets per tile, compact slot per non-empty tile, and work
 //                    UNITS of <= 64 (tile, face) entries) -> k_bin_fill (tile lists).
-//   2. k_tile_raster: persistent grid of independent waves, one unit per wave: each lane
-//                    clips one face's pixel bbox to the tile, the wave expands the
-//                    (face, pixel) pairs 64 at a time (DPP prefix sums), evaluates each
-//                    pair exactly and keeps the per-pixel minimum of the packed (z, face)
-//                    key with ds_min_u64; the tile's 64 keys go to a compact slot buffer
-//                    (a plain store, or a global u64 atomicMin when a tile has > 1 unit).
+//   2. k_tile_raster: persistent grid of independent waves (XCD-partitioned units, 3-deep
+//                    unit/list/record prefetch): each lane clips one face's pixel bbox to
+//                    the tile, the wave expands the (face, pixel) pairs 64 at a time (DPP
+//                    prefix sums), evaluates each pair exactly and keeps the per-pixel
+//                    minimum of the packed (z, face) key with ds_min_u64; the tile's 64
+//                    winners go to its slot (a plain store, or a global u64 atomicMin merge
+//                    when a tile has > 1 unit). The same waves stream the background.
 //                    The minimum equals the CPU's "strictly nearer, earlier face wins".
-//   3. k_resolve<M>: streaming pass over EVERY pixel, 4 per thread: background pixels
-//                    are written with 16-B vector stores; pixels of non-empty tiles read
-//                    their key, recompute the winning fragment exactly and write M=0
-//                    PyTorch3D Fragments or M=1 shaded depth/silhouette/rgb (+ a compact
-//                    list of covered (pixel, face) pairs for the backward).
-//   4. backward    : k_render_bwd — waves over the covered-pixel list; per pixel the
-//                    fragment and shading are recomputed and differentiated; per-face
-//                    gradient rows are summed over runs of equal faces inside the wave
-//                    (segmented shuffles) and scattered with one float atomic per run
-//                    and component; per-view R/T gradients are wave-reduced.
-//                    k_raster_bwd is the modular _C.rasterize_meshes_backward.
+//   3. k_shade<M>  : per covered tile, recompute each winner's fragment exactly and write
+//                    M=0 PyTorch3D Fragments or M=1 shaded depth/silhouette/rgb.
+//      K > 1 (modular): k_fill<0> then k_raster_k (per-lane sorted K-lists in LDS).
+//   4. backward    : k_bwd_fused — per covered tile: shading backward (record handed over
+//                    in LDS), raster + projection backward, per-face rows summed over runs
+//                    of equal faces (segmented scan) with one atomic per run, per-slot R/T
+//                    partials (k_rt_reduce). k_raster_bwd is the modular
+//                    _C.rasterize_meshes_backward (any K).
 //   5. vertex kernels gather per-face rows through a CSR vertex adjacency
 //      (deterministic order) and chain the vertex-normal backward.
 #include <hip/hip_runtime.h>

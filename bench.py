@@ -98,6 +98,10 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
         "k_shade<1>": 256 * slots + 20 * cov,              # winners in, 20 B of outputs per covered pixel
         "k_bwd_shade": 256 * slots + (20 + 80) * cov,      # winners + upstream grads, 80-B gradient record out
         "k_bwd_geom": 256 * slots + 80 * cov + 72 * F,     # winners + gradient record in, per-face rows out
+        # fused backward: winners + R/T partial per tile, upstream grads per covered pixel, each
+        # face's packed record + ShadeRec read once and its 72-B gradient row written once (the
+        # per-pixel record gathers are cache traffic, reported by PMC as roofline.traffic)
+        "k_bwd_fused": (256 + 48) * slots + 20 * cov + (64 + 144 + 72) * F,
         "k_bin_count": 64 * F * views + 24 * F,            # face records out, mesh in
         "k_bin_fill": 64 * F * views + 4 * ent,            # face records in, list ids out
     }

@@ -240,7 +240,7 @@ DEFAULT_MAT = {"ambient": (1.0, 1.0, 1.0), "diffuse": (1.0, 1.0, 1.0), "specular
 
 def render_ref(verts, faces, R, T, intr, H, W, *, texture=None, light=DEFAULT_LIGHT, mat=DEFAULT_MAT,
                cam_center=(0.0, 0.0, 0.0), sigma=1e-4, gamma=1e-4, bg=(1.0, 1.0, 1.0), sigma_sil=1e-4,
-               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0):
+               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0, clip=False):
     """The reference CPU render path for one mesh shared by N views:
     depth = relu(zbuf[...,0]); sil = sigmoid_alpha_blend alpha; rgba = softmax_rgb_blend(phong).
     texture: None (white), ("vertex", vcolors (V,3)), ("uv", verts_uvs, faces_uvs, map (Ht,Wt,C)).
@@ -250,7 +250,7 @@ def render_ref(verts, faces, R, T, intr, H, W, *, texture=None, light=DEFAULT_LI
     fv = project_faces_torch(verts, faces, R, T, intr)
     first = torch.arange(N, dtype=torch.int64) * Fn
     count = torch.full((N,), Fn, dtype=torch.int64)
-    p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, False, False)
+    p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, clip, False)
     faces_packed = faces.long().repeat(N, 1)
     verts_packed_faces = faces_packed  # faces index the shared verts
     local = p2f.clone()

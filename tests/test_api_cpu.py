@@ -37,10 +37,11 @@ def test_unsupported_settings_raise():
     cams = PerspectiveCameras()
     r = MeshRenderer(MeshRasterizer(cams, RasterizationSettings(image_size=32, faces_per_pixel=4)),
                      SoftPhongShader(cameras=cams))
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError):    # K-deep soft path: the HIP rasterizer refuses CPU tensors
         r(m)
-    with pytest.raises(NotImplementedError):
-        DepthRender(torch.eye(3), (32, 32), faces_per_pixel=3, device="cpu")
+    d3 = DepthRender(torch.eye(3), (32, 32), faces_per_pixel=3, device="cpu")
+    with pytest.raises(RuntimeError):    # no CPU fallback behind the drop-in classes either
+        d3.render(m, torch.eye(3)[None], torch.tensor([[0.0, 0.0, 3.0]]))
     with pytest.raises(NotImplementedError):
         ColorRender(torch.eye(3), (32, 32), blur_radius=1e-4, device="cpu")
     with pytest.raises(AssertionError):
@@ -66,3 +67,33 @@ def test_cpu_tensors_fail_loudly():
     ren.build_color_renderer()
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         ren.render()
+
+
+def test_soft_shading_matches_oracle_on_cpu_fragments():
+    """soft_shading.py (the modular K > 1 shader) restates the same upstream formulas as the
+    oracle: fed the oracle's own K=3 fragments on the CPU, both give identical images."""
+    import torch
+
+    from oracle import oracle as O
+    from tests.helpers import canonical_views, mesh_arrays
+    from torch_renderer_amd import Meshes, TexturesVertex
+    from torch_renderer_amd import soft_shading as S
+    from torch_renderer_amd.mesh_renderer import BlendParams, Fragments, Materials, PointLights
+
+    H, W, N, Kf = 24, 24, 2, 3
+    verts, faces, _ = mesh_arrays("teapot")
+    R, T, intr, _ = canonical_views(verts, N, H, W)
+    vcol = torch.rand(verts.shape, generator=torch.Generator().manual_seed(2))
+    cc = torch.tensor([[0.1, 0.2, -0.3]])
+    ref = O.render_ref(verts, faces, R, T, intr, H, W, texture=("vertex", vcol), cam_center=cc, K=Kf, blur=1e-4,
+                       bg=(0.0, 0.5, 1.0))
+    frags = Fragments(ref["p2f"], ref["zbuf"], ref["bary"], ref["dists"])
+    meshes = Meshes([verts], [faces], TexturesVertex([vcol])).extend(N)
+    texels = S.sample_textures(meshes, frags)
+    colors = S.phong_shading(meshes, frags, texels, PointLights(location=((0.0, 0.0, -3.0),)), Materials(), cc)
+    bp = BlendParams(background_color=(0.0, 0.5, 1.0))
+    rgba = S.softmax_rgb_blend(colors, frags, bp)
+    sil = S.sigmoid_alpha_blend(frags, bp)
+    assert (ref["p2f"][..., 1] >= 0).any()
+    assert torch.allclose(rgba, ref["rgba"], atol=1e-6, rtol=0)
+    assert torch.allclose(sil[..., 3], ref["sil"], atol=1e-6, rtol=0)

@@ -15,9 +15,13 @@ argument meaning and outputs:
   raster + shade + blend, ``mr_render_forward``) and returns the shader's (N,H,W,4) image,
   differentiable w.r.t. vertex positions, R, T and vertex colours.
 
-Everything runs on the HIP kernels; there is no CPU fallback. Settings the MI355X path does not
-implement yet (K > 1 or blur > 0 through the shaders, near-plane clipping) raise
-``NotImplementedError`` rather than returning different numbers.
+* With ``faces_per_pixel > 1`` or ``blur_radius > 0`` (soft rasterization)
+  ``MeshRenderer`` runs the K-deep HIP rasterizer and then the shader's modular pass over the
+  stored fragments (soft_shading.py), exactly as upstream composes them.
+
+Rasterization always runs on the HIP kernels; there is no CPU fallback. Settings the MI355X path
+does not implement yet (near-plane clipping, cull_to_frustum) raise ``NotImplementedError``
+rather than returning different numbers.
 """
 from __future__ import annotations
 
@@ -205,13 +209,29 @@ class _SoftShader(torch.nn.Module):
         self.blend_params = blend_params if blend_params is not None else BlendParams()
 
     def forward(self, fragments, meshes, **kwargs):
-        raise NotImplementedError(
-            "shading stored Fragments is not a separate pass on the MI355X path: use MeshRenderer, which "
-            "rasterizes and shades in one fused launch")
+        raise NotImplementedError(f"{type(self).__name__} cannot shade stored fragments")
 
 
 class SoftPhongShader(_SoftShader):
-    """upstream mesh/shader.py SoftPhongShader: phong_shading + softmax_rgb_blend -> RGBA."""
+    """upstream mesh/shader.py SoftPhongShader: phong_shading + softmax_rgb_blend -> RGBA.
+
+    Called on stored Fragments (any faces_per_pixel) it runs the modular soft pass of
+    soft_shading.py; inside MeshRenderer with K = 1 and blur = 0 the fused launch shades instead."""
+
+    def forward(self, fragments, meshes, **kwargs):
+        from . import soft_shading as S
+
+        cameras = kwargs.get("cameras", self.cameras)
+        if cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward pass")
+        lights = kwargs.get("lights", self.lights)
+        materials = kwargs.get("materials", self.materials)
+        bp = kwargs.get("blend_params", self.blend_params)
+        texels = S.sample_textures(meshes, fragments)
+        colors = S.phong_shading(meshes, fragments, texels, lights, materials, cameras.get_camera_center())
+        znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
+        zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
+        return S.softmax_rgb_blend(colors, fragments, bp, znear=float(znear), zfar=float(zfar))
 
 
 class SoftSilhouetteShader(_SoftShader):
@@ -219,6 +239,11 @@ class SoftSilhouetteShader(_SoftShader):
 
     def __init__(self, blend_params=None):
         super().__init__(blend_params=blend_params)
+
+    def forward(self, fragments, meshes, **kwargs):
+        from . import soft_shading as S
+
+        return S.sigmoid_alpha_blend(fragments, kwargs.get("blend_params", self.blend_params))
 
 
 class MeshRenderer(torch.nn.Module):
@@ -231,9 +256,6 @@ class MeshRenderer(torch.nn.Module):
 
     def _config(self, cameras, H, W):
         rs = self.rasterizer.raster_settings
-        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0:
-            raise NotImplementedError("MeshRenderer: faces_per_pixel > 1 / blur_radius > 0 (soft rasterization) "
-                                      "is not implemented on the MI355X fused path yet")
         if rs.cull_to_frustum:
             raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
         sh = self.shader
@@ -277,7 +299,11 @@ class MeshRenderer(torch.nn.Module):
         cameras = kwargs.get("cameras", self.rasterizer.cameras)
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward pass")
-        H, W = self.rasterizer.raster_settings.hw()
+        rs = self.rasterizer.raster_settings
+        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0:
+            # soft rasterization: K-deep HIP raster, then the modular shader
+            return self.shader(self.rasterizer(meshes, **kwargs), meshes, **kwargs)
+        H, W = rs.hw()
         cfg = self._config(cameras, H, W)
         R, T, _ = _views(meshes, cameras, (H, W), kwargs)
         z_clip = _z_clip_value(cameras, self.rasterizer.raster_settings)

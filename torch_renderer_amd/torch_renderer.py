@@ -68,6 +68,22 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
     return {k: torch.cat([o[k] for o in outs], 0) for k in outs[0]}
 
 
+def _soft_renderers(r, faces_per_pixel, light_location):
+    """(MeshRasterizer, MeshRenderer) for faces_per_pixel > 1, as torch_renderer.py:90-108 (depth and
+    silhouette) and :132-153 (Phong, PointLights at `light_location`) build them."""
+    from .mesh_renderer import (MeshRasterizer, MeshRenderer, PointLights, RasterizationSettings,
+                                SoftPhongShader, SoftSilhouetteShader)
+
+    rasterizer = MeshRasterizer(cameras=r._cameras, raster_settings=RasterizationSettings(
+        image_size=r._image_size, blur_radius=0.0, faces_per_pixel=faces_per_pixel))
+    if light_location is None:
+        shader = SoftSilhouetteShader()
+    else:
+        shader = SoftPhongShader(device=r._device, cameras=r._cameras,
+                                 lights=PointLights(device=r._device, location=[list(light_location)]))
+    return rasterizer, MeshRenderer(rasterizer=rasterizer, shader=shader)
+
+
 class DifferentiableRenderer:
     """torch_renderer.py:39-80."""
 
@@ -105,12 +121,19 @@ class DepthRender(DifferentiableRenderer):
     def __init__(self, K, image_size, faces_per_pixel=1, device="cuda:0"):
         super().__init__(K, image_size, device)
         print("INFO: Initializing DepthRender ...")
-        if faces_per_pixel != 1:
-            raise NotImplementedError("DepthRender: faces_per_pixel > 1 is not implemented on the MI355X path yet")
-        self._faces_per_pixel = faces_per_pixel
+        self._faces_per_pixel = int(faces_per_pixel)
+        if self._faces_per_pixel != 1:
+            # K-deep soft path (torch_renderer.py:90-108): modular rasterizer + SoftSilhouetteShader
+            self._rasterizer, self._silhouette_renderer = _soft_renderers(self, self._faces_per_pixel, None)
 
     def render(self, meshes, R, tvec, return_silhouette=False):
         self._check_meshes(meshes)
+        if self._faces_per_pixel != 1:
+            Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
+            depths = torch.relu(self._rasterizer(meshes, R=Rs, T=ts).zbuf[..., 0])
+            if not return_silhouette:
+                return depths
+            return depths, self._silhouette_renderer(meshes, R=Rs, T=ts)[..., 3]
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], want_depth=True,
                           want_sil=bool(return_silhouette), want_rgb=False)
         out = render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)
@@ -129,12 +152,16 @@ class ColorRender(DifferentiableRenderer):
             # Upstream passes a BlendParams object as RasterizationSettings.blur_radius here
             # (torch_renderer.py:129,137), which cannot rasterize; refuse instead of guessing.
             raise NotImplementedError("ColorRender: blur_radius != 0 is broken in the reference; only 0 is supported")
-        if faces_per_pixel != 1:
-            raise NotImplementedError("ColorRender: faces_per_pixel > 1 is not implemented on the MI355X path yet")
         self._light_location = (0.0, 0.0, -3.0)
+        self._faces_per_pixel = int(faces_per_pixel)
+        if self._faces_per_pixel != 1:
+            _, self._phong_renderer = _soft_renderers(self, self._faces_per_pixel, self._light_location)
 
     def render(self, meshes, R, tvec):
         self._check_meshes(meshes)
+        if self._faces_per_pixel != 1:
+            Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
+            return self._phong_renderer(meshes, R=Rs, T=ts)[..., :3]
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location,
                           want_depth=False, want_sil=False, want_rgb=True)
         return render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)["rgb"]

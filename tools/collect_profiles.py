@@ -16,7 +16,7 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 def short(name):
     n = name.replace("void ", "").split("(")[0].strip()
-    m = re.match(r"(k_bwd_fused|k_bwd_geom|k_vgrad_a|k_vgrad_b|k_tile_raster|k_bin_count_world|k_bin_fill_world)<.*>", n)
+    m = re.match(r"(k_bwd_fused|k_rt_vgrad_a|k_bwd_geom|k_vgrad_a|k_vgrad_b|k_tile_raster|k_bin_count_world|k_bin_fill_world)<.*>", n)
     if m:
         return {"k_bin_count_world": "k_bin_count", "k_bin_fill_world": "k_bin_fill"}.get(m.group(1), m.group(1))
     m = re.match(r"k_shade<(\d+), *\d+>", n)

@@ -60,13 +60,14 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_BWD_FUSED, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
-                                              "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused"};
+                                              "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
+                                              "k_rt_vgrad_a"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -568,55 +569,44 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
   if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   const int* c = P.cnt + (int64_t)n * P.T;
-  // pass 1: entry offsets; unit and slot totals of the view
-  int run_e = 0, tot_u = 0, tot_s = 0;
-  for (int b0 = 0; b0 < P.T; b0 += 1024) {
-    const int tt = b0 + t;
-    const int cc = tt < P.T ? c[tt] : 0;
-    int te;
-    const int ie = block_incl_sum(cc, part, te);
-    const int ex = run_e + ie - cc;
-    run_e += te;
-    if (tt < P.T) {
-      P.start[(int64_t)n * P.T + tt] = ex;
-      P.cur[(int64_t)n * P.T + tt] = ex;
-    }
+  // Each thread owns a run of C consecutive tiles, so the view needs three block-wide scans
+  // (entries, units, slots) instead of three per 1024 tiles; slots and units still come out in
+  // tile order.
+  const int C = (P.T + 1023) / 1024;
+  const int t0 = min(t * C, P.T), t1 = min(t0 + C, P.T);
+  int le = 0;
+  for (int tt = t0; tt < t1; ++tt) le += c[tt];
+  int te;
+  const int ex0 = block_incl_sum(le, part, te) - le;  // view-local entry offset of tile t0
+  // pass 1: entry offsets; unit and slot counts of the run
+  int my_u = 0, my_s = 0;
+  for (int tt = t0, ex = ex0; tt < t1; ++tt) {
+    const int cc = c[tt];
+    P.start[(int64_t)n * P.T + tt] = ex;
+    P.cur[(int64_t)n * P.T + tt] = ex;
+    const bool ovf = cc > 0 && (vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb));
+    my_u += cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
+    my_s += cc > 0 ? 1 : 0;
+    ex += cc;
+  }
+  int au, as;
+  const int iu = block_incl_sum(my_u, part, au);
+  const int is = block_incl_sum(my_s, part, as);
+  if (t == 0) {
+    base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
+    base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
+    P.vslot[n] = base[1];
+    P.vslot[gridDim.x + n] = as;
+  }
+  __syncthreads();
+  // pass 2: units, slots, key init for shared slots
+  int u0 = base[0] + iu - my_u, slot = base[1] + is - my_s;
+  for (int tt = t0, ex = ex0; tt < t1; ++tt) {
+    const int cc = c[tt];
     const bool ovf = cc > 0 && (vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb));
     const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
-    tot_u += nu;
-    tot_s += cc > 0 ? 1 : 0;
-  }
-  {
-    const int su = wave_sum(tot_u), ss = wave_sum(tot_s);
-    if (lane == 0) { part[wave] = su; red[wave] = ss; }
-    __syncthreads();
-    if (t == 0) {
-      int au = 0, as = 0;
-      for (int k = 0; k < 16; ++k) { au += part[k]; as += (int)red[k]; }
-      base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
-      base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
-      P.vslot[n] = base[1];
-      P.vslot[gridDim.x + n] = as;
-    }
-    __syncthreads();
-  }
-  // pass 2: units, slots, key init for shared slots (each thread re-reads its own tiles)
-  int run_u = base[0], run_s = base[1];
-  for (int b0 = 0; b0 < P.T; b0 += 1024) {
-    const int tt = b0 + t;
-    const int cc = tt < P.T ? c[tt] : 0;
-    const int ex = tt < P.T ? P.start[(int64_t)n * P.T + tt] : 0;
-    const bool ovf = cc > 0 && (vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb));
-    const int nu = cc == 0 ? 0 : ovf ? 1 : (cc + MR_UE - 1) / MR_UE;
-    const int ns = cc > 0 ? 1 : 0;
-    int tu, ts;
-    const int iu = block_incl_sum(nu, part, tu);
-    const int is = block_incl_sum(ns, part, ts);
-    const int u0 = run_u + iu - nu, slot = run_s + is - ns;
-    run_u += tu;
-    run_s += ts;
     const int gt = n * P.T + tt;
-    if (ns) P.stile[slot] = gt;
+    if (cc > 0) P.stile[slot] = gt;
     const int multi = nu > 1 ? (int)0x80000000u : 0;
     for (int k = 0; k < nu; ++k) {
       int4 U;
@@ -630,6 +620,9 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
       P.tdone[slot] = nu - 1;
       for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
     }
+    u0 += nu;
+    slot += cc > 0 ? 1 : 0;
+    ex += cc;
   }
 }
 
@@ -1579,6 +1572,34 @@ __global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
 // the wave's LDS instead of HBM (80 B written + 80 B read per covered pixel), and the slot,
 // winners and face record are fetched once. Peak VGPRs stay those of the larger half: the
 // LDS hand-off ends the first half's live ranges.
+// Face record and upstream gradients (depth, silhouette, RGB) of one slot pixel; zeros when the
+// pixel is uncovered or the slot is past the end (f < 0).
+MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, FaceRec& r, float g[5]) {
+#pragma unroll
+  for (int i = 0; i < 5; ++i) g[i] = 0.0f;
+  if (f < 0) return;
+  int n, px, py;
+  slot_pixel(P, gt, lane, n, px, py);
+  const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
+  r = P.recs[f];
+  if (P.gD) g[0] = P.gD[pix];
+  if (P.gS) g[1] = P.gS[pix];
+  if (P.gRGB) {
+    const float* c = P.gRGB + pix * P.rgb_ch;
+    g[2] = c[0];
+    g[3] = c[1];
+    g[4] = c[2];
+  }
+}
+
+// Alpha-channel upstream gradient (RGBA outputs only; the drop-in frame has rgb_ch = 3).
+MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
+  int n, px, py;
+  slot_pixel(P, gt, lane, n, px, py);
+  const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
+  return P.gRGB[pix * P.rgb_ch + 3];
+}
+
 template <int ACC>
 __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   __shared__ float lrow[4][64 * ACC];
@@ -1588,28 +1609,46 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
   const int G = gridDim.x * 4;
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
-    const int gt = P.stile[s];
-    const int f = P.sface[(int64_t)s * 64 + lane];
+  // Three-deep software pipeline (the kernel runs at 2 waves/SIMD, so a wave must hide its own
+  // latency): while slot s is processed, the face record and upstream gradients of slot s + G
+  // and the tile id and winner of slot s + 2G are in flight.
+  int s = blockIdx.x * 4 + wave;
+  int gt_c = 0, f_c = -1, gt_n = 0, f_n = -1;
+  if (s < nslots) {
+    gt_c = P.stile[s];
+    f_c = P.sface[(int64_t)s * 64 + lane];
+  }
+  if (s + G < nslots) {
+    gt_n = P.stile[s + G];
+    f_n = P.sface[(int64_t)(s + G) * 64 + lane];
+  }
+  FaceRec r_c;
+  float g_c[5];
+  bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
+  for (; s < nslots; s += G) {
+    const int gt = gt_c, f = f_c;
+    const FaceRec r = r_c;
+    float gin[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
+    gt_c = gt_n;
+    f_c = f_n;
+    bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
+    gt_n = 0;
+    f_n = -1;
+    if (s + 2 * G < nslots) {
+      gt_n = P.stile[s + 2 * G];
+      f_n = P.sface[(int64_t)(s + 2 * G) * 64 + lane];
+    }
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (f >= 0) {
-      const int64_t HW = (int64_t)P.H * P.W;
-      const int64_t pix = n * HW + (int64_t)py * P.W + px;
-      const FaceRec r = P.recs[f];
       PixGeom Gm;
       load_geom(P.srec, (uint32_t)(f - n * P.F), Gm);
-      const float gD = P.gD ? P.gD[pix] : 0.0f;
-      const float gS = P.gS ? P.gS[pix] : 0.0f;
-      float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
-      if (P.gRGB) {
-        const float* g = P.gRGB + pix * P.rgb_ch;
-        gC[0] = g[0];
-        gC[1] = g[1];
-        gC[2] = g[2];
-        if (P.rgb_ch == 4) gA = g[3];
-      }
+      const float gD = gin[0], gS = gin[1];
+      float gC[3] = {gin[2], gin[3], gin[4]};
+      const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
       FragEval e;
       float4 o[MR_BWD_REC];
       if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
@@ -1645,7 +1684,6 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     int key = -1;
     if (f >= 0) {
       const int face = (int)(f - n * P.F);
-      const FaceRec r = P.recs[f];
       const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
       const float4 a3 = lrec[wave][3][lane];
       const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1683,10 +1721,10 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
-__global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                   int N, float* __restrict__ out) {
+MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N,
+                           float* __restrict__ out, int n) {
   __shared__ float sm[12][4];
-  const int n = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s0 = vslot[n], ns = vslot[N + n];
   for (int i = 0; i < 12; ++i) {
     float v = 0.0f;
@@ -1696,6 +1734,11 @@ __global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ par
   }
   __syncthreads();
   if (threadIdx.x < 12) out[n * 12 + threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + sm[threadIdx.x][2]) + sm[threadIdx.x][3];
+}
+
+__global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
+                                                   int N, float* __restrict__ out) {
+  rt_reduce_view(part, vslot, N, out, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1737,10 +1780,10 @@ __global__ void __launch_bounds__(256) k_vertex_normals(const float* __restrict_
 
 // A: gNu[v] = normalize_bwd(raw[v], sum of gface normal rows)
 template <int ACC>
-__global__ void __launch_bounds__(256) k_vgrad_a(int64_t V, const int32_t* __restrict__ ptr,
-                                                 const int32_t* __restrict__ adj, const float* __restrict__ gface,
-                                                 const float* __restrict__ vraw, float* __restrict__ gnu) {
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
+                          const float* __restrict__ gface, const float* __restrict__ vraw, float* __restrict__ gnu,
+                          int64_t blk) {
+  const int64_t v = blk * blockDim.x + threadIdx.x;
   if (v >= V) return;
   float g[3] = {0.f, 0.f, 0.f};
   for (int e = ptr[v]; e < ptr[v + 1]; ++e) {
@@ -1753,6 +1796,26 @@ __global__ void __launch_bounds__(256) k_vgrad_a(int64_t V, const int32_t* __res
   float gx[3];
   normalize3_bwd(x, nrm, den, g, gx);
   for (int k = 0; k < 3; ++k) gnu[3 * v + k] = gx[k];
+}
+
+template <int ACC>
+__global__ void __launch_bounds__(256) k_vgrad_a(int64_t V, const int32_t* __restrict__ ptr,
+                                                 const int32_t* __restrict__ adj, const float* __restrict__ gface,
+                                                 const float* __restrict__ vraw, float* __restrict__ gnu) {
+  vgrad_a_block<ACC>(V, ptr, adj, gface, vraw, gnu, blockIdx.x);
+}
+
+// The per-view R/T reduction and the vertex-normal gradient read disjoint inputs written by
+// k_bwd_fused, so one launch does both: blocks [0, N) reduce views, the rest run k_vgrad_a
+// (saves a dependent launch of two tiny kernels per step).
+template <int ACC>
+__global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ part, const int* __restrict__ vslot,
+                                                    int N, float* __restrict__ gviews, int64_t V,
+                                                    const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
+                                                    const float* __restrict__ gface, const float* __restrict__ vraw,
+                                                    float* __restrict__ gnu) {
+  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, gviews, blockIdx.x);
+  else vgrad_a_block<ACC>(V, ptr, adj, gface, vraw, gnu, (int64_t)blockIdx.x - N);
 }
 
 // B: grad_verts[v] = sum over incident (f, c) of position rows + cross-product backward of the face normal.
@@ -2251,15 +2314,15 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18><<<cap(f18), 256, 0, st>>>(P)));
     MR_CHECK_LAUNCH("k_bwd_fused");
   }
-  MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
-  MR_CHECK_LAUNCH("k_rt_reduce");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V, 256);
+  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
+  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
-    if (use_n) MR_TIMED(KID_VGRAD_A, st, (k_vgrad_a<27><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   } else {
-    if (use_n) MR_TIMED(KID_VGRAD_A, st, (k_vgrad_a<18><<<vb, 256, 0, st>>>(m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");

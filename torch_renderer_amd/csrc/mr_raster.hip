@@ -1779,30 +1779,33 @@ __global__ void __launch_bounds__(256) k_vertex_normals(const float* __restrict_
 }
 
 // A: gNu[v] = normalize_bwd(raw[v], sum of gface normal rows)
+#define MR_VL 8  // lanes per vertex in the CSR gathers of the vertex-gradient kernels
 template <int ACC>
 MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                           const float* __restrict__ gface, const float* __restrict__ vraw, float* __restrict__ gnu,
                           int64_t blk) {
-  const int64_t v = blk * blockDim.x + threadIdx.x;
-  if (v >= V) return;
+  // MR_VL lanes per vertex split its CSR entries, then a fixed xor-tree sums them (deterministic)
+  const int64_t gid = blk * blockDim.x + threadIdx.x;
+  const int64_t v = gid / MR_VL;
+  const int j = (int)(gid % MR_VL);
+  const bool act = v < V;
   float g[3] = {0.f, 0.f, 0.f};
-  for (int e = ptr[v]; e < ptr[v + 1]; ++e) {
-    const int f = adj[e] >> 2, c = adj[e] & 3;
-    for (int k = 0; k < 3; ++k) g[k] += gface[(int64_t)f * ACC + 9 + 3 * c + k];
+  if (act) {
+    for (int e = ptr[v] + j; e < ptr[v + 1]; e += MR_VL) {
+      const int f = adj[e] >> 2, c = adj[e] & 3;
+      for (int k = 0; k < 3; ++k) g[k] += gface[(int64_t)f * ACC + 9 + 3 * c + k];
+    }
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int o = MR_VL / 2; o > 0; o >>= 1) g[k] += __shfl_xor(g[k], o, 64);
+  if (!act || j != 0) return;
   const float x[3] = {vraw[3 * v], vraw[3 * v + 1], vraw[3 * v + 2]};
   const float nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
   const float den = smax(nrm, 1e-6f);
   float gx[3];
   normalize3_bwd(x, nrm, den, g, gx);
   for (int k = 0; k < 3; ++k) gnu[3 * v + k] = gx[k];
-}
-
-template <int ACC>
-__global__ void __launch_bounds__(256) k_vgrad_a(int64_t V, const int32_t* __restrict__ ptr,
-                                                 const int32_t* __restrict__ adj, const float* __restrict__ gface,
-                                                 const float* __restrict__ vraw, float* __restrict__ gnu) {
-  vgrad_a_block<ACC>(V, ptr, adj, gface, vraw, gnu, blockIdx.x);
 }
 
 // The per-view R/T reduction and the vertex-normal gradient read disjoint inputs written by
@@ -1825,10 +1828,13 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
                                                  const int32_t* __restrict__ adj, const float* __restrict__ gface,
                                                  const float* __restrict__ gnu, int use_normals,
                                                  float* __restrict__ gverts, float* __restrict__ gcol) {
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t v = gid / MR_VL;
+  const int j = (int)(gid % MR_VL);
+  const bool act = v < V;
   float g[3] = {0.f, 0.f, 0.f}, gc[3] = {0.f, 0.f, 0.f};
-  for (int e = ptr[v]; e < ptr[v + 1]; ++e) {
+  const int e0 = act ? ptr[v] + j : 0, e1 = act ? ptr[v + 1] : 0;
+  for (int e = e0; e < e1; e += MR_VL) {
     const int f = adj[e] >> 2, c = adj[e] & 3;
     for (int k = 0; k < 3; ++k) g[k] += gface[(int64_t)f * ACC + 3 * c + k];
     if (ACC == 27)
@@ -1851,6 +1857,13 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
       }
     }
   }
+#pragma unroll
+  for (int k = 0; k < 3; ++k)
+    for (int o = MR_VL / 2; o > 0; o >>= 1) {
+      g[k] += __shfl_xor(g[k], o, 64);
+      if (ACC == 27) gc[k] += __shfl_xor(gc[k], o, 64);
+    }
+  if (!act || j != 0) return;
   for (int k = 0; k < 3; ++k) gverts[3 * v + k] = g[k];
   if (ACC == 27 && gcol)
     for (int k = 0; k < 3; ++k) gcol[3 * v + k] = gc[k];
@@ -2315,7 +2328,7 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
     MR_CHECK_LAUNCH("k_bwd_fused");
   }
   const int use_n = sp->light_kind == 0;
-  const int vb = ceil_div(m->V, 256);
+  const int vb = ceil_div(m->V * MR_VL, 256);
   if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
   else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
   else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));

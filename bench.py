@@ -157,8 +157,8 @@ def main():
     nv = args.views
     R_all, t_all, K = canonical_views(verts0, nv * world, H, W)
     R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
-    R_cv = R_cv.to(dev).requires_grad_(True)
-    t_cv = t_cv.to(dev).requires_grad_(True)
+    R_cv = R_cv.to(dev).contiguous().requires_grad_(True)
+    t_cv = t_cv.to(dev).contiguous().requires_grad_(True)
     verts = meshes.shared_verts().clone().requires_grad_(True)
     bmesh = Meshes([verts], [faces], meshes.textures).extend(nv)
     renderer = DepthColorRender(K.to(dev), (H, W), device=dev)

@@ -37,6 +37,7 @@
 #define MR_TS 8         // raster tile edge: one 64-lane wave per 8x8 tile (lane = pixel)
 #define MR_BT 32        // tile edge of the modular (fragments) backward
 #define MR_HT 512       // LDS hash slots in the backward
+#define MR_BIN_FPT 2     // faces per thread in the world-space binning kernels (MR_BIN_FPT env overrides)
 #define MR_LDS_HIST 16384  // per-view tiles binned through an LDS histogram (else global atomics)
 
 static thread_local char g_err[512];
@@ -356,24 +357,27 @@ MR_DEV void world_face_verts(const float* __restrict__ verts, const int32_t* __r
 template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const float* __restrict__ verts,
                                                          const int32_t* __restrict__ faces, int64_t F,
-                                                         const ViewRec* __restrict__ views) {
+                                                         const ViewRec* __restrict__ views, int fpt) {
+  // fpt faces per thread: the per-block LDS histogram clear and flush (T entries each) are
+  // paid once per 256 * fpt faces
   extern __shared__ __attribute__((aligned(16))) int hist[];
   const int n = blockIdx.y;
   if (LDS) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
   }
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int mine = 0;
-  if (f < F) {
-    const ViewRec V = views[n];
+  const ViewRec V = views[n];
+  for (int k = 0; k < fpt; ++k) {
+    const int64_t f = ((int64_t)blockIdx.x * fpt + k) * blockDim.x + threadIdx.x;
+    if (f >= F) break;
     float v[3][3];
     world_face_verts(verts, faces, f, V, v);
     const FaceRec r = make_rec(P, (uint32_t)f, v);
     P.recs[(int64_t)n * F + f] = r;
     int tx0, tx1, ty0, ty1;
     if (rec_tiles(P, r, tx0, tx1, ty0, ty1)) {
-      mine = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+      mine += (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
       for (int ty = ty0; ty <= ty1; ++ty)
         for (int tx = tx0; tx <= tx1; ++tx) {
           const int t = ty * P.TX + tx;
@@ -390,41 +394,48 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
 }
 
 template <bool LDS>
-__global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F) {
+__global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F, int fpt) {
   extern __shared__ __attribute__((aligned(16))) int hist[];
   const int n = blockIdx.y;
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  FaceRec r;
-  int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
-  bool ok = false;
-  if (f < F) {
-    r = P.recs[(int64_t)n * F + f];
-    ok = rec_tiles(P, r, tx0, tx1, ty0, ty1);
-  }
-  const int rid = (int)((int64_t)n * F + f);
+  const int64_t f0 = (int64_t)blockIdx.x * fpt * blockDim.x + threadIdx.x;
   if (LDS) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    if (ok)
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+    for (int k = 0; k < fpt; ++k) {
+      const int64_t f = f0 + (int64_t)k * blockDim.x;
+      int tx0, tx1, ty0, ty1;
+      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
+        for (int ty = ty0; ty <= ty1; ++ty)
+          for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+    }
     __syncthreads();
     const int vb = P.vbase[n];
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
       if (hist[i]) hist[i] = vb + atomicAdd(&P.cur[(int64_t)n * P.T + i], hist[i]);  // reserve a block
     __syncthreads();
-    if (ok)
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-          const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
-          if (pos < P.list_cap) P.list[pos] = rid;
-        }
-  } else if (ok) {
-    for (int ty = ty0; ty <= ty1; ++ty)
-      for (int tx = tx0; tx <= tx1; ++tx) {
-        const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
-        if (pos < P.list_cap) P.list[pos] = rid;
-      }
+    for (int k = 0; k < fpt; ++k) {
+      const int64_t f = f0 + (int64_t)k * blockDim.x;
+      const int rid = (int)((int64_t)n * F + f);
+      int tx0, tx1, ty0, ty1;
+      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
+        for (int ty = ty0; ty <= ty1; ++ty)
+          for (int tx = tx0; tx <= tx1; ++tx) {
+            const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
+            if (pos < P.list_cap) P.list[pos] = rid;
+          }
+    }
+  } else {
+    for (int k = 0; k < fpt; ++k) {
+      const int64_t f = f0 + (int64_t)k * blockDim.x;
+      const int rid = (int)((int64_t)n * F + f);
+      int tx0, tx1, ty0, ty1;
+      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
+        for (int ty = ty0; ty <= ty1; ++ty)
+          for (int tx = tx0; tx <= tx1; ++tx) {
+            const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
+            if (pos < P.list_cap) P.list[pos] = rid;
+          }
+    }
   }
 }
 
@@ -2228,19 +2239,21 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.p2f32 = p2f32;
   MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
   MR_CHECK_LAUNCH("k_shade_rec");
-  dim3 sgrid(ceil_div(m->F, 256), (unsigned)N);
+  static const int fpt_env = getenv("MR_BIN_FPT") ? atoi(getenv("MR_BIN_FPT")) : 0;
+  const int fpt = fpt_env > 0 ? fpt_env : MR_BIN_FPT;
+  dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   if (lds)
-    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<true><<<sgrid, 256, shm, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, fpt)));
   else
-    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views)));
+    MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, fpt)));
   MR_CHECK_LAUNCH("k_bin_count_world");
   if ((rc = launch_scan(w, N, g, nullptr, m->F, st))) return rc;
   if (lds)
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F, fpt)));
   else
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F, fpt)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
   if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st);
   return launch_raster_and_shade<1, 3>(P, g, N, st);

@@ -55,6 +55,7 @@ class TexturesUV:
             verts_uvs = list(verts_uvs.unbind(0)) if verts_uvs.dim() == 3 else [verts_uvs]
         self._maps, self._faces_uvs, self._verts_uvs = list(maps), list(faces_uvs), list(verts_uvs)
         self._rgba_cache = None
+        self._idx_cache = None
 
     def maps_list(self):
         return self._maps
@@ -79,6 +80,16 @@ class TexturesUV:
 
     def __getitem__(self, i):
         return TexturesUV([self._maps[i]], [self._faces_uvs[i]], [self._verts_uvs[i]])
+
+    def kernel_uvs(self, i=0):
+        """(verts_uvs float32, faces_uvs int32) of mesh i, contiguous, as the kernels read them.
+        Cached per source tensor version, so a steady render loop (or a captured HIP graph)
+        launches no per-step cast/copy kernels."""
+        vu, fu = self._verts_uvs[i], self._faces_uvs[i]
+        key = (vu.data_ptr(), fu.data_ptr(), vu.device, getattr(vu, "_version", 0), getattr(fu, "_version", 0))
+        if self._idx_cache is None or self._idx_cache[0] != key:
+            self._idx_cache = (key, vu.float().contiguous(), fu.to(torch.int32).contiguous())
+        return self._idx_cache[1], self._idx_cache[2]
 
     def rgba_map(self, i=0):
         """(Ht, Wt, 4) float32 copy of map i, padded for 16-byte texel loads (cached)."""

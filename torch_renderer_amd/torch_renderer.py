@@ -30,8 +30,8 @@ def texture_args(meshes: Meshes, need_color: bool):
     if tex is None:
         raise ValueError("Meshes does not have textures")  # upstream Meshes.sample_textures
     if isinstance(tex, TexturesUV):
-        return TextureArgs(2, tex.verts_uvs_list()[0].float().contiguous(),
-                           tex.faces_uvs_list()[0].to(torch.int32).contiguous(), tex.rgba_map(0)), None
+        vuv, fuv = tex.kernel_uvs(0)
+        return TextureArgs(2, vuv, fuv, tex.rgba_map(0)), None
     if isinstance(tex, TexturesVertex):
         vc = tex.verts_features_list()[0]
         if vc.shape[-1] != 3:

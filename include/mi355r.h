@@ -150,6 +150,15 @@ int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, con
                            const float* grad_silhouette, const float* grad_rgb, const void* fwd_workspace,
                            void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts, float* grad_views,
                            float* grad_vcolors, void* stream);
+/* Same as mr_render_backward for views built by mr_views_from_opencv: the per-view pose
+ * gradients are written straight in the OpenCV frame, grad_R_cv (N,3,3) and grad_t_cv (N,3)
+ * (the chain rule of mr_view_grads_to_opencv fused into the reduction; torch_renderer.py:73-80). */
+int32_t mr_render_backward_opencv(const mr_mesh_t* mesh, const float* vnormals_raw, const mr_view_t* views, int64_t N,
+                                  const float* cam_centers, int64_t num_cam_centers, const mr_raster_settings_t* rs,
+                                  const mr_shade_params_t* sp, const float* grad_depth,
+                                  const float* grad_silhouette, const float* grad_rgb, const void* fwd_workspace,
+                                  void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts,
+                                  float* grad_R_cv, float* grad_t_cv, float* grad_vcolors, void* stream);
 
 /* ---------------- instrumentation ---------------- */
 /* Work counters left in `workspace` by the last mr_render_forward / mr_rasterize_meshes that used it

@@ -1732,8 +1732,10 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
+// out (N,12) PyTorch3D-frame R/T grads, or (gRcv, gtcv) non-null: the same grads written
+// straight in the OpenCV frame (k_view_grads_to_opencv's chain rule, saving its launch).
 MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N,
-                           float* __restrict__ out, int n) {
+                           float* __restrict__ out, float* __restrict__ gRcv, float* __restrict__ gtcv, int n) {
   __shared__ float sm[12][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s0 = vslot[n], ns = vslot[N + n];
@@ -1744,12 +1746,23 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
     if (lane == 0) sm[i][wave] = v;
   }
   __syncthreads();
-  if (threadIdx.x < 12) out[n * 12 + threadIdx.x] = ((sm[threadIdx.x][0] + sm[threadIdx.x][1]) + sm[threadIdx.x][2]) + sm[threadIdx.x][3];
+  const int i = threadIdx.x;
+  if (i >= 12) return;
+  const float v = ((sm[i][0] + sm[i][1]) + sm[i][2]) + sm[i][3];
+  if (!gRcv) {
+    out[n * 12 + i] = v;
+  } else if (i < 9) {  // dL/dR_cv[b][a] = dL/dR_p3d[a][b] * s[b]
+    const int a = i / 3, b = i - 3 * a;
+    gRcv[(int64_t)n * 9 + 3 * b + a] = b < 2 ? -v : v;
+  } else {
+    gtcv[(int64_t)n * 3 + (i - 9)] = i < 11 ? -v : v;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                   int N, float* __restrict__ out) {
-  rt_reduce_view(part, vslot, N, out, blockIdx.x);
+                                                   int N, float* __restrict__ out, float* __restrict__ gRcv,
+                                                   float* __restrict__ gtcv) {
+  rt_reduce_view(part, vslot, N, out, gRcv, gtcv, blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1824,11 +1837,12 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
 // (saves a dependent launch of two tiny kernels per step).
 template <int ACC>
 __global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                    int N, float* __restrict__ gviews, int64_t V,
+                                                    int N, float* __restrict__ gviews, float* __restrict__ gRcv,
+                                                    float* __restrict__ gtcv, int64_t V,
                                                     const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                                                     const float* __restrict__ gface, const float* __restrict__ vraw,
                                                     float* __restrict__ gnu) {
-  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, gviews, blockIdx.x);
+  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, gviews, gRcv, gtcv, blockIdx.x);
   else vgrad_a_block<ACC>(V, ptr, adj, gface, vraw, gnu, (int64_t)blockIdx.x - N);
 }
 
@@ -2268,17 +2282,43 @@ size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, 
   return off;
 }
 
+static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_t* views, int64_t N,
+                               const float* cc, int64_t ncc, const mr_raster_settings_t* s,
+                               const mr_shade_params_t* sp, const float* gD, const float* gS, const float* gRGB,
+                               const void* fws, void* bws, size_t bws_bytes, float* gverts, float* gviews,
+                               float* gRcv, float* gtcv, float* gcol, void* stream);
+
 int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_t* views, int64_t N, const float* cc,
                            int64_t ncc, const mr_raster_settings_t* s, const mr_shade_params_t* sp,
                            const float* gD, const float* gS, const float* gRGB, const void* fws, void* bws,
                            size_t bws_bytes, float* gverts, float* gviews, float* gcol, void* stream) {
+  if (!gviews) return set_err(MR_EINVAL, "NULL argument");
+  return render_backward(m, vraw, views, N, cc, ncc, s, sp, gD, gS, gRGB, fws, bws, bws_bytes, gverts, gviews,
+                         nullptr, nullptr, gcol, stream);
+}
+
+int32_t mr_render_backward_opencv(const mr_mesh_t* m, const float* vraw, const mr_view_t* views, int64_t N,
+                                  const float* cc, int64_t ncc, const mr_raster_settings_t* s,
+                                  const mr_shade_params_t* sp, const float* gD, const float* gS, const float* gRGB,
+                                  const void* fws, void* bws, size_t bws_bytes, float* gverts, float* grad_R_cv,
+                                  float* grad_t_cv, float* gcol, void* stream) {
+  if (!grad_R_cv || !grad_t_cv) return set_err(MR_EINVAL, "NULL argument");
+  return render_backward(m, vraw, views, N, cc, ncc, s, sp, gD, gS, gRGB, fws, bws, bws_bytes, gverts, nullptr,
+                         grad_R_cv, grad_t_cv, gcol, stream);
+}
+
+static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_t* views, int64_t N,
+                               const float* cc, int64_t ncc, const mr_raster_settings_t* s,
+                               const mr_shade_params_t* sp, const float* gD, const float* gS, const float* gRGB,
+                               const void* fws, void* bws, size_t bws_bytes, float* gverts, float* gviews,
+                               float* gRcv, float* gtcv, float* gcol, void* stream) {
   int rc = check_settings(s);
   if (rc) return rc;
   rc = check_mesh(m, sp);
   if (rc) return rc;
   if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
-  if (!fws || !bws || !gverts || !gviews) return set_err(MR_EINVAL, "NULL argument");
+  if (!fws || !bws || !gverts || (!gviews && !(gRcv && gtcv))) return set_err(MR_EINVAL, "NULL argument");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
   const size_t need = mr_render_backward_workspace(N, m->V, m->F, s->H, s->W);
   if (bws_bytes < need) return set_err(MR_EWORKSPACE, "backward workspace too small");
@@ -2342,9 +2382,9 @@ int32_t mr_render_backward(const mr_mesh_t* m, const float* vraw, const mr_view_
   }
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V * MR_VL, 256);
-  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews)));
-  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
-  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv)));
+  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));

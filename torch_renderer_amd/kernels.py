@@ -371,15 +371,18 @@ class RenderViews(torch.autograd.Function):
         bwb = L.mr_render_backward_workspace(N, v.shape[0], f.shape[0], cfg.H, cfg.W)
         bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
         c = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
+        if ctx.pose_cv:  # pose grads straight in the OpenCV frame (no separate conversion launch)
+            gR = torch.empty((N, 3, 3), device=dev)
+            gt = torch.empty((N, 3), device=dev)
+            check(L.mr_render_backward_opencv(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N,
+                                              ptr(cc), cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
+                                              ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gR),
+                                              ptr(gt), ptr(gcol), _lib.stream_handle(dev)))
+            return (gverts, gR, gt, gcol, None, None, None, None, None, None)
         check(L.mr_render_backward(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N, ptr(cc),
                                    cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
                                    ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gviews),
                                    ptr(gcol), _lib.stream_handle(dev)))
-        if ctx.pose_cv:
-            gR = torch.empty((N, 3, 3), device=dev)
-            gt = torch.empty((N, 3), device=dev)
-            check(L.mr_view_grads_to_opencv(ptr(gviews), N, ptr(gR), ptr(gt), _lib.stream_handle(dev)))
-            return (gverts, gR, gt, gcol, None, None, None, None, None, None)
         return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None, None)
 
 

@@ -1058,6 +1058,28 @@ __global__ void __launch_bounds__(256) k_shade_rec(ShadeParams S, int64_t F, Sha
   out[f] = R;
 }
 
+// k_shade_rec plus the binning counters' clear in one launch (the fused forward's first kernel):
+// blocks [0, ceil(F/256)) pack ShadeRecs, the rest zero `nzero` ints (per-tile counts, view
+// totals, work counters) with coalesced vector stores — replaces a separate memset.
+__global__ void __launch_bounds__(256) k_shade_rec_zero(ShadeParams S, int64_t F, ShadeRec* __restrict__ out,
+                                                        int* __restrict__ zero, int64_t nzero) {
+  const int64_t fb = (F + 255) / 256;
+  if ((int64_t)blockIdx.x < fb) {
+    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    ShadeRec R;
+    make_shade_rec(S, (uint32_t)f, R);
+    out[f] = R;
+    return;
+  }
+  const int64_t base = ((int64_t)blockIdx.x - fb) * 1024;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t i = base + k * 256 + threadIdx.x;
+    if (i < nzero) zero[i] = 0;
+  }
+}
+
 // Covered pixels: waves stride over the non-empty tiles' slots, one tile pixel per lane:
 // recompute the winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade
 // (M = 1) over the background k_tile_raster wrote.
@@ -2241,7 +2263,6 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
   RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, m->F);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
-  if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
   FwdParams P = make_fwd(s, g, w, N, nullptr, m->F);
   P.S = make_shade(m, sp, cc, ncc);
@@ -2251,8 +2272,9 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, w.srec)));
-  MR_CHECK_LAUNCH("k_shade_rec");
+  const int64_t nzero = (int64_t)(zero_bytes(N, g) / sizeof(int));
+  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec_zero<<<(unsigned)(ceil_div(m->F, 256) + ceil_div(nzero, 1024)), 256, 0, st>>>(P.S, m->F, w.srec, w.cnt, nzero)));
+  MR_CHECK_LAUNCH("k_shade_rec_zero");
   static const int fpt_env = getenv("MR_BIN_FPT") ? atoi(getenv("MR_BIN_FPT")) : 0;
   const int fpt = fpt_env > 0 ? fpt_env : MR_BIN_FPT;
   dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);

@@ -46,6 +46,9 @@ def lib():
         vp, i32, i64, f32 = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
         L.orc_raster_fwd.argtypes = [vp, vp, vp, i32, i32, i32, i32, f32, i32, i32, i32, vp, vp, vp, vp]
         L.orc_raster_fwd.restype = None
+        L.orc_raster_fwd_ex.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, i32, i32, i32, i32, i32, i32,
+                                        vp, vp, vp, vp]
+        L.orc_raster_fwd_ex.restype = None
         L.orc_raster_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]
         L.orc_raster_bwd.restype = None
         L.orc_project_faces.argtypes = [vp, vp, i64, vp, i32, vp]
@@ -60,7 +63,9 @@ def _p(t):
 
 
 # ---------------------------------------------------------------- rasterizer
-def raster_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=False, cull=False):
+def raster_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=False, cull=False, neighbor=None,
+               window=None):
+    """window = (y0, y1, x0, x1): rasterize only those pixels (others stay background)."""
     fv = face_verts.detach().float().contiguous().cpu()
     first = first.to(torch.int64).contiguous().cpu()
     count = count.to(torch.int64).contiguous().cpu()
@@ -69,8 +74,11 @@ def raster_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=F
     zbuf = torch.empty((N, H, W, K))
     bary = torch.empty((N, H, W, K, 3))
     dists = torch.empty((N, H, W, K))
-    lib().orc_raster_fwd(_p(fv), _p(first), _p(count), N, H, W, K, float(blur), int(persp), int(clip), int(cull),
-                         _p(p2f), _p(zbuf), _p(bary), _p(dists))
+    nb = None if neighbor is None else neighbor.to(torch.int64).contiguous().cpu()
+    wy0, wy1, wx0, wx1 = window if window is not None else (0, 0, 0, 0)
+    lib().orc_raster_fwd_ex(_p(fv), _p(first), _p(count), None if nb is None else _p(nb), N, H, W, K, float(blur),
+                            int(persp), int(clip), int(cull), wy0, wy1, wx0, wx1, _p(p2f), _p(zbuf), _p(bary),
+                            _p(dists))
     return p2f, zbuf, bary, dists
 
 
@@ -87,8 +95,9 @@ class RasterizeRef(torch.autograd.Function):
     """_RasterizeFaceVerts restated on the C oracle."""
 
     @staticmethod
-    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull):
-        p2f, zbuf, bary, dists = raster_fwd(face_verts, first, count, H, W, K, blur, persp, clip, cull)
+    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, neighbor=None, window=None):
+        p2f, zbuf, bary, dists = raster_fwd(face_verts, first, count, H, W, K, blur, persp, clip, cull, neighbor,
+                                            window)
         ctx.save_for_backward(face_verts, p2f)
         ctx.persp, ctx.clip = persp, clip
         ctx.mark_non_differentiable(p2f)
@@ -98,7 +107,7 @@ class RasterizeRef(torch.autograd.Function):
     def backward(ctx, _gp, gz, gb, gd):
         fv, p2f = ctx.saved_tensors
         g = raster_bwd(fv, p2f, gz, gb, gd, ctx.persp, ctx.clip)
-        return g, None, None, None, None, None, None, None, None, None
+        return g, None, None, None, None, None, None, None, None, None, None, None
 
 
 def project_faces_c(verts, faces, views):
@@ -127,6 +136,133 @@ def project_faces_torch(verts, faces, R, T, intr):
     ny = ay * (vy / vz) + by
     fv = torch.stack([nx, ny, vz], dim=-1)  # (N,F,3,3)
     return fv.reshape(-1, 3, 3)
+
+
+# ---------------------------------------------------------------- near-plane clipping
+def _clip_point(a, b, w, c, persp):
+    """Point on edge a->b (rows (x_ndc, y_ndc, z_view)) at view z = c, w = (c - za) / (zb - za).
+    Perspective: interpolate the view-linear ndc*z and divide by c (upstream clip.py
+    _find_verts_intersecting_clipping_plane); otherwise interpolate ndc linearly. z = c."""
+    if persp:
+        axw, ayw = a[:, 0] * a[:, 2], a[:, 1] * a[:, 2]
+        bxw, byw = b[:, 0] * b[:, 2], b[:, 1] * b[:, 2]
+        x = (axw + w * (bxw - axw)) / c
+        y = (ayw + w * (byw - ayw)) / c
+    else:
+        x = a[:, 0] + w * (b[:, 0] - a[:, 0])
+        y = a[:, 1] + w * (b[:, 1] - a[:, 1])
+    return torch.stack([x, y, torch.full_like(x, c)], dim=1)
+
+
+def clip_faces_ref(face_verts, first, count, z_clip, persp=True):
+    """upstream mesh/clip.py clip_faces restated (z plane only; cull_to_frustum off).
+
+    Per face (corners ordered i, j = i+1, k = i+2 mod 3) with b = #corners at view z < z_clip:
+      b = 0 -> unchanged; b = 3 -> culled;
+      b = 2 (front corner i) -> one triangle: slot i = p_i, slot j = p_ij, slot k = p_ik;
+      b = 1 (behind corner i) -> the quadrilateral p_ij, p_j, p_k, p_ik split into
+        t1 = (slot i = p_ij, j = p_j, k = p_k) and t2 = (slot i = p_ik, j = p_ij, k = p_k),
+        consecutive packed ids, each the other's clipped_faces_neighbor_idx;
+    p_ij is the point on edge i->j at z_clip. Sub-triangles keep the original orientation and
+    take the original's place in the packed order (culled faces drop out). conversion[t] (3,3):
+    row s = original-face barycentrics of the sub-triangle's slot-s vertex, so the original
+    barycentrics of a fragment are sum_s b_sub[s] * conversion[t][s].
+
+    Returns dict(face_verts (Fc,3,3), first (N), count (N), neighbor (Fc) i64, orig (Fc) i64,
+    conversion (Fc,3,3)). Differentiable w.r.t. face_verts (autograd through the torch ops)."""
+    fv = face_verts
+    F = fv.shape[0]
+    c = float(z_clip)
+    z = fv[:, :, 2]
+    behind = z < c
+    nb = behind.sum(1)
+    eye = torch.eye(3, dtype=fv.dtype)
+    ar = torch.arange(F)
+    # corner i per face: the single front corner (b = 2) or the single behind corner (b = 1)
+    i_front = torch.argmax((~behind).to(torch.int64), dim=1)
+    i_back = torch.argmax(behind.to(torch.int64), dim=1)
+    i = torch.where(nb == 2, i_front, i_back)
+    j, k = (i + 1) % 3, (i + 2) % 3
+    pi, pj, pk = fv[ar, i], fv[ar, j], fv[ar, k]
+    zi, zj, zk = pi[:, 2], pj[:, 2], pk[:, 2]
+    # only clipped faces use wj / wk; elsewhere the denominators may be 0 (and a masked NaN would
+    # still poison autograd), so they divide by 1 there
+    clipped = (nb == 1) | (nb == 2)
+    one = torch.ones_like(zi)
+    wj = (c - zi) / torch.where(clipped, zj - zi, one)
+    wk = (c - zi) / torch.where(clipped, zk - zi, one)
+    wj = torch.where(clipped, wj, torch.zeros_like(wj))
+    wk = torch.where(clipped, wk, torch.zeros_like(wk))
+    pij = _clip_point(pi, pj, wj, c, persp)
+    pik = _clip_point(pi, pk, wk, c, persp)
+    ei, ej, ek = eye[i], eye[j], eye[k]
+    cij = (1.0 - wj)[:, None] * ei + wj[:, None] * ej
+    cik = (1.0 - wk)[:, None] * ei + wk[:, None] * ek
+
+    def slots(a, b_, c_):  # rows placed at slots (i, j, k)
+        out = torch.zeros(F, 3, a.shape[1], dtype=fv.dtype)
+        out = out.index_put((ar, i), a).index_put((ar, j), b_).index_put((ar, k), c_)
+        return out
+
+    t_case2 = slots(pi, pij, pik)
+    c_case2 = slots(ei, cij, cik)
+    t1 = slots(pij, pj, pk)
+    c1 = slots(cij, ej, ek)
+    t2 = slots(pik, pij, pk)
+    c2 = slots(cik, cij, ek)
+    eye3 = eye.expand(F, 3, 3)
+    first_t = torch.where((nb == 2)[:, None, None], t_case2, torch.where((nb == 1)[:, None, None], t1, fv))
+    first_c = torch.where((nb == 2)[:, None, None], c_case2, torch.where((nb == 1)[:, None, None], c1, eye3))
+    keep = nb < 3
+    quad = nb == 1
+    verts_out, conv_out, orig, nbr = [], [], [], []
+    n_out = torch.zeros(len(first), dtype=torch.int64)
+    mesh = torch.zeros(F, dtype=torch.int64)
+    for m in range(len(first)):
+        mesh[int(first[m]):int(first[m]) + int(count[m])] = m
+    pos = 0
+    idx_first, idx_second = [], []
+    for f in range(F):
+        if not bool(keep[f]):
+            continue
+        idx_first.append((f, pos))
+        orig.append(f)
+        nbr.append(pos + 1 if bool(quad[f]) else -1)
+        n_out[mesh[f]] += 1
+        pos += 1
+        if bool(quad[f]):
+            idx_second.append((f, pos))
+            orig.append(f)
+            nbr.append(pos - 1)
+            n_out[mesh[f]] += 1
+            pos += 1
+    Fc = pos
+    order = torch.empty(Fc, dtype=torch.int64)
+    which = torch.zeros(Fc, dtype=torch.bool)
+    for f, p_ in idx_first:
+        order[p_] = f
+    for f, p_ in idx_second:
+        order[p_] = f
+        which[p_] = True
+    verts = torch.where(which[:, None, None], t2[order], first_t[order])
+    conv = torch.where(which[:, None, None], c2[order], first_c[order])
+    cnt = n_out
+    fst = torch.cumsum(cnt, 0) - cnt
+    return {"face_verts": verts, "first": fst, "count": cnt, "neighbor": torch.tensor(nbr, dtype=torch.int64),
+            "orig": torch.tensor(orig, dtype=torch.int64), "conversion": conv}
+
+
+def unclip_fragments(p2f, bary, clip):
+    """convert_clipped_rasterization_to_original_faces: packed ids of the original faces and the
+    original-face barycentrics sum_s b_sub[s] * conversion[s] (explicit (s0 + s1) + s2 order)."""
+    valid = p2f >= 0
+    idx = p2f.clamp(min=0)
+    conv = clip["conversion"][idx]  # (..., 3, 3)
+    b = bary
+    ob = (b[..., 0:1] * conv[..., 0, :] + b[..., 1:2] * conv[..., 1, :]) + b[..., 2:3] * conv[..., 2, :]
+    ob = torch.where(valid[..., None], ob, bary)
+    op2f = torch.where(valid, clip["orig"][idx], p2f)
+    return op2f, ob
 
 
 # ---------------------------------------------------------------- mesh / shading restatement
@@ -240,7 +376,7 @@ DEFAULT_MAT = {"ambient": (1.0, 1.0, 1.0), "diffuse": (1.0, 1.0, 1.0), "specular
 
 def render_ref(verts, faces, R, T, intr, H, W, *, texture=None, light=DEFAULT_LIGHT, mat=DEFAULT_MAT,
                cam_center=(0.0, 0.0, 0.0), sigma=1e-4, gamma=1e-4, bg=(1.0, 1.0, 1.0), sigma_sil=1e-4,
-               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0, clip=False):
+               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0, clip=False, z_clip=None, window=None):
     """The reference CPU render path for one mesh shared by N views:
     depth = relu(zbuf[...,0]); sil = sigmoid_alpha_blend alpha; rgba = softmax_rgb_blend(phong).
     texture: None (white), ("vertex", vcolors (V,3)), ("uv", verts_uvs, faces_uvs, map (Ht,Wt,C)).
@@ -250,7 +386,13 @@ def render_ref(verts, faces, R, T, intr, H, W, *, texture=None, light=DEFAULT_LI
     fv = project_faces_torch(verts, faces, R, T, intr)
     first = torch.arange(N, dtype=torch.int64) * Fn
     count = torch.full((N,), Fn, dtype=torch.int64)
-    p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, clip, False)
+    if z_clip is None:
+        p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, clip, False, None, window)
+    else:  # MeshRasterizer with a znear camera: clip_faces -> raster -> convert back (upstream clip.py)
+        cf = clip_faces_ref(fv, first, count, z_clip, persp)
+        p2f_c, zbuf, bary_c, dists = RasterizeRef.apply(cf["face_verts"], cf["first"], cf["count"], H, W, K, blur,
+                                                        persp, clip, False, cf["neighbor"], window)
+        p2f, bary = unclip_fragments(p2f_c, bary_c, cf)
     faces_packed = faces.long().repeat(N, 1)
     verts_packed_faces = faces_packed  # faces index the shared verts
     local = p2f.clone()

@@ -27,8 +27,9 @@
  *     (PyTorch3D's std::sort over NaN keys is undefined behaviour);
  *   - the final K entries are written in ascending (z, face) order (the CUDA
  *     path's order; identical to CPU for K=1);
- *   - z-clipping (clipped_faces_neighbor_idx != -1) is not restated: callers
- *     raise before reaching it.
+ *   - z-clipping: clipped_faces_neighbor_idx (the two triangles a face clipped
+ *     into a quadrilateral is split into) follows the CPU rule as restated in
+ *     orc_raster_fwd_ex; the clipping itself is restated in oracle.py.
  *
  * Also restated here: the world->NDC projection used by the MI355X kernels
  * (explicit operand order, see DESIGN.md "Projection"), so parity tests can
@@ -146,14 +147,21 @@ static inline int finite9(const float* fv) {
 /*
  * RasterizeMeshesNaiveCpu restated.
  * face_verts (F,3,3) f32 NDC xy + view z; mesh_first/mesh_count (N) i64.
+ * neighbor (F) i64 or NULL: clipped_faces_neighbor_idx (-1 = none). When face f's neighbour
+ * (the other half of its clipped quadrilateral) is already among the pixel's kept faces, f
+ * replaces it iff f's unsigned distance is smaller than the neighbour's |signed distance|, and
+ * is otherwise dropped; f is handled as a normal face when the neighbour is not kept.
+ * Pixel window [y0, y1) x [x0, x1) (the whole image when y1 <= 0): outputs outside it keep the
+ * background, so a large image can be checked on a crop.
  * Outputs (N,H,W,K): p2f i64, zbuf f32, dists f32; bary (N,H,W,K,3).
  * Background: -1 everywhere (as torch::full(..., -1)).
  */
-void orc_raster_fwd(const float* face_verts, const int64_t* mesh_first, const int64_t* mesh_count,
-                    int N, int H, int W, int K, float blur_radius, int perspective_correct,
-                    int clip_barycentric_coords, int cull_backfaces, int64_t* p2f, float* zbuf,
-                    float* bary, float* dists) {
+void orc_raster_fwd_ex(const float* face_verts, const int64_t* mesh_first, const int64_t* mesh_count,
+                       const int64_t* neighbor, int N, int H, int W, int K, float blur_radius,
+                       int perspective_correct, int clip_barycentric_coords, int cull_backfaces, int wy0, int wy1,
+                       int wx0, int wx1, int64_t* p2f, float* zbuf, float* bary, float* dists) {
   const float bbox_pad = sqrtf(blur_radius);
+  if (wy1 <= 0) { wy0 = 0; wy1 = H; wx0 = 0; wx1 = W; }
 #pragma omp parallel for collapse(2) schedule(dynamic, 1)
   for (int n = 0; n < N; ++n) {
     for (int yi = 0; yi < H; ++yi) {
@@ -164,7 +172,8 @@ void orc_raster_fwd(const float* face_verts, const int64_t* mesh_first, const in
         const float xf = pix_to_ndc(W - 1 - xi, W, H);
         const v2f p = {xf, yf};
         int qn = 0;
-        for (int64_t f = f0; f < f1; ++f) {
+        const int in_win = yi >= wy0 && yi < wy1 && xi >= wx0 && xi < wx1;
+        for (int64_t f = f0; in_win && f < f1; ++f) {
           const float* fv = face_verts + f * 9;
           if (!finite9(fv)) continue;
           const float x0 = fv[0], y0 = fv[1], z0 = fv[2];
@@ -195,6 +204,17 @@ void orc_raster_fwd(const float* face_verts, const int64_t* mesh_first, const in
           const int inside = b[0] > 0.0f && b[1] > 0.0f && b[2] > 0.0f;
           const float sdist = inside ? -dist : dist;
           if (!inside && dist >= blur_radius) continue;
+          const int64_t nb = neighbor ? neighbor[f] : -1;
+          int at = -1;
+          for (int i = 0; nb != -1 && i < qn; ++i)
+            if (q[i].f == nb) { at = i; break; }
+          if (at >= 0) {  /* the other half of a clipped quad is kept: keep the nearer-edged one */
+            if (dist < fabsf(q[at].d)) {
+              q[at].z = pz; q[at].f = f; q[at].d = sdist;
+              q[at].b0 = bc[0]; q[at].b1 = bc[1]; q[at].b2 = bc[2];
+            }
+            continue;
+          }
           q[qn].z = pz; q[qn].f = f; q[qn].d = sdist;
           q[qn].b0 = bc[0]; q[qn].b1 = bc[1]; q[qn].b2 = bc[2];
           ++qn;
@@ -217,6 +237,14 @@ void orc_raster_fwd(const float* face_verts, const int64_t* mesh_first, const in
       free(q);
     }
   }
+}
+
+void orc_raster_fwd(const float* face_verts, const int64_t* mesh_first, const int64_t* mesh_count,
+                    int N, int H, int W, int K, float blur_radius, int perspective_correct,
+                    int clip_barycentric_coords, int cull_backfaces, int64_t* p2f, float* zbuf,
+                    float* bary, float* dists) {
+  orc_raster_fwd_ex(face_verts, mesh_first, mesh_count, NULL, N, H, W, K, blur_radius, perspective_correct,
+                    clip_barycentric_coords, cull_backfaces, 0, 0, 0, 0, p2f, zbuf, bary, dists);
 }
 
 /* ---------------- backward helpers (geometry_utils.h) ---------------- */

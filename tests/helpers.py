@@ -32,3 +32,36 @@ def canonical_views(verts, N, H, W, dist=None, fov_deg=60.0, seed=0, elev_range=
     s = min(H, W) / 2.0
     intr = torch.tensor([[f / s, (W / 2.0 - K[0, 2].item()) / s, f / s, (H / 2.0 - K[1, 2].item()) / s]]).expand(N, 4)
     return R.float(), T.float(), intr.float().contiguous(), (R_cv, t_cv, K)
+
+
+def cv_to_p3d(R, t):
+    """torch_renderer.py:73-80 restated for the oracle side (R^T, negate columns 0,1; negate t0,t1)."""
+    Rp = R.transpose(1, 2).clone()
+    Rp[:, :, :2] = -Rp[:, :, :2]
+    Tp = t.clone()
+    Tp[:, :2] = -Tp[:, :2]
+    return Rp, Tp
+
+
+def intr_from_K(K, H, W, N):
+    """(N,4) ax, bx, ay, by of PerspectiveCameras(in_ndc=False) for a pixel K (torch_renderer.py:61-71)."""
+    s = min(H, W) / 2.0
+    return torch.tensor([[K[0, 0] / s, (W / 2.0 - K[0, 2]) / s, K[1, 1] / s,
+                          (H / 2.0 - K[1, 2]) / s]]).expand(N, 4).contiguous()
+
+
+def report(name, got, ref, tol=1e-4, rel_above_one=True):
+    """Compare a GPU tensor with the oracle's. Prints the absolute error next to the value scale.
+    Bar: |err| <= tol absolute for values of scale <= 1; for larger values (vertex / pose gradients,
+    which carry the 1/sigma = 1e4 factor of the soft blends and sum thousands of f32 terms in a
+    different order on each side) |err| <= tol * scale."""
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    assert got.shape == ref.shape, (name, got.shape, ref.shape)
+    assert torch.isfinite(got).all(), f"{name}: non-finite values"
+    err = (got - ref).abs().max().item() if got.numel() else 0.0
+    scale = ref.abs().max().item() if ref.numel() else 0.0
+    bar = tol * max(1.0, scale) if rel_above_one else tol
+    print(f"[parity] {name}: max|err| = {err:.3e}, scale = {scale:.3e}, bar = {bar:.3e}")
+    assert err <= bar, f"{name}: max abs err {err:.3e} > {bar:.3e} (scale {scale:.3e})"
+    return err, scale

@@ -46,6 +46,23 @@ class CamerasBase:
     def ndc_affine(self, image_size):  # (N,4): ax, bx, ay, by
         raise NotImplementedError
 
+    def __getitem__(self, i):
+        """Camera i of the batch (mesh_deformer.py:197 renders with ``target_cameras[j]``): every
+        per-camera tensor attribute with a batch dimension > 1 is sliced, singletons broadcast."""
+        import copy
+
+        n = len(self)
+        if not -n <= i < n:
+            raise IndexError(f"camera index {i} out of range for a batch of {n}")
+        c = copy.copy(self)
+        c.__dict__ = {k: v for k, v in self.__dict__.items() if not k.startswith("_") or k in ("_in_ndc",)}
+        for k, v in list(c.__dict__.items()):
+            if torch.is_tensor(v) and v.dim() >= 1 and v.shape[0] == n and n > 1 and k != "image_size":
+                c.__dict__[k] = v[i:i + 1]
+        if hasattr(self, "_n_intr"):
+            c._n_intr = 1 if self._n_intr > 1 else self._n_intr
+        return c
+
     def to(self, device):
         self.device = torch.device(device)
         for k, v in list(self.__dict__.items()):

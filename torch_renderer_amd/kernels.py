@@ -238,6 +238,7 @@ class ShadeConfig:
     want_rgb: bool = True
     rgb_channels: int = 3
     want_p2f: bool = False  # also return the (N,H,W) int32 packed face ids (tests / tools)
+    z_clip: float | None = None  # near clip plane (view z) of FoVPerspectiveCameras: znear / 2
 
     def raster_struct(self):
         return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,

@@ -64,15 +64,31 @@ class BlendParams:
     background_color: tuple = (1.0, 1.0, 1.0)
 
 
-def _triple(x, default):
+def _bg_triple(bp):
+    """background_color as floats, converted once per BlendParams object (cached on it)."""
+    key = id(bp.background_color)
+    c = bp.__dict__.get("_bg_cache")
+    if c is None or c[0] != key:
+        c = (key, _triple(bp.background_color, None, "BlendParams.background_color"))
+        bp.__dict__["_bg_cache"] = c
+    return c[1]
+
+
+def _triple(x, default, what="lights/materials"):
+    """One RGB (or xyz) triple as Python floats, converted ONCE at construction (a device tensor
+    costs one host read here, never per render call). Differentiable light / material
+    parameters are not supported by the fused kernels: refuse them instead of dropping the
+    gradient."""
     if x is None:
         x = default
+    if torch.is_tensor(x) and x.requires_grad:
+        raise NotImplementedError(f"{what}: parameters that require grad are not supported on the MI355X path")
     t = torch.as_tensor(x, dtype=torch.float32).reshape(-1)
     if t.numel() == 1:
         t = t.expand(3)
     if t.numel() != 3:
-        raise NotImplementedError("lights/materials: one colour per batch (3 values) is supported")
-    return tuple(float(v) for v in t)
+        raise NotImplementedError(f"{what}: one colour per batch (3 values) is supported")
+    return tuple(float(v) for v in t.cpu())
 
 
 class PointLights:
@@ -84,10 +100,11 @@ class PointLights:
         self.diffuse_color = _triple(diffuse_color, None)
         self.specular_color = _triple(specular_color, None)
         self.location = location
+        self._location = _triple(location, None, "PointLights.location")
         self.device = device
 
     def location_tuple(self):
-        return _triple(self.location, None)
+        return self._location
 
 
 class AmbientLights:
@@ -106,7 +123,9 @@ class Materials:
         self.ambient_color = _triple(ambient_color, None)
         self.diffuse_color = _triple(diffuse_color, None)
         self.specular_color = _triple(specular_color, None)
-        self.shininess = float(torch.as_tensor(shininess).reshape(-1)[0])
+        if torch.is_tensor(shininess) and shininess.requires_grad:
+            raise NotImplementedError("Materials.shininess: parameters that require grad are not supported")
+        self.shininess = float(torch.as_tensor(shininess).reshape(-1)[0].cpu())
         self.device = device
 
 
@@ -159,8 +178,9 @@ class MeshRasterizer(torch.nn.Module):
         self.cameras = cameras
         self.raster_settings = raster_settings or RasterizationSettings()
 
-    def transform(self, meshes: Meshes, **kwargs):
+    def transform(self, meshes_world: Meshes, **kwargs):
         """Packed face_verts (sum F_n, 3, 3): NDC xy + view z, packed ids n*F + f."""
+        meshes = meshes_world
         cameras = kwargs.get("cameras", self.cameras)
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward pass")
@@ -177,11 +197,14 @@ class MeshRasterizer(torch.nn.Module):
                                             intr[i:i + 1].contiguous()))
         return torch.cat(parts, 0)
 
-    def forward(self, meshes: Meshes, **kwargs) -> Fragments:
+    def forward(self, meshes_world: Meshes, **kwargs) -> Fragments:
+        """upstream signature: forward(meshes_world, **kwargs) (camera_pose_optimizer.py:175-177,244
+        call it as rasterizer(meshes_world=..., R=..., T=...))."""
+        meshes = meshes_world
         cameras = kwargs.get("cameras", self.cameras)
         rs = kwargs.get("raster_settings", self.raster_settings)
         H, W = rs.hw()
-        fv = self.transform(meshes, **kwargs)
+        fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
         _check_no_clipping(fv, _z_clip_value(cameras, rs), rs.cull_to_frustum)
         persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
         clip = rs.blur_radius > 0.0 if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
@@ -254,27 +277,30 @@ class MeshRenderer(torch.nn.Module):
         self.rasterizer = rasterizer
         self.shader = shader
 
-    def _config(self, cameras, H, W):
-        rs = self.rasterizer.raster_settings
+    def _config(self, cameras, rs, H, W, kwargs):
+        """ShadeConfig of one fused call. Per-call ``lights=``, ``materials=``, ``blend_params=``
+        override the shader's own, as upstream SoftPhongShader.forward does (the reference passes
+        ``lights=`` on every call: mesh_deformer.py:153,197, deform_mesh_with_color.py:185,342)."""
         if rs.cull_to_frustum:
             raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
         sh = self.shader
-        bp = sh.blend_params
+        bp = kwargs.get("blend_params", sh.blend_params)
         persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
         clip = False if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
-        znear = getattr(cameras, "znear", 1.0)
-        zfar = getattr(cameras, "zfar", 100.0)
+        znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
+        zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
         cfg = ShadeConfig(H=H, W=W, persp=persp, clip=clip, cull=bool(rs.cull_backfaces),
                           max_faces_per_bin=rs.max_faces_per_bin, sigma_rgb=float(bp.sigma), gamma=float(bp.gamma),
-                          background=_triple(bp.background_color, None), znear=float(znear), zfar=float(zfar),
-                          sigma_sil=float(bp.sigma), want_depth=False)
+                          background=_bg_triple(bp), znear=float(znear), zfar=float(zfar),
+                          sigma_sil=float(bp.sigma), want_depth=False, z_clip=_z_clip_value(cameras, rs))
         if isinstance(sh, SoftSilhouetteShader):
             cfg.want_rgb = False
             cfg.want_sil = True
             return cfg
         if not isinstance(sh, SoftPhongShader):
             raise NotImplementedError(f"shader {type(sh).__name__} is not implemented on the MI355X path")
-        lights, mats = sh.lights, sh.materials
+        lights = kwargs.get("lights", sh.lights)
+        mats = kwargs.get("materials", sh.materials)
         if isinstance(lights, AmbientLights):
             cfg.light_kind = 1
             cfg.light_ambient = lights.ambient_color
@@ -293,22 +319,28 @@ class MeshRenderer(torch.nn.Module):
         cfg.rgb_channels = 4
         return cfg
 
-    def forward(self, meshes: Meshes, **kwargs) -> torch.Tensor:
+    def forward(self, meshes_world: Meshes, **kwargs) -> torch.Tensor:
+        """upstream signature: forward(meshes_world, **kwargs) (camera_pose_optimizer.py:177)."""
         from .torch_renderer import render_mesh_batch
 
+        meshes = meshes_world
         cameras = kwargs.get("cameras", self.rasterizer.cameras)
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward pass")
-        rs = self.rasterizer.raster_settings
-        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0:
-            # soft rasterization: K-deep HIP raster, then the modular shader
+        rs = kwargs.get("raster_settings", self.rasterizer.raster_settings)
+        from .torch_renderer import textures_need_modular
+
+        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0 or (
+                isinstance(self.shader, SoftPhongShader) and textures_need_modular(meshes)):
+            # soft rasterization (SURVEY §8f rank 1), or a texture map that needs gradients: the HIP
+            # raster, then the shader over the fragments (differentiable w.r.t. the map and uvs)
             return self.shader(self.rasterizer(meshes, **kwargs), meshes, **kwargs)
         H, W = rs.hw()
-        cfg = self._config(cameras, H, W)
+        cfg = self._config(cameras, rs, H, W, kwargs)
         R, T, _ = _views(meshes, cameras, (H, W), kwargs)
-        z_clip = _z_clip_value(cameras, self.rasterizer.raster_settings)
-        if z_clip is not None:
-            _check_no_clipping(self.rasterizer.transform(meshes, cameras=cameras, R=R, T=T).detach(), z_clip, False)
+        if cfg.z_clip is not None:
+            _check_no_clipping(self.rasterizer.transform(meshes, cameras=cameras, R=R, T=T,
+                                                         raster_settings=rs).detach(), cfg.z_clip, False)
         # specular camera position: cameras.get_camera_center() without the R/T kwargs (upstream
         # shading.py), i.e. from the camera object's own R, T
         out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg)

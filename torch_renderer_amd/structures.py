@@ -38,6 +38,9 @@ class TexturesVertex:
     def __getitem__(self, i):
         return TexturesVertex([self._feats[i]])
 
+    def requires_grad(self) -> bool:
+        return False  # vertex colours are a differentiable input of the fused kernels
+
 
 class TexturesUV:
     """UV texture (upstream TexturesUV; defaults align_corners=True,
@@ -80,6 +83,12 @@ class TexturesUV:
 
     def __getitem__(self, i):
         return TexturesUV([self._maps[i]], [self._faces_uvs[i]], [self._verts_uvs[i]])
+
+    def requires_grad(self) -> bool:
+        """True when a map or verts_uvs tensor requires grad (deform_mesh_with_color.py:269-271,329):
+        the fused K=1 kernels sample a cached copy and carry no gradient to them, so such renders
+        take the modular path (HIP raster + differentiable shading over the fragments)."""
+        return any(t.requires_grad for t in self._maps + self._verts_uvs)
 
     def kernel_uvs(self, i=0):
         """(verts_uvs float32, faces_uvs int32) of mesh i, contiguous, as the kernels read them.
@@ -225,6 +234,40 @@ class Meshes:
         sizes = [v.shape[0] for v in self._verts_list]
         offs = vert_offsets_packed.split(sizes, 0)
         return Meshes([v + o for v, o in zip(self._verts_list, offs)], self._faces_list, self.textures)
+
+    def offset_verts_(self, vert_offsets_packed):
+        """In-place offset (mesh_deformer.py:103): a (3,) offset applies to every vertex, a
+        (sum V, 3) one per packed vertex (a shared/extended batch takes a per-source-vertex (V,3)
+        offset, which keeps it shared)."""
+        off = torch.as_tensor(vert_offsets_packed, dtype=self._verts_list[0].dtype, device=self.device)
+        if off.dim() == 1 or off.shape[0] == 1:
+            self._verts_list = [v + off.reshape(1, 3) for v in self._verts_list]
+            return self
+        if self._shared is not None:
+            V = self._verts_list[0].shape[0]
+            if off.shape[0] == V:
+                self._verts_list = [self._verts_list[0] + off]
+                return self
+            raise ValueError("offset_verts_ on an extended batch needs one (V,3) offset shared by all meshes")
+        sizes = [v.shape[0] for v in self._verts_list]
+        if off.shape[0] != sum(sizes):
+            raise ValueError("Verts offsets must have dimension (all_v, 3).")
+        self._verts_list = [v + o for v, o in zip(self._verts_list, off.split(sizes, 0))]
+        return self
+
+    def scale_verts_(self, scale):
+        """In-place uniform scale per mesh (mesh_deformer.py:104): a float or an (N,) tensor."""
+        sc = torch.as_tensor(scale, dtype=self._verts_list[0].dtype, device=self.device).reshape(-1)
+        if sc.numel() == 1:
+            self._verts_list = [v * sc for v in self._verts_list]
+            return self
+        if self._shared is not None or sc.numel() != len(self._verts_list):
+            raise ValueError("scale_verts_: one scale per mesh (a shared batch takes a single scale)")
+        self._verts_list = [v * sc[i] for i, v in enumerate(self._verts_list)]
+        return self
+
+    def scale_verts(self, scale):
+        return self.clone().scale_verts_(scale)
 
     def update_padded(self, new_verts_padded):
         vl = [new_verts_padded[i, : v.shape[0]] for i, v in enumerate(self.verts_list())]

@@ -40,6 +40,14 @@ def texture_args(meshes: Meshes, need_color: bool):
     raise NotImplementedError(f"textures of type {type(tex).__name__}")
 
 
+def textures_need_modular(meshes: Meshes) -> bool:
+    """A TexturesUV map / uv set that requires grad cannot go through the fused K=1 kernels
+    (they read a cached detached RGBA copy): route the render through the modular path instead of
+    silently dropping the gradient (never silently differ)."""
+    tex = meshes.textures
+    return tex is not None and getattr(tex, "requires_grad", lambda: False)()
+
+
 def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfig, cam_center=None,
                       pose_cv=False):
     """Render every view of `meshes` (shared mesh or per-view meshes) with the fused kernels.
@@ -159,7 +167,9 @@ class ColorRender(DifferentiableRenderer):
 
     def render(self, meshes, R, tvec):
         self._check_meshes(meshes)
-        if self._faces_per_pixel != 1:
+        if self._faces_per_pixel != 1 or textures_need_modular(meshes):
+            if self._faces_per_pixel == 1 and not hasattr(self, "_phong_renderer"):
+                _, self._phong_renderer = _soft_renderers(self, 1, self._light_location)
             Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
             return self._phong_renderer(meshes, R=Rs, T=ts)[..., :3]
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location,
@@ -177,6 +187,13 @@ class DepthColorRender(DifferentiableRenderer):
 
     def render(self, meshes, R, tvec):
         self._check_meshes(meshes)
+        if textures_need_modular(meshes):
+            if not hasattr(self, "_soft"):
+                self._soft = (_soft_renderers(self, 1, None), _soft_renderers(self, 1, self._light_location))
+            (rast, sil_r), (_, phong_r) = self._soft
+            Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
+            depth = torch.relu(rast(meshes, R=Rs, T=ts).zbuf[..., 0])
+            return depth, sil_r(meshes, R=Rs, T=ts)[..., 3], phong_r(meshes, R=Rs, T=ts)[..., :3]
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location)
         out = render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)
         return out["depth"], out["sil"], out["rgb"]

@@ -131,17 +131,24 @@ def main():
     ap.add_argument("--cpu-views", type=int, default=2)
     ap.add_argument("--eager", action="store_true",
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
+    ap.add_argument("--mode", choices=("render", "fragments"), default="render",
+                    help="render: the headline fwd+bwd step; fragments: the rasterizer alone "
+                         "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
+    if args.mode == "fragments":
+        return bench_fragments(args, dev, world, rank)
     from torch_renderer_amd import _lib
     from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset, load_asset_arrays
@@ -295,5 +302,125 @@ def main():
         dist.destroy_process_group()
 
 
+FRAG_KERNELS = ("k_project_faces", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster", "k_shade<0>")
+
+
+def bench_fragments(args, dev, world, rank):
+    """The fragment pass alone: MeshRasterizer(meshes_world, R, T) -> Fragments(pix_to_face int64, zbuf,
+    bary_coords, dists), K=1 (camera_pose_optimizer.py:244-246, batch_rendering_test.py:274): projection
+    (mr_project_faces) + binning + raster + fragment writes (mr_rasterize_meshes). API-minimum bytes per
+    frame: 28 B/px of fragments + 36 B/face of face_verts."""
+    from torch_renderer_amd import _lib
+    from torch_renderer_amd import distributed as D
+    from torch_renderer_amd.assets import load_asset
+    from torch_renderer_amd.kernels import ProjectFaces, RasterizeFaceVerts, mesh_topology
+    from torch_renderer_amd.cameras import PerspectiveCameras, view_batch
+    from torch_renderer_amd.transforms import opencv_to_pytorch3d
+
+    H = W = args.size
+    meshes = load_asset(args.mesh, device=dev, textures=False)
+    verts = meshes.shared_verts()
+    faces = meshes.shared_faces()
+    Fn = faces.shape[0]
+    nv = args.views
+    R_all, t_all, K = canonical_views(verts.cpu(), nv * world, H, W)
+    R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
+    Rp, Tp = opencv_to_pytorch3d(R_cv.to(dev), t_cv.to(dev))
+    cams = PerspectiveCameras(focal_length=((float(K[0, 0]), float(K[1, 1])),),
+                              principal_point=((float(K[0, 2]), float(K[1, 2])),), in_ndc=False,
+                              image_size=torch.tensor([[H, W]]), device=dev)
+    Rb, Tb, intr = view_batch(cams, (H, W), Rp, Tp, n_views=nv)
+    intr = intr.contiguous()
+    mesh_topology(faces, verts.shape[0])
+    first = (torch.arange(nv, device=dev) * Fn).contiguous()
+    count = torch.full((nv,), Fn, device=dev, dtype=torch.int64)
+
+    def step():
+        fv = ProjectFaces.apply(verts, Rb, Tb, faces, intr)
+        return RasterizeFaceVerts.apply(fv, first, count, H, W, 1, 0.0, True, False, False, None)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            out = step()
+        del out
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            out = step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        covered = int((out[0] >= 0).sum())
+        del out
+        if world > 1:
+            e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            elapsed = e.item()
+        _lib.timing_enable(True)
+        for _ in range(min(args.steps, 20)):
+            out = step()
+        torch.cuda.synchronize()
+        kt = _lib.timing_read()
+        _lib.timing_enable(False)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    frames = nv * world * args.steps
+    value = frames / elapsed
+    per_frame = 28 * H * W + 36 * Fn
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    us = sum(kt[k][1] / kt[k][0] * 1e3 for k in FRAG_KERNELS if k in kt)
+    ach = per_frame * nv / (us * 1e-6) / 1e9
+    dom = max(kt.items(), key=lambda kv: kv[1][1])
+    line = {
+        "metric": "frames/sec fragment pass (MeshRasterizer -> Fragments, K=1), 512x512, ~6k-face mesh, batch=64",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "launch": "eager", "data": "synthetic camera poses on the reference mesh",
+        "config": {"workload": f"{args.mesh} (F={Fn}), {H}x{W}, {nv} views/GPU, projection + rasterization to "
+                               "PyTorch3D Fragments (pix_to_face int64, zbuf, bary_coords, dists)",
+                   "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "parallelism": f"view-sharded x{world}"},
+        "fragment_roofline": {"bound": "hbm", "bytes_per_frame": per_frame, "kernels": [k for k in FRAG_KERNELS if k in kt],
+                              "us_per_step": round(us, 2), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                              "step_frac": round(value * per_frame / 1e9 / HBM_PEAK_GBS, 4),
+                              "dominant_kernel": dom[0]},
+        "work": {"covered": covered}, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N fresh rank processes (one per GPU) with the
+    torch.distributed env a launcher would set, before this parent touches the GPU (it never
+    initialises HIP, so no process exec follows GPU init). Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    return rc
+
+
 if __name__ == "__main__":
+    _a = argparse.ArgumentParser(add_help=False)
+    _a.add_argument("--gpus", type=int, default=1)
+    _known, _ = _a.parse_known_args()
+    if _known.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(_known.gpus))
     main()

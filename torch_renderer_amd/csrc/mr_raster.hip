@@ -1080,6 +1080,22 @@ __global__ void __launch_bounds__(256) k_shade_rec_zero(ShadeParams S, int64_t F
   }
 }
 
+// XCD-aware slot ranges: workgroups are dispatched round-robin over the 8 XCDs (blockIdx % 8
+// names the XCD), so each XCD takes a contiguous eighth of the (view-major, tile-ordered) slots
+// and its waves stride inside it. Horizontally / vertically adjacent tiles then run on the same
+// XCD at about the same time and share that XCD's L2 lines (the 128-B lines of the per-pixel
+// upstream gradients and outputs span two 8-pixel tile rows; a face record serves neighbouring
+// tiles). Returns the wave's first slot, its stride and the range end.
+MR_DEV void xcd_slot_range(int nslots, int wave, int& s0, int& step, int& end) {
+  const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int per = (nslots + parts - 1) / parts;
+  const int x = blockIdx.x % parts;
+  const int b = x * per;
+  end = b + per < nslots ? b + per : nslots;
+  s0 = b + (int)(blockIdx.x / parts) * 4 + wave;
+  step = (int)(gridDim.x / parts) * 4;
+}
+
 // Covered pixels: waves stride over the non-empty tiles' slots, one tile pixel per lane:
 // recompute the winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade
 // (M = 1) over the background k_tile_raster wrote.
@@ -1089,17 +1105,18 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
   const int64_t HW = (int64_t)P.H * P.W;
+  int s0, G, send;
+  xcd_slot_range(nslots, wave, s0, G, send);
   // slot s + G's tile and winners are loaded while slot s is processed
-  const int G = gridDim.x * 4;
   int gt_n = 0, f_n = -1;
-  if (blockIdx.x * 4 + wave < nslots) {
-    gt_n = P.stile[blockIdx.x * 4 + wave];
-    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
+  if (s0 < send) {
+    gt_n = P.stile[s0];
+    f_n = P.sface[(int64_t)s0 * 64 + lane];
   }
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
+  for (int s = s0; s < send; s += G) {
     const int gt = gt_n;
     const int f = f_n;
-    if (s + G < nslots) {
+    if (s + G < send) {
       gt_n = P.stile[s + G];
       f_n = P.sface[(int64_t)(s + G) * 64 + lane];
     }
@@ -1285,7 +1302,8 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
   const int64_t slots_cap = N * (int64_t)g.T;
-  const int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
+  int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
+  sg = (sg + 7) / 8 * 8;  // XCD-partitioned slot ranges
   MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sg, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_shade");
   return MR_OK;
@@ -1389,29 +1407,55 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   acc_flush(L, P.gfv);
 }
 
-// Sum ACC-float rows over runs of equal `key` in lane order (segmented shuffle scan; the
+// DPP lane moves (GFX9 / CDNA): no LDS round trip (a __shfl is a ds_bpermute_b32 with LDS
+// latency; the backward issued ~180 of them per tile in dependent chains).
+MR_DEV int dpp_wave_shr1(int v, int old) { return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false); }  // wave_shr:1
+MR_DEV int dpp_wave_shl1(int v, int old) { return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xf, 0xf, false); }  // wave_shl:1
+template <int CTRL, int ROW_MASK>
+MR_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+// Segmented inclusive sum over lanes: d = distance from the lane to the first lane of its run.
+// row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry a run across rows
+// (the structure of wave_incl_sum, each step gated on the run reaching that far back).
+MR_DEV float seg_incl_sum(float x, int d, int lane) {
+  const int r = lane & 15;
+  float y;
+  y = dppf<0x111, 0xf>(x); x += (d >= 1) ? y : 0.0f;
+  y = dppf<0x112, 0xf>(x); x += (d >= 2) ? y : 0.0f;
+  y = dppf<0x114, 0xf>(x); x += (d >= 4) ? y : 0.0f;
+  y = dppf<0x118, 0xf>(x); x += (d >= 8) ? y : 0.0f;
+  y = dppf<0x142, 0xa>(x); x += (d > r) ? y : 0.0f;            // rows 1, 3 <- lanes 15, 47
+  y = dppf<0x143, 0xc>(x); x += (d > lane - 32) ? y : 0.0f;    // rows 2, 3 <- lane 31
+  return x;
+}
+// Full-wave sum, result in lane 63.
+MR_DEV float wave_sum_f_dpp(float x) {
+  x += dppf<0x111, 0xf>(x);
+  x += dppf<0x112, 0xf>(x);
+  x += dppf<0x114, 0xf>(x);
+  x += dppf<0x118, 0xf>(x);
+  x += dppf<0x142, 0xa>(x);
+  x += dppf<0x143, 0xc>(x);
+  return x;
+}
+
+// Sum ACC-float rows over runs of equal `key` in lane order (segmented DPP scan; the
 // covered-pixel list is row-major, so a face's pixels along a row are consecutive lanes).
 // The run totals are staged in the wave's LDS rows and added with float atomics whose
 // lanes cover consecutive components of consecutive runs (contiguous 4*ACC-byte rows per
 // run instead of one scattered dword per lane and instruction). Lanes with key < 0 carry
-// zero rows. Uniform call (full EXEC).
+// zero rows. Uniform call (full EXEC). (Measured alternative: one LDS row per distinct face
+// filled with LDS float atomics — slower, 124 vs 102 us, the same-address LDS atomics serialise.)
 template <int ACC>
 MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float* lrow, int* lkey) {
   const int lane = threadIdx.x & 63;
-  const int prev = __shfl_up(key, 1, 64);
+  const int prev = dpp_wave_shr1(key, -2);  // lane 0: no predecessor
   const bool head = lane == 0 || key != prev;
   const int d = lane - wave_incl_max(head ? lane : 0);  // distance to the run's first lane
 #pragma unroll
-  for (int i = 0; i < ACC; ++i) {
-    float x = v[i];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const float y = __shfl_up(x, o, 64);
-      if (d >= o) x += y;
-    }
-    v[i] = x;
-  }
-  const int next = __shfl_down(key, 1, 64);
+  for (int i = 0; i < ACC; ++i) v[i] = seg_incl_sum(v[i], d, lane);
+  const int next = dpp_wave_shl1(key, -2);  // lane 63: no successor
   const bool emit = (lane == 63 || key != next) && key >= 0;
   const unsigned long long m = __ballot(emit);
   if (emit) {
@@ -1425,9 +1469,26 @@ MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float
   for (int j = lane; j < nt * ACC; j += 64) {
     const int r = j / ACC;
     const float x = lrow[j];
+#ifndef MR_EXP_NOATOMIC
     if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
+#else
+    if (x == 1234.5f) dst[0] = x;  // experiment build: keep the reduction, drop the atomics
+#endif
   }
   wave_lds_sync();
+}
+
+// The slot's 12 R/T partial sums (wave-wide DPP sums, fixed order: deterministic) written by
+// lanes 0..11 with one store instruction. Uniform call (full EXEC).
+MR_DEV void store_rt_partial(const float (&gR)[9], const float (&gT)[3], float* __restrict__ out, int lane) {
+  float o = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const float t = wave_sum_f_dpp(i < 9 ? gR[i] : gT[i - 9]);
+    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+    o = lane == i ? s : o;
+  }
+  if (lane < 12) out[lane] = o;
 }
 
 // Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
@@ -1592,12 +1653,7 @@ __global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
     }
     seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     // the slot's R/T partial sums (a slot is one view): wave reduction, no atomics
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      float v = i < 9 ? gR[i] : gT[i - 9];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == i) P.rt_part[(int64_t)s * 12 + i] = v;
-    }
+    store_rt_partial(gR, gT, P.rt_part + (int64_t)s * 12, lane);
   }
 }
 
@@ -1641,24 +1697,32 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
-  const int G = gridDim.x * 4;
+  int s, G, send;
+  xcd_slot_range(nslots, wave, s, G, send);
   // Three-deep software pipeline (the kernel runs at 2 waves/SIMD, so a wave must hide its own
   // latency): while slot s is processed, the face record and upstream gradients of slot s + G
   // and the tile id and winner of slot s + 2G are in flight.
-  int s = blockIdx.x * 4 + wave;
   int gt_c = 0, f_c = -1, gt_n = 0, f_n = -1;
-  if (s < nslots) {
+  if (s < send) {
     gt_c = P.stile[s];
     f_c = P.sface[(int64_t)s * 64 + lane];
   }
-  if (s + G < nslots) {
+  if (s + G < send) {
     gt_n = P.stile[s + G];
     f_n = P.sface[(int64_t)(s + G) * 64 + lane];
   }
   FaceRec r_c;
   float g_c[5];
   bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
-  for (; s < nslots; s += G) {
+#ifdef MR_PROF
+  unsigned long long pacc[7] = {0, 0, 0, 0, 0, 0, 0}, nit = 0;
+  unsigned long long tp0 = __builtin_amdgcn_s_memtime();
+  const unsigned long long tstart = tp0;
+#define BACC(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); pacc[i] += _t - tp0; tp0 = _t; } while (0)
+#else
+#define BACC(i) do {} while (0)
+#endif
+  for (; s < send; s += G) {
     const int gt = gt_c, f = f_c;
     const FaceRec r = r_c;
     float gin[5];
@@ -1669,12 +1733,13 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
     gt_n = 0;
     f_n = -1;
-    if (s + 2 * G < nslots) {
+    if (s + 2 * G < send) {
       gt_n = P.stile[s + 2 * G];
       f_n = P.sface[(int64_t)(s + 2 * G) * 64 + lane];
     }
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
+    BACC(0);
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (f >= 0) {
       PixGeom Gm;
@@ -1687,9 +1752,12 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
         ShadeOut so;
         ShadeCache C;
+        BACC(1);
         shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C);
+        BACC(2);
         ShadeGrad SG;
         shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
+        BACC(3);
         o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
         o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
         o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
@@ -1729,6 +1797,7 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       const float b[3] = {a2.w, a3.x, a3.y};
       const float gt3[3] = {a3.z, a3.w, a4.x};
       float gfv[3][3];
+      BACC(4);
       raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
       key = face;
 #pragma unroll
@@ -1743,14 +1812,26 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
         }
       }
     }
+    BACC(5);
     seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
-#pragma unroll
-    for (int i = 0; i < 12; ++i) {
-      float v = i < 9 ? gR[i] : gT[i - 9];
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      if (lane == i) P.rt_part[(int64_t)s * 12 + i] = v;
+    BACC(6);
+    store_rt_partial(gR, gT, P.rt_part + (int64_t)s * 12, lane);
+#ifdef MR_PROF
+    ++nit;
+#endif
+  }
+#ifdef MR_PROF
+  {
+    const int gw = 32768 + blockIdx.x * 4 + wave;  // k_tile_raster's stamps use waves < 32768
+    if (g_prof && lane == 0) {
+      unsigned long long* o = g_prof + (size_t)gw * 8;
+      for (int i = 0; i < 6; ++i) o[i] = pacc[i];
+      o[6] = nit;
+      o[7] = __builtin_amdgcn_s_memtime() - tstart;
     }
   }
+#endif
+#undef BACC
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
@@ -2222,6 +2303,10 @@ static ShadeParams make_shade(const mr_mesh_t* m, const mr_shade_params_t* sp, c
   S.znear = sp->znear;
   S.zfar = sp->zfar;
   S.sigma_sil = sp->sigma_sil;
+  S.inv_sigma_rgb = 1.0f / sp->sigma_rgb;
+  S.inv_gamma = 1.0f / sp->gamma;
+  S.inv_zrange = 1.0f / (sp->zfar - sp->znear);
+  S.inv_sigma_sil = 1.0f / sp->sigma_sil;
   return S;
 }
 
@@ -2386,7 +2471,10 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   if (!g1) g1 = resident_grid(k_bwd_shade, 256, 3);
   if (!g2) g2 = resident_grid(k_bwd_geom<18>, 256, 3);
   if (!g3) g3 = resident_grid(k_bwd_geom<27>, 256, 3);
-  auto cap = [&](int gr) { return (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr); };
+  auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
+    const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
+    return (c + 7) / 8 * 8;
+  };
   static const bool split = getenv("MR_BWD_SPLIT") != nullptr;  // two-kernel variant, for comparison
   if (split) {
     MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<cap(g1), 256, 0, st>>>(P)));

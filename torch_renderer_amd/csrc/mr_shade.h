@@ -36,6 +36,8 @@ struct ShadeParams {
   // blending
   float sigma_rgb, gamma, bg[3], znear, zfar;
   float sigma_sil;
+  // reciprocals precomputed on the host (multiplications in the per-pixel code)
+  float inv_sigma_rgb, inv_gamma, inv_zrange, inv_sigma_sil;
 };
 
 struct ViewRec {  // 16 floats, matches mr_view_t
@@ -48,21 +50,23 @@ struct ShadeOut {
 
 // ---- F.normalize(x, eps=1e-6) forward/backward ----
 MR_DEV void normalize3(const float x[3], float y[3], float& nrm, float& den) {
-  nrm = sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
+  nrm = fsqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
   den = smax(nrm, 1e-6f);
-  y[0] = x[0] / den;
-  y[1] = x[1] / den;
-  y[2] = x[2] / den;
+  const float r = frcp(den);
+  y[0] = x[0] * r;
+  y[1] = x[1] * r;
+  y[2] = x[2] * r;
 }
 MR_DEV void normalize3_bwd(const float x[3], float nrm, float den, const float g[3], float gx[3]) {
-  const float gd = -((g[0] * x[0] + g[1] * x[1]) + g[2] * x[2]) / (den * den);
-  const float gn = (nrm >= 1e-6f && nrm > 0.0f) ? gd / nrm : 0.0f;
-  gx[0] = g[0] / den + gn * x[0];
-  gx[1] = g[1] / den + gn * x[1];
-  gx[2] = g[2] / den + gn * x[2];
+  const float r = frcp(den);
+  const float gd = -((g[0] * x[0] + g[1] * x[1]) + g[2] * x[2]) * (r * r);
+  const float gn = (nrm >= 1e-6f && nrm > 0.0f) ? gd * frcp(nrm) : 0.0f;
+  gx[0] = g[0] * r + gn * x[0];
+  gx[1] = g[1] * r + gn * x[1];
+  gx[2] = g[2] * r + gn * x[2];
 }
 MR_DEV float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
-MR_DEV float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+MR_DEV float sigmoidf_(float x) { return frcp(1.0f + fexp(-x)); }
 
 // ---- texture: grid_sample(bilinear, align_corners=True, border) on flipped map ----
 struct TexTap {
@@ -207,7 +211,7 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
   // DepthRender: relu(zbuf[..., 0])
   o.depth = zb > 0.0f ? zb : 0.0f;
   // SoftSilhouetteShader / sigmoid_alpha_blend
-  C.ps = sigmoidf_((-dd) / S.sigma_sil) * m;
+  C.ps = sigmoidf_((-dd) * S.inv_sigma_sil) * m;
   o.sil = 1.0f - (1.0f - C.ps);
   // Phong colours (only meaningful for hit pixels; background weight is 0)
   for (int k = 0; k < 3; ++k) C.col[k] = 0.0f;
@@ -239,7 +243,7 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
       C.vr = dot3(C.vh, C.r);
       const float ms = C.cosd > 0.0f ? 1.0f : 0.0f;
       C.as = (C.vr > 0.0f ? C.vr : 0.0f) * ms;
-      C.spow = powf(C.as, S.shininess);
+      C.spow = fpow(C.as, S.shininess);
       for (int k = 0; k < 3; ++k) {
         C.diff[k] = S.mat_diff[k] * (S.light_diff[k] * angle);
         C.spec[k] = S.mat_spec[k] * (S.light_spec[k] * C.spow);
@@ -251,16 +255,17 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
   }
   // softmax_rgb_blend (K = 1)
   const float eps = 1e-10f;
-  C.pc = sigmoidf_((-dd) / S.sigma_rgb) * m;
+  C.pc = sigmoidf_((-dd) * S.inv_sigma_rgb) * m;
   const float alpha = 1.0f - C.pc;
-  C.zi = (S.zfar - zb) / (S.zfar - S.znear) * m;
+  C.zi = ((S.zfar - zb) * S.inv_zrange) * m;
   C.zimax = smax(C.zi, eps);
-  C.E = expf((C.zi - C.zimax) / S.gamma);
+  C.E = fexp((C.zi - C.zimax) * S.inv_gamma);
   C.w = C.pc * C.E;
-  C.ex = expf((eps - C.zimax) / S.gamma);
+  C.ex = fexp((eps - C.zimax) * S.inv_gamma);
   C.delta = smax(C.ex, eps);
   C.den = C.w + C.delta;
-  for (int k = 0; k < 3; ++k) o.rgb[k] = (C.w * C.col[k] + C.delta * S.bg[k]) / C.den;
+  const float rden = frcp(C.den);
+  for (int k = 0; k < 3; ++k) o.rgb[k] = (C.w * C.col[k] + C.delta * S.bg[k]) * rden;
   o.alpha = 1.0f - alpha;
 }
 
@@ -286,16 +291,17 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   // silhouette: sil = 1 - (1 - ps), ps = sigmoid(-sd / sigma_sil)
   {
     const float gx = gS * (C.ps * (1.0f - C.ps));
-    R.gsd += -(gx / S.sigma_sil);
+    R.gsd += -(gx * S.inv_sigma_sil);
   }
   // rgb = (w*col + delta*bg) / den
   float gw = 0.0f, gdelta = 0.0f, gcol[3];
   {
     float gden = 0.0f;
+    const float rden = frcp(C.den);
     for (int k = 0; k < 3; ++k) {
       const float num = C.w * C.col[k] + C.delta * S.bg[k];
-      const float gnum = gRGB[k] / C.den;
-      gden += -gRGB[k] * num / (C.den * C.den);
+      const float gnum = gRGB[k] * rden;
+      gden += -gRGB[k] * num * (rden * rden);
       gw += gnum * C.col[k];
       gcol[k] = gnum * C.w;
       gdelta += gnum * S.bg[k];
@@ -307,16 +313,16 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   float gzimax = 0.0f, gzi = 0.0f;
   {
     const float gu = (C.ex >= 1e-10f) ? gdelta * C.ex : 0.0f;  // clamp(min) backward
-    gzimax += -(gu / S.gamma);
+    gzimax += -(gu * S.inv_gamma);
     gp += gw * C.E;
     const float gE = gw * C.pc;
     const float gv = gE * C.E;
-    gzi += gv / S.gamma;
-    gzimax += -(gv / S.gamma);
+    gzi += gv * S.inv_gamma;
+    gzimax += -(gv * S.inv_gamma);
     gzi += (C.zi >= 1e-10f) ? gzimax : 0.0f;  // max over K=1, then clamp(min=eps)
-    R.gz += -(gzi / (S.zfar - S.znear));
+    R.gz += -(gzi * S.inv_zrange);
     const float gx = gp * (C.pc * (1.0f - C.pc));
-    R.gsd += -(gx / S.sigma_rgb);
+    R.gsd += -(gx * S.inv_sigma_rgb);
   }
   // colours = (amb + diff) * texel + spec
   float gtex[3], gP[3] = {0.f, 0.f, 0.f}, gNn[3] = {0.f, 0.f, 0.f};
@@ -327,7 +333,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
       gangle += gcol[k] * C.texel[k] * S.mat_diff[k] * S.light_diff[k];
       gspow += gcol[k] * S.mat_spec[k] * S.light_spec[k];
     }
-    const float gas = (C.as > 0.0f) ? gspow * S.shininess * powf(C.as, S.shininess - 1.0f) : 0.0f;
+    const float gas = (C.as > 0.0f) ? gspow * S.shininess * fpow(C.as, S.shininess - 1.0f) : 0.0f;
     const float ms = C.cosd > 0.0f ? 1.0f : 0.0f;
     const float gvr = (C.vr > 0.0f) ? gas * ms : 0.0f;
     float gvh[3], gr[3], glh[3], gnh[3];
@@ -391,27 +397,27 @@ MR_DEV void edge_bwd(float px, float py, float ax, float ay, float bx, float by,
 // BarycentricCoordsBackward -> dv[0..2] (x,y)
 MR_DEV void bary_bwd(float px, float py, const FaceRec& r, const float g[3], float dv[3][2]) {
   const float area = r.area;
-  const float area2 = area * area;
-  const float area_inv = 1.0f / area;
+  const float area_inv = frcp(area);
+  const float area2_inv = area_inv * area_inv;
   const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
   const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
   const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
   float de[6], da[6];
   // w0: e0 over (p, v1, v2); area over (v2, v0, v1)
   edge_bwd(px, py, r.x1, r.y1, r.x2, r.y2, g[0] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[0] * (-e0 / area2), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[0] * (-e0 * area2_inv), da);
   float v0x = da[2], v0y = da[3];
   float v1x = de[2] + da[4], v1y = de[3] + da[5];
   float v2x = de[4] + da[0], v2y = de[5] + da[1];
   // w1: e1 over (p, v2, v0)
   edge_bwd(px, py, r.x2, r.y2, r.x0, r.y0, g[1] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[1] * (-e1 / area2), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[1] * (-e1 * area2_inv), da);
   const float w1v0x = de[4] + da[2], w1v0y = de[5] + da[3];
   const float w1v1x = da[4], w1v1y = da[5];
   const float w1v2x = de[2] + da[0], w1v2y = de[3] + da[1];
   // w2: e2 over (p, v0, v1)
   edge_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g[2] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[2] * (-e2 / area2), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[2] * (-e2 * area2_inv), da);
   const float w2v0x = de[2] + da[2], w2v0y = de[3] + da[3];
   const float w2v1x = de[4] + da[4], w2v1y = de[5] + da[5];
   const float w2v2x = da[0], w2v2y = da[1];
@@ -427,9 +433,10 @@ MR_DEV void persp_bwd(float w0, float w1, float w2, float z0, float z1, float z2
                       float gzv[3]) {
   const float t0 = w0 * z1 * z2, t1 = w1 * z0 * z2, t2 = w2 * z0 * z1;
   const float d = smax(t0 + t1 + t2, (float)MR_KEPS_D);
+  const float rd = frcp(d);
   const float gdt = -t0 * go[0] - t1 * go[1] - t2 * go[2];
-  const float gd = gdt / (d * d);
-  const float g0 = gd + go[0] / d, g1 = gd + go[1] / d, g2 = gd + go[2] / d;
+  const float gd = gdt * (rd * rd);
+  const float g0 = gd + go[0] * rd, g1 = gd + go[1] * rd, g2 = gd + go[2] * rd;
   gb[0] = g0 * z1 * z2;
   gb[1] = g1 * z0 * z2;
   gb[2] = g2 * z0 * z1;
@@ -441,11 +448,12 @@ MR_DEV void persp_bwd(float w0, float w1, float w2, float z0, float z1, float z2
 MR_DEV void clip_bwd(float c0, float c1, float c2, const float go[3], float gb[3]) {
   const float w0 = smax(c0, 0.0f), w1 = smax(c1, 0.0f), w2 = smax(c2, 0.0f);
   const float s = smax(w0 + w1 + w2, 1e-5f);
+  const float rs = frcp(s);
   const float num = w0 * go[0] + w1 * go[1] + w2 * go[2];
-  const float gs = -num / (s * s);
-  gb[0] = c0 > 0.0f ? go[0] / s + gs : 0.0f;
-  gb[1] = c1 > 0.0f ? go[1] / s + gs : 0.0f;
-  gb[2] = c2 > 0.0f ? go[2] / s + gs : 0.0f;
+  const float gs = -num * (rs * rs);
+  gb[0] = c0 > 0.0f ? go[0] * rs + gs : 0.0f;
+  gb[1] = c1 > 0.0f ? go[1] * rs + gs : 0.0f;
+  gb[2] = c2 > 0.0f ? go[2] * rs + gs : 0.0f;
 }
 
 MR_DEV void pt_line_bwd(float px, float py, float ax, float ay, float bx, float by, float g, float& gax,
@@ -453,7 +461,7 @@ MR_DEV void pt_line_bwd(float px, float py, float ax, float ay, float bx, float 
   const float dx = bx - ax, dy = by - ay;
   const float t_bot = dx * dx + dy * dy;
   const float t_top = dx * (px - ax) + dy * (py - ay);
-  const float t = t_top / t_bot;
+  const float t = fdiv(t_top, t_bot);
   const float tt = smin(smax(t, 0.0f), 1.0f);
   const float qx = (1.0f - tt) * ax + tt * bx, qy = (1.0f - tt) * ay + tt * by;
   const float ex = qx - px, ey = qy - py;
@@ -464,10 +472,26 @@ MR_DEV void pt_line_bwd(float px, float py, float ax, float ay, float bx, float 
   gby = s1 * ey;
 }
 
+// PointLineDistanceForward with a fast reciprocal: the backward only uses it to pick the
+// closest edge (exact ties resolve as in the forward except within a few ulp).
+MR_DEV float pt_line_dist_fast(float px, float py, float ax, float ay, float bx, float by) {
+  const float dx = bx - ax, dy = by - ay;
+  const float l2 = dx * dx + dy * dy;
+  if ((double)l2 <= MR_KEPS_D) {
+    const float ex = px - bx, ey = py - by;
+    return ex * ex + ey * ey;
+  }
+  const float t = (dx * (px - ax) + dy * (py - ay)) * frcp(l2);
+  const float tt = smin(smax(t, 0.0f), 1.0f);
+  const float qx = ax + tt * dx, qy = ay + tt * dy;
+  const float ex = px - qx, ey = py - qy;
+  return ex * ex + ey * ey;
+}
+
 MR_DEV void pt_tri_bwd(float px, float py, const FaceRec& r, float g, float gv[3][2]) {
-  const float e01 = pt_line_dist(px, py, r.x0, r.y0, r.x1, r.y1);
-  const float e02 = pt_line_dist(px, py, r.x0, r.y0, r.x2, r.y2);
-  const float e12 = pt_line_dist(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e01 = pt_line_dist_fast(px, py, r.x0, r.y0, r.x1, r.y1);
+  const float e02 = pt_line_dist_fast(px, py, r.x0, r.y0, r.x2, r.y2);
+  const float e12 = pt_line_dist_fast(px, py, r.x1, r.y1, r.x2, r.y2);
   for (int c = 0; c < 3; ++c) gv[c][0] = gv[c][1] = 0.0f;
   if (e01 <= e02 && e01 <= e12)
     pt_line_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g, gv[0][0], gv[0][1], gv[1][0], gv[1][1]);
@@ -484,12 +508,21 @@ MR_DEV void raster_bwd_pixel(const FaceRec& r, float px, float py, bool persp, b
   const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
   const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
   const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
-  const float w0 = e0 / r.area, w1 = e1 / r.area, w2 = e2 / r.area;
+  // forward quantities recomputed for the derivative (fast reciprocals: the signs, hence
+  // `inside`, are exact; the values feed gradients only)
+  const float ra = frcp(r.area);
+  const float w0 = e0 * ra, w1 = e1 * ra, w2 = e2 * ra;
   float c0, c1, c2, b0, b1, b2;
-  if (persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
-  else { c0 = w0; c1 = w1; c2 = w2; }
-  if (clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
-  else { b0 = c0; b1 = c1; b2 = c2; }
+  if (persp) {
+    const float t0 = w0 * r.z1 * r.z2, t1 = w1 * r.z0 * r.z2, t2 = w2 * r.z0 * r.z1;
+    const float rd = frcp(smax(t0 + t1 + t2, (float)MR_KEPS_D));
+    c0 = t0 * rd; c1 = t1 * rd; c2 = t2 * rd;
+  } else { c0 = w0; c1 = w1; c2 = w2; }
+  if (clipb) {
+    const float u0 = smax(c0, 0.0f), u1 = smax(c1, 0.0f), u2 = smax(c2, 0.0f);
+    const float rs = frcp(smax(u0 + u1 + u2, 1e-5f));
+    b0 = u0 * rs; b1 = u1 * rs; b2 = u2 * rs;
+  } else { b0 = c0; b1 = c1; b2 = c2; }
   const bool inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
   const float sign = inside ? -1.0f : 1.0f;
   float dd[3][2];
@@ -528,11 +561,13 @@ MR_DEV void project_point(const ViewRec& V, const float X[3], float& vx, float& 
 // g_ndc (x, y, z=view z) at world point X -> g_view; then g_X = R g_view,
 // g_R += X (x) g_view, g_T += g_view.
 MR_DEV void project_bwd(const ViewRec& V, const float X[3], const float gn[3], float gX[3], float gR[9], float gT[3]) {
-  float vx, vy, vz, nx, ny;
-  project_point(V, X, vx, vy, vz, nx, ny);
-  const float qx = vx / vz, qy = vy / vz;
+  const float vx = ((X[0] * V.R[0] + X[1] * V.R[3]) + X[2] * V.R[6]) + V.T[0];
+  const float vy = ((X[0] * V.R[1] + X[1] * V.R[4]) + X[2] * V.R[7]) + V.T[1];
+  const float vz = ((X[0] * V.R[2] + X[1] * V.R[5]) + X[2] * V.R[8]) + V.T[2];
+  const float rz = frcp(vz);
+  const float qx = vx * rz, qy = vy * rz;
   const float gqx = gn[0] * V.ax, gqy = gn[1] * V.ay;
-  const float gv[3] = {gqx / vz, gqy / vz, gn[2] - gqx * qx / vz - gqy * qy / vz};
+  const float gv[3] = {gqx * rz, gqy * rz, gn[2] - gqx * qx * rz - gqy * qy * rz};
   for (int a = 0; a < 3; ++a) {
     gX[a] = (V.R[3 * a] * gv[0] + V.R[3 * a + 1] * gv[1]) + V.R[3 * a + 2] * gv[2];
     for (int bb = 0; bb < 3; ++bb) gR[3 * a + bb] += X[a] * gv[bb];

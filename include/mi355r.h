@@ -43,12 +43,20 @@ typedef struct mr_view {
 /* RasterizationSettings (upstream rasterizer.py) — blur/K/clip/cull as there. */
 typedef struct mr_raster_settings {
   int32_t H, W;
-  int32_t faces_per_pixel;   /* only 1 is implemented on the GPU path */
+  int32_t faces_per_pixel;   /* 1..128 on mr_rasterize_meshes; 1 on the fused mr_render_* path */
   float blur_radius;
   int32_t perspective_correct;
   int32_t clip_barycentric_coords;
   int32_t cull_backfaces;
   int32_t max_faces_per_bin; /* <= 0: library default; overflow is handled exactly */
+  /* Near-plane clipping (upstream MeshRasterizer: z_clip_value = znear / 2 for FoVPerspectiveCameras,
+   * then mesh/clip.py clip_faces -> rasterize -> convert_clipped_rasterization_to_original_faces).
+   * clip_z != 0: faces crossing view z = z_clip_value are split (one or two sub-triangles, the two
+   * halves of a clipped quadrilateral being each other's clipped_faces_neighbor_idx); outputs refer
+   * to the original faces (pix_to_face, barycentrics converted back); backward chains through the
+   * split. Done inside the binning kernels: no host round trip, nothing to do when nothing crosses. */
+  int32_t clip_z;
+  float z_clip_value;
 } mr_raster_settings_t;
 
 /* Shading / blending parameters (SoftPhongShader, PointLights, Materials,
@@ -86,6 +94,9 @@ typedef struct mr_mesh {
 
 const char* mr_last_error(void);
 int32_t mr_version(void);
+/* sizeof of the ABI structs as compiled into the library (binding self-check):
+ * 0 mr_view_t, 1 mr_raster_settings_t, 2 mr_shade_params_t, 3 mr_mesh_t; -1 otherwise. */
+int32_t mr_struct_size(int32_t which);
 
 /* ---------------- PyTorch3D _C.rasterize_meshes boundary ---------------- */
 size_t mr_rasterize_meshes_workspace(int64_t num_meshes, int64_t total_faces, int32_t H, int32_t W,

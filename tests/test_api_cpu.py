@@ -1,5 +1,5 @@
 """Host-side behaviour of the PyTorch3D-style API and the drop-in classes that needs no GPU:
-settings, error behaviour of unsupported settings, near-plane detection, and the loud failure
+settings, error behaviour of unsupported settings, and the loud failure
 on CPU tensors (the MI355X path has no CPU fallback)."""
 import pytest
 import torch
@@ -8,7 +8,7 @@ from tests.helpers import mesh_arrays
 from torch_renderer_amd import Meshes, TexturesVertex
 from torch_renderer_amd.cameras import FoVPerspectiveCameras, PerspectiveCameras
 from torch_renderer_amd.mesh_renderer import (MeshRasterizer, MeshRenderer, RasterizationSettings, SoftPhongShader,
-                                              _check_no_clipping, _z_clip_value)
+                                              _check_cull_to_frustum, _z_clip_value)
 from torch_renderer_amd.torch_renderer import ColorRender, DepthRender
 
 
@@ -21,14 +21,10 @@ def test_settings_and_zclip_value():
     assert _z_clip_value(PerspectiveCameras(), RasterizationSettings(z_clip_value=0.2)) == 0.2
 
 
-def test_near_plane_crossing_raises():
-    fv = torch.ones(4, 3, 3)
-    _check_no_clipping(fv, 0.5, False)          # all in front: clip_faces is the identity
-    fv[2, 1, 2] = 0.3
+def test_cull_to_frustum_raises():
+    _check_cull_to_frustum(False)
     with pytest.raises(NotImplementedError):
-        _check_no_clipping(fv, 0.5, False)
-    with pytest.raises(NotImplementedError):
-        _check_no_clipping(torch.ones(1, 3, 3), None, True)
+        _check_cull_to_frustum(True)
 
 
 def test_unsupported_settings_raise():

@@ -35,7 +35,7 @@ def test_all_header_symbols_exported(lib):
 
 
 def test_version_and_workspace_queries(lib):
-    assert lib.mr_version() == 1
+    assert lib.mr_version() == 2  # 2: mr_raster_settings_t gained clip_z / z_clip_value
     a = lib.mr_render_workspace(64, 5856, 512, 512, 0)
     b = lib.mr_render_workspace(8, 5856, 512, 512, 0)
     assert a > b > 0
@@ -62,9 +62,13 @@ def test_invalid_arguments_fail_loudly_without_touching_the_gpu(lib):
 
 
 def test_struct_layouts_match_header():
-    assert ctypes.sizeof(_lib.MrView) == 64
-    assert ctypes.sizeof(_lib.MrRasterSettings) == 32
-    assert ctypes.sizeof(_lib.MrShadeParams) == 4 * (1 + 3 * 7 + 1 + 2 + 3 + 2 + 1 + 2)
+    """The ctypes mirrors have the sizes the library was compiled with (mr_struct_size)."""
+    lib = _lib.load()
+    assert ctypes.sizeof(_lib.MrView) == 64 == lib.mr_struct_size(0)
+    assert ctypes.sizeof(_lib.MrRasterSettings) == 40 == lib.mr_struct_size(1)
+    assert ctypes.sizeof(_lib.MrShadeParams) == lib.mr_struct_size(2) == 4 * (1 + 3 * 7 + 1 + 2 + 3 + 2 + 1 + 2)
+    assert ctypes.sizeof(_lib.MrMesh) == lib.mr_struct_size(3)
+    assert lib.mr_struct_size(9) == -1
 
 
 def test_missing_library_raises(tmp_path):

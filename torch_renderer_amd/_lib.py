@@ -34,7 +34,7 @@ class MrRasterSettings(ctypes.Structure):
     _fields_ = [("H", ctypes.c_int32), ("W", ctypes.c_int32), ("faces_per_pixel", ctypes.c_int32),
                 ("blur_radius", ctypes.c_float), ("perspective_correct", ctypes.c_int32),
                 ("clip_barycentric_coords", ctypes.c_int32), ("cull_backfaces", ctypes.c_int32),
-                ("max_faces_per_bin", ctypes.c_int32)]
+                ("max_faces_per_bin", ctypes.c_int32), ("clip_z", ctypes.c_int32), ("z_clip_value", ctypes.c_float)]
 
 
 F3 = ctypes.c_float * 3
@@ -65,6 +65,7 @@ _SZ = ctypes.c_size_t
 _SIGS = [
     ("mr_last_error", ctypes.c_char_p, []),
     ("mr_version", _I32, []),
+    ("mr_struct_size", _I32, [_I32]),
     ("mr_rasterize_meshes_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
     ("mr_rasterize_meshes", _I32, [_VP, _VP, _VP, _I64, _I64, ctypes.POINTER(MrRasterSettings), _VP, _VP, _VP,
                                    _VP, _VP, _SZ, _VP]),

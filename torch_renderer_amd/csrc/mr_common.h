@@ -55,7 +55,11 @@ struct __attribute__((aligned(16))) FaceRec {
   uint32_t flags;                            // FR_VALID | FR_FAST
   uint32_t face;                             // mesh face index (into faces array)
 };
-enum : uint32_t { FR_VALID = 1u, FR_FAST = 2u };
+enum : uint32_t { FR_VALID = 1u, FR_FAST = 2u, FR_CLIP = 4u, FR_PAIR = 8u };
+// FR_CLIP: the record is a sub-triangle of a face clipped at the near plane (its ClipRec holds
+// the barycentric conversion to the original face). FR_PAIR: one of the two triangles a face
+// with one corner behind the plane is split into; record id rid (< NF) is the first, NF + rid the
+// second (NF = number of face instances), each the other's clipped_faces_neighbor_idx.
 
 // BarycentricPerspectiveCorrectionForward
 MR_DEV void persp_fwd(float w0, float w1, float w2, float z0, float z1, float z2, float& o0, float& o1,
@@ -154,4 +158,150 @@ MR_DEV bool rec_finite(const FaceRec& r) {
 // Lexicographic (z, face) order == std::sort over (pz, f, ...) tuples.
 MR_DEV bool frag_less(float za, int64_t fa, float zb, int64_t fb) {
   return za < zb || (!(zb < za) && fa < fb);
+}
+
+// ---------------------------------------------------------------------------
+// Near-plane clipping (upstream mesh/clip.py clip_faces, restated in oracle.py clip_faces_ref
+// with the same operation order): corners (x_ndc, y_ndc, z_view); c = z_clip_value.
+//   nb = #corners with z < c: 0 unchanged, 3 culled;
+//   nb = 2 (front corner i): one triangle, slot i = p_i, slot j = p_ij, slot k = p_ik;
+//   nb = 1 (behind corner i): t1 = (p_ij, p_j, p_k), t2 = (p_ik, p_ij, p_k) in slots (i, j, k);
+// j = i+1, k = i+2 (mod 3); p_ab = the point of edge a->b at z = c, w_ab = (c - z_a) / (z_b - z_a):
+// perspective: xy = (xy_a z_a + w (xy_b z_b - xy_a z_a)) / c, else xy_a + w (xy_b - xy_a); z = c.
+// ---------------------------------------------------------------------------
+struct __attribute__((aligned(16))) ClipRec {
+  float conv[9];  // row s = original-face barycentrics of the sub-triangle's slot-s vertex
+  float wj, wk;   // interpolation weights of p_ij, p_ik
+  uint32_t info;  // nb (bits 0-1) | corner i << 2 | second triangle of a pair << 4
+};
+
+MR_DEV void clip_point(const float a[3], const float b[3], float w, float c, bool persp, float q[3]) {
+  if (persp) {
+    const float axw = a[0] * a[2], ayw = a[1] * a[2];
+    const float bxw = b[0] * b[2], byw = b[1] * b[2];
+    q[0] = (axw + w * (bxw - axw)) / c;
+    q[1] = (ayw + w * (byw - ayw)) / c;
+  } else {
+    q[0] = a[0] + w * (b[0] - a[0]);
+    q[1] = a[1] + w * (b[1] - a[1]);
+  }
+  q[2] = c;
+}
+
+// Number of corners behind the plane and the odd corner i (the front one for nb = 2, the behind
+// one for nb = 1; argmax order as the oracle: the first such corner).
+MR_DEV int clip_class(const float v[3][3], float c, int& i) {
+  const bool b0 = v[0][2] < c, b1 = v[1][2] < c, b2 = v[2][2] < c;
+  const int nb = (int)b0 + (int)b1 + (int)b2;
+  if (nb == 2) i = !b0 ? 0 : !b1 ? 1 : 2;
+  else i = b0 ? 0 : b1 ? 1 : 2;
+  return nb;
+}
+
+// Sub-triangle `sub` (0 or 1) of a clipped face: corners out[3][3] and its ClipRec.
+MR_DEV void clip_sub(const float v[3][3], int nb, int i, int sub, float c, bool persp, float out[3][3],
+                     ClipRec& cr) {
+  const int j = i == 2 ? 0 : i + 1, k = j == 2 ? 0 : j + 1;
+  const float wj = (c - v[i][2]) / (v[j][2] - v[i][2]);
+  const float wk = (c - v[i][2]) / (v[k][2] - v[i][2]);
+  float pij[3], pik[3];
+  clip_point(v[i], v[j], wj, c, persp, pij);
+  clip_point(v[i], v[k], wk, c, persp, pik);
+  for (int q = 0; q < 9; ++q) cr.conv[q] = 0.0f;
+  cr.wj = wj;
+  cr.wk = wk;
+  cr.info = (uint32_t)nb | ((uint32_t)i << 2) | ((uint32_t)sub << 4);
+  const float* s_i;
+  const float* s_j;
+  const float* s_k;
+  if (nb == 2) {  // (p_i, p_ij, p_ik)
+    s_i = v[i]; s_j = pij; s_k = pik;
+    cr.conv[3 * i + i] = 1.0f;
+    cr.conv[3 * j + i] = 1.0f - wj; cr.conv[3 * j + j] = wj;
+    cr.conv[3 * k + i] = 1.0f - wk; cr.conv[3 * k + k] = wk;
+  } else if (sub == 0) {  // t1 = (p_ij, p_j, p_k)
+    s_i = pij; s_j = v[j]; s_k = v[k];
+    cr.conv[3 * i + i] = 1.0f - wj; cr.conv[3 * i + j] = wj;
+    cr.conv[3 * j + j] = 1.0f;
+    cr.conv[3 * k + k] = 1.0f;
+  } else {  // t2 = (p_ik, p_ij, p_k)
+    s_i = pik; s_j = pij; s_k = v[k];
+    cr.conv[3 * i + i] = 1.0f - wk; cr.conv[3 * i + k] = wk;
+    cr.conv[3 * j + i] = 1.0f - wj; cr.conv[3 * j + j] = wj;
+    cr.conv[3 * k + k] = 1.0f;
+  }
+  for (int q = 0; q < 3; ++q) {
+    out[i][q] = s_i[q];
+    out[j][q] = s_j[q];
+    out[k][q] = s_k[q];
+  }
+}
+
+// Original-face barycentrics of a sub-triangle fragment: sum_s b_sub[s] * conv[s] ((s0 + s1) + s2).
+MR_DEV void clip_unconvert(const ClipRec& cr, float b0, float b1, float b2, float& o0, float& o1, float& o2) {
+  o0 = (b0 * cr.conv[0] + b1 * cr.conv[3]) + b2 * cr.conv[6];
+  o1 = (b0 * cr.conv[1] + b1 * cr.conv[4]) + b2 * cr.conv[7];
+  o2 = (b0 * cr.conv[2] + b1 * cr.conv[5]) + b2 * cr.conv[8];
+}
+
+// Chain rule of the clip for one fragment of a sub-triangle.
+//  v: the original corners; gb_orig: gradient w.r.t. the original barycentrics; b_sub: the
+//  sub-triangle's barycentrics (rasterizer output); gfv_sub: gradient w.r.t. the sub-triangle's
+//  corners as returned by raster_bwd_pixel (given gb_sub from clip_gb_sub). Accumulates the
+//  gradient w.r.t. the original corners into gfv (the sub-vertex z = c is a constant).
+MR_DEV void clip_gb_sub(const ClipRec& cr, const float g[3], float gs[3]) {
+  for (int s = 0; s < 3; ++s) gs[s] = (cr.conv[3 * s] * g[0] + cr.conv[3 * s + 1] * g[1]) + cr.conv[3 * s + 2] * g[2];
+}
+
+MR_DEV void clip_point_bwd(const float a[3], const float b[3], float w, float c, bool persp, const float gq[3],
+                           float ga[3], float gbv[3], float& gw) {
+  if (persp) {
+    const float rc = 1.0f / c;
+    ga[0] += gq[0] * a[2] * (1.0f - w) * rc;
+    ga[1] += gq[1] * a[2] * (1.0f - w) * rc;
+    ga[2] += (gq[0] * a[0] + gq[1] * a[1]) * (1.0f - w) * rc;
+    gbv[0] += gq[0] * w * b[2] * rc;
+    gbv[1] += gq[1] * w * b[2] * rc;
+    gbv[2] += (gq[0] * b[0] + gq[1] * b[1]) * w * rc;
+    gw += (gq[0] * (b[0] * b[2] - a[0] * a[2]) + gq[1] * (b[1] * b[2] - a[1] * a[2])) * rc;
+  } else {
+    ga[0] += gq[0] * (1.0f - w);
+    ga[1] += gq[1] * (1.0f - w);
+    gbv[0] += gq[0] * w;
+    gbv[1] += gq[1] * w;
+    gw += gq[0] * (b[0] - a[0]) + gq[1] * (b[1] - a[1]);
+  }
+}
+
+MR_DEV void clip_bwd_chain(const ClipRec& cr, const float v[3][3], float c, bool persp, const float b_sub[3],
+                           const float g_orig[3], const float gfv_sub[3][3], float gfv[3][3]) {
+  const int nb = (int)(cr.info & 3u), i = (int)((cr.info >> 2) & 3u), sub = (int)((cr.info >> 4) & 1u);
+  const int j = i == 2 ? 0 : i + 1, k = j == 2 ? 0 : j + 1;
+  float gwj = 0.0f, gwk = 0.0f;
+  // conversion entries (1 - w, w): dL/dconv[s][o] = b_sub[s] * g_orig[o]
+  if (nb == 2) {
+    gwj += b_sub[j] * (g_orig[j] - g_orig[i]);
+    gwk += b_sub[k] * (g_orig[k] - g_orig[i]);
+    for (int q = 0; q < 3; ++q) gfv[i][q] += gfv_sub[i][q];
+    clip_point_bwd(v[i], v[j], cr.wj, c, persp, gfv_sub[j], gfv[i], gfv[j], gwj);
+    clip_point_bwd(v[i], v[k], cr.wk, c, persp, gfv_sub[k], gfv[i], gfv[k], gwk);
+  } else if (sub == 0) {
+    gwj += b_sub[i] * (g_orig[j] - g_orig[i]);
+    clip_point_bwd(v[i], v[j], cr.wj, c, persp, gfv_sub[i], gfv[i], gfv[j], gwj);
+    for (int q = 0; q < 3; ++q) {
+      gfv[j][q] += gfv_sub[j][q];
+      gfv[k][q] += gfv_sub[k][q];
+    }
+  } else {
+    gwk += b_sub[i] * (g_orig[k] - g_orig[i]);
+    gwj += b_sub[j] * (g_orig[j] - g_orig[i]);
+    clip_point_bwd(v[i], v[k], cr.wk, c, persp, gfv_sub[i], gfv[i], gfv[k], gwk);
+    clip_point_bwd(v[i], v[j], cr.wj, c, persp, gfv_sub[j], gfv[i], gfv[j], gwj);
+    for (int q = 0; q < 3; ++q) gfv[k][q] += gfv_sub[k][q];
+  }
+  // w_ab = (c - z_a) / (z_b - z_a)
+  const float dj = v[j][2] - v[i][2], dk = v[k][2] - v[i][2];
+  gfv[i][2] += gwj * ((c - v[j][2]) / (dj * dj)) + gwk * ((c - v[k][2]) / (dk * dk));
+  gfv[j][2] += gwj * (-cr.wj / dj);
+  gfv[k][2] += gwk * (-cr.wk / dk);
 }

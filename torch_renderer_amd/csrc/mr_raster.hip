@@ -37,7 +37,7 @@
 #define MR_TS 8         // raster tile edge: one 64-lane wave per 8x8 tile (lane = pixel)
 #define MR_BT 32        // tile edge of the modular (fragments) backward
 #define MR_HT 512       // LDS hash slots in the backward
-#define MR_BIN_FPT 2     // faces per thread in the world-space binning kernels (MR_BIN_FPT env overrides)
+#define MR_BIN_FPT 2     // faces per thread in the world-space binning kernels
 #define MR_LDS_HIST 16384  // per-view tiles binned through an LDS histogram (else global atomics)
 
 static thread_local char g_err[512];
@@ -64,7 +64,7 @@ enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_
                 KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
-                                              "k_raster_bwd", "k_bwd_shade", "k_bwd_geom", "k_rt_reduce",
+                                              "k_raster_bwd", "k_bwd_shade(unused)", "k_bwd_geom(unused)", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
@@ -161,6 +161,7 @@ struct RasterWS {
   unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
   int* sface;  // (N*T*64) per slot, per tile pixel (row-major 8x8): winning face record or -1
   ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
+  ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
   size_t bytes;
 };
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
@@ -170,8 +171,10 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   size_t off = 0;
   char* b = (char*)base;
   const size_t NT = (size_t)N * g.T;
+  // face records: [0, Ftot) one per face instance, [Ftot, 2 Ftot) the second triangle of a face
+  // split at the near plane (only written for such faces)
   w.recs = (FaceRec*)(b + off);
-  off = align_up(off + sizeof(FaceRec) * (size_t)(Ftot > 0 ? Ftot : 1), 256);
+  off = align_up(off + sizeof(FaceRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.cnt = (int*)(b + off);
   w.vtot = w.cnt + NT;
   w.ctr = w.vtot + N;
@@ -198,6 +201,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * 64 * NT, 256);
   w.srec = (ShadeRec*)(b + off);
   off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
+  w.crec = (ClipRec*)(b + off);
+  off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.bytes = off;
   return w;
 }
@@ -212,6 +217,10 @@ struct SetupParams {
   int H, W, TX, TY, T;
   float bbox_pad;
   int persp, cull;
+  int clipz;      // near-plane clipping on
+  float zc;       // z_clip_value
+  int64_t NF;     // face instances (record id of a pair's second triangle = NF + rid)
+  ClipRec* crec;
   int64_t list_cap;
   FaceRec* recs;
   int* cnt;
@@ -316,7 +325,11 @@ MR_DEV bool rec_tiles(const SetupParams& P, const FaceRec& r, int& tx0, int& tx1
   return true;
 }
 
+MR_DEV FaceRec make_rec_core(int cull, int persp, uint32_t face, const float v[3][3]);
 MR_DEV FaceRec make_rec(const SetupParams& P, uint32_t face, const float v[3][3]) {
+  return make_rec_core(P.cull, P.persp, face, v);
+}
+MR_DEV FaceRec make_rec_core(int cull, int persp, uint32_t face, const float v[3][3]) {
   FaceRec r;
   r.x0 = v[0][0]; r.y0 = v[0][1]; r.z0 = v[0][2];
   r.x1 = v[1][0]; r.y1 = v[1][1]; r.z1 = v[1][2];
@@ -331,11 +344,11 @@ MR_DEV FaceRec make_rec(const SetupParams& P, uint32_t face, const float v[3][3]
   r.ymax = smax(r.y0, smax(r.y1, r.y2));
   const float zmax = smax(r.z0, smax(r.z1, r.z2));
   bool valid = fin;
-  if (P.cull && face_area < 0.0f) valid = false;
+  if (cull && face_area < 0.0f) valid = false;
   if ((double)face_area <= MR_KEPS_D && (double)face_area >= -1.0f * MR_KEPS_D) valid = false;
   if (zmax < 0.0f) valid = false;
   bool fast = valid && __builtin_isfinite(r.area) && r.area != 0.0f;
-  if (P.persp) fast = fast && r.z0 > 0.0f && r.z1 > 0.0f && r.z2 > 0.0f;
+  if (persp) fast = fast && r.z0 > 0.0f && r.z1 > 0.0f && r.z2 > 0.0f;
   r.flags = (valid ? FR_VALID : 0u) | (fast ? FR_FAST : 0u);
   return r;
 }
@@ -349,6 +362,42 @@ MR_DEV void world_face_verts(const float* __restrict__ verts, const int32_t* __r
     project_point(V, X, vx, vy, vz, v[c][0], v[c][1]);
     v[c][2] = vz;
   }
+}
+
+// The record(s) of face instance rid (mesh face `face`, projected corners v): the face itself,
+// or with near-plane clipping its sub-triangle(s) (recs[rid] and, for a split quadrilateral,
+// recs[NF + rid]) and their ClipRecs. Returns the second record through r1 (flags 0 if none).
+MR_DEV FaceRec build_records(const SetupParams& P, int64_t rid, uint32_t face, const float v[3][3], FaceRec& r1) {
+  r1.flags = 0u;
+  if (!P.clipz) return make_rec(P, face, v);
+  int i = 0;
+  const int nb = clip_class(v, P.zc, i);
+  if (nb == 0) return make_rec(P, face, v);
+  FaceRec r0 = make_rec(P, face, v);
+  if (nb == 3) {  // entirely behind the plane: culled
+    r0.flags = 0u;
+    return r0;
+  }
+  float sv[3][3];
+  ClipRec cr;
+  clip_sub(v, nb, i, 0, P.zc, P.persp != 0, sv, cr);
+  r0 = make_rec(P, face, sv);
+  r0.flags |= FR_CLIP | (nb == 1 ? FR_PAIR : 0u);
+  P.crec[rid] = cr;
+  if (nb == 1) {
+    clip_sub(v, nb, i, 1, P.zc, P.persp != 0, sv, cr);
+    r1 = make_rec(P, face, sv);
+    r1.flags |= FR_CLIP | FR_PAIR;
+    P.crec[P.NF + rid] = cr;
+    P.recs[P.NF + rid] = r1;
+  }
+  return r0;
+}
+
+MR_DEV int rec_tile_count(const SetupParams& P, const FaceRec& r) {
+  int tx0, tx1, ty0, ty1;
+  if (!rec_tiles(P, r, tx0, tx1, ty0, ty1)) return 0;
+  return (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
 }
 
 // World mode (one mesh shared by N views, rec = n*F + f): project, write the record,
@@ -373,17 +422,21 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
     if (f >= F) break;
     float v[3][3];
     world_face_verts(verts, faces, f, V, v);
-    const FaceRec r = make_rec(P, (uint32_t)f, v);
+    FaceRec r2;
+    const FaceRec r = build_records(P, (int64_t)n * F + f, (uint32_t)f, v, r2);
     P.recs[(int64_t)n * F + f] = r;
-    int tx0, tx1, ty0, ty1;
-    if (rec_tiles(P, r, tx0, tx1, ty0, ty1)) {
-      mine += (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-          const int t = ty * P.TX + tx;
-          if (LDS) atomicAdd(&hist[t], 1);
-          else atomicAdd(&P.cnt[(int64_t)n * P.T + t], 1);
-        }
+    for (int q = 0; q < 2; ++q) {
+      const FaceRec& rq = q == 0 ? r : r2;
+      int tx0, tx1, ty0, ty1;
+      if (rec_tiles(P, rq, tx0, tx1, ty0, ty1)) {
+        mine += (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+        for (int ty = ty0; ty <= ty1; ++ty)
+          for (int tx = tx0; tx <= tx1; ++tx) {
+            const int t = ty * P.TX + tx;
+            if (LDS) atomicAdd(&hist[t], 1);
+            else atomicAdd(&P.cnt[(int64_t)n * P.T + t], 1);
+          }
+      }
     }
   }
   block_add_256(mine, &P.vtot[n]);  // also the barrier before the histogram flush
@@ -398,15 +451,28 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
   extern __shared__ __attribute__((aligned(16))) int hist[];
   const int n = blockIdx.y;
   const int64_t f0 = (int64_t)blockIdx.x * fpt * blockDim.x + threadIdx.x;
+  // q = 0: the face instance's record; q = 1: the second triangle of a split face (FR_PAIR)
+  auto rec_q = [&](int64_t f, int q, FaceRec& r) -> bool {
+    const int64_t rid = (int64_t)n * F + f;
+    r = P.recs[rid];
+    if (q == 0) return true;
+    if (!(r.flags & FR_PAIR)) return false;
+    r = P.recs[P.NF + rid];
+    return true;
+  };
+  const int nq = P.clipz ? 2 : 1;
   if (LDS) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      int tx0, tx1, ty0, ty1;
-      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
-        for (int ty = ty0; ty <= ty1; ++ty)
-          for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+      for (int q = 0; q < nq && f < F; ++q) {
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
+      }
     }
     __syncthreads();
     const int vb = P.vbase[n];
@@ -415,26 +481,32 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
     __syncthreads();
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      const int rid = (int)((int64_t)n * F + f);
-      int tx0, tx1, ty0, ty1;
-      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
-        for (int ty = ty0; ty <= ty1; ++ty)
-          for (int tx = tx0; tx <= tx1; ++tx) {
-            const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
-            if (pos < P.list_cap) P.list[pos] = rid;
-          }
+      for (int q = 0; q < nq && f < F; ++q) {
+        const int rid = (int)((int64_t)n * F + f + (q ? P.NF : 0));
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+              const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
+              if (pos < P.list_cap) P.list[pos] = rid;
+            }
+      }
     }
   } else {
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      const int rid = (int)((int64_t)n * F + f);
-      int tx0, tx1, ty0, ty1;
-      if (f < F && rec_tiles(P, P.recs[(int64_t)n * F + f], tx0, tx1, ty0, ty1))
-        for (int ty = ty0; ty <= ty1; ++ty)
-          for (int tx = tx0; tx <= tx1; ++tx) {
-            const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
-            if (pos < P.list_cap) P.list[pos] = rid;
-          }
+      for (int q = 0; q < nq && f < F; ++q) {
+        const int rid = (int)((int64_t)n * F + f + (q ? P.NF : 0));
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+              const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
+              if (pos < P.list_cap) P.list[pos] = rid;
+            }
+      }
     }
   }
 }
@@ -449,47 +521,99 @@ MR_DEV int mesh_of_face(const int64_t* __restrict__ first, int64_t N, int64_t f)
   return (int)lo;
 }
 
-// face_verts mode (PyTorch3D _C boundary): rec = packed face id. A workgroup whose 256
-// faces all belong to one mesh counts through an LDS histogram (the common case: meshes
-// are contiguous runs of faces); otherwise global atomics.
+// face_verts mode (PyTorch3D _C boundary): rec = packed face id. A workgroup takes a run of
+// 256 * MR_FV_FPT consecutive faces: their face_verts (36 B each) are staged in LDS with
+// coalesced 16-B loads, the mesh of each face comes from a binary search over the mesh offsets
+// cached in LDS (N <= MR_FV_NMAX; else in global memory), and a workgroup whose faces all belong
+// to one mesh (the common case: meshes are contiguous runs of faces) counts tiles through an LDS
+// histogram, otherwise with global atomics.
+#define MR_FV_FPT 2
+#define MR_FV_NMAX 2048
+struct FvBlock {
+  int64_t f0, nf;  // first face, faces of this workgroup
+  int n0, n1;      // meshes of the first and last face
+};
+
+MR_DEV int mesh_of_face_lds(const int* first32, int64_t N, int64_t f) {
+  int lo = 0, hi = (int)N - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (first32[mid] <= f) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Workgroup prologue: cache the mesh offsets in LDS; stage this workgroup's face_verts in LDS.
+MR_DEV FvBlock fv_block_setup(const float* __restrict__ fv, int64_t Ftot, const int64_t* __restrict__ first, int64_t N,
+                              int* first32, float* sfv, bool stage) {
+  FvBlock B;
+  B.f0 = (int64_t)blockIdx.x * blockDim.x * MR_FV_FPT;
+  B.nf = Ftot - B.f0 < (int64_t)blockDim.x * MR_FV_FPT ? Ftot - B.f0 : (int64_t)blockDim.x * MR_FV_FPT;
+  if (N <= MR_FV_NMAX)
+    for (int i = threadIdx.x; i < N; i += blockDim.x) first32[i] = (int)first[i];
+  if (stage) {
+    // 9 floats per face, the workgroup's floats start 16-B aligned (f0 is a multiple of 4)
+    const float4* src = (const float4*)(fv + 9 * B.f0);
+    const int n4 = ((uintptr_t)src & 15) == 0 ? (int)(9 * B.nf) / 4 : 0;  // else scalar loads below
+    for (int i = threadIdx.x; i < n4; i += blockDim.x) ((float4*)sfv)[i] = src[i];
+    for (int i = 4 * n4 + threadIdx.x; i < 9 * B.nf; i += blockDim.x) sfv[i] = fv[9 * B.f0 + i];
+  }
+  __syncthreads();
+  B.n0 = N <= MR_FV_NMAX ? mesh_of_face_lds(first32, N, B.f0) : mesh_of_face(first, N, B.f0);
+  B.n1 = N <= MR_FV_NMAX ? mesh_of_face_lds(first32, N, B.f0 + B.nf - 1) : mesh_of_face(first, N, B.f0 + B.nf - 1);
+  return B;
+}
+
+MR_DEV int fv_mesh(const FvBlock& B, const int* first32, const int64_t* first, int64_t N, int64_t f) {
+  if (B.n0 == B.n1) return B.n0;
+  return N <= MR_FV_NMAX ? mesh_of_face_lds(first32, N, f) : mesh_of_face(first, N, f);
+}
+
 template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot,
                                                       const int64_t* __restrict__ first, int64_t N) {
   extern __shared__ __attribute__((aligned(16))) int hist[];
-  const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t f = f0 + threadIdx.x;
-  const int64_t fl = f0 + blockDim.x - 1 < Ftot ? f0 + blockDim.x - 1 : Ftot - 1;
-  const int n0 = mesh_of_face(first, N, f0), n1 = mesh_of_face(first, N, fl);
-  const bool lds = LDS && n0 == n1;  // uniform over the workgroup
+  __shared__ __attribute__((aligned(16))) float sfv[9 * 256 * MR_FV_FPT];
+  __shared__ int first32[MR_FV_NMAX];
+  const FvBlock B = fv_block_setup(fv, Ftot, first, N, first32, sfv, true);
+  const bool lds = LDS && B.n0 == B.n1;  // uniform over the workgroup
   if (lds) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
   }
   int mine = 0;
-  int n = n0;
-  if (f < Ftot) {
-    n = lds ? n0 : mesh_of_face(first, N, f);
+  for (int k = 0; k < MR_FV_FPT; ++k) {
+    const int64_t lf = (int64_t)k * blockDim.x + threadIdx.x;
+    if (lf >= B.nf) break;
+    const int64_t f = B.f0 + lf;
+    const int n = fv_mesh(B, first32, first, N, f);
     float v[3][3];
     for (int c = 0; c < 3; ++c)
-      for (int k = 0; k < 3; ++k) v[c][k] = fv[9 * f + 3 * c + k];
-    const FaceRec r = make_rec(P, (uint32_t)f, v);
+      for (int q = 0; q < 3; ++q) v[c][q] = sfv[9 * lf + 3 * c + q];
+    FaceRec r2;
+    const FaceRec r = build_records(P, f, (uint32_t)f, v, r2);
     P.recs[f] = r;
-    int tx0, tx1, ty0, ty1;
-    if (rec_tiles(P, r, tx0, tx1, ty0, ty1)) {
-      mine = (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-          if (lds) atomicAdd(&hist[ty * P.TX + tx], 1);
-          else atomicAdd(&P.cnt[(int64_t)n * P.T + ty * P.TX + tx], 1);
-        }
+    int m = 0;
+    for (int q = 0; q < 2; ++q) {
+      const FaceRec& rq = q == 0 ? r : r2;
+      int tx0, tx1, ty0, ty1;
+      if (rec_tiles(P, rq, tx0, tx1, ty0, ty1)) {
+        m += (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+        for (int ty = ty0; ty <= ty1; ++ty)
+          for (int tx = tx0; tx <= tx1; ++tx) {
+            if (lds) atomicAdd(&hist[ty * P.TX + tx], 1);
+            else atomicAdd(&P.cnt[(int64_t)n * P.T + ty * P.TX + tx], 1);
+          }
+      }
     }
+    if (lds) mine += m;
+    else if (m) atomicAdd(&P.vtot[n], m);
   }
   if (lds) {
-    block_add_256(mine, &P.vtot[n0]);
+    block_add_256(mine, &P.vtot[B.n0]);
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
-      if (hist[i]) atomicAdd(&P.cnt[(int64_t)n0 * P.T + i], hist[i]);
-  } else if (mine) {
-    atomicAdd(&P.vtot[n], mine);
+      if (hist[i]) atomicAdd(&P.cnt[(int64_t)B.n0 * P.T + i], hist[i]);
   }
 }
 
@@ -497,42 +621,65 @@ template <bool LDS>
 __global__ void __launch_bounds__(256) k_bin_fill_fv(SetupParams P, int64_t Ftot, const int64_t* __restrict__ first,
                                                      int64_t N) {
   extern __shared__ __attribute__((aligned(16))) int hist[];
-  const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
-  const int64_t f = f0 + threadIdx.x;
-  const int64_t fl = f0 + blockDim.x - 1 < Ftot ? f0 + blockDim.x - 1 : Ftot - 1;
-  const int n0 = mesh_of_face(first, N, f0), n1 = mesh_of_face(first, N, fl);
-  const bool lds = LDS && n0 == n1;
-  FaceRec r;
-  int tx0 = 0, tx1 = -1, ty0 = 0, ty1 = -1;
-  bool ok = false;
-  if (f < Ftot) {
+  __shared__ int first32[MR_FV_NMAX];
+  const FvBlock B = fv_block_setup(nullptr, Ftot, first, N, first32, nullptr, false);
+  const bool lds = LDS && B.n0 == B.n1;
+  const int nq = P.clipz ? 2 : 1;
+  auto rec_q = [&](int64_t f, int q, FaceRec& r) -> bool {
     r = P.recs[f];
-    ok = rec_tiles(P, r, tx0, tx1, ty0, ty1);
-  }
+    if (q == 0) return true;
+    if (!(r.flags & FR_PAIR)) return false;
+    r = P.recs[P.NF + f];
+    return true;
+  };
   if (lds) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
-    if (ok)
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
-    __syncthreads();
-    const int vb = P.vbase[n0];
-    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
-      if (hist[i]) hist[i] = vb + atomicAdd(&P.cur[(int64_t)n0 * P.T + i], hist[i]);  // reserve a block
-    __syncthreads();
-    if (ok)
-      for (int ty = ty0; ty <= ty1; ++ty)
-        for (int tx = tx0; tx <= tx1; ++tx) {
-          const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
-          if (pos < P.list_cap) P.list[pos] = (int)f;
-        }
-  } else if (ok) {
-    const int n = mesh_of_face(first, N, f);
-    for (int ty = ty0; ty <= ty1; ++ty)
-      for (int tx = tx0; tx <= tx1; ++tx) {
-        const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
-        if (pos < P.list_cap) P.list[pos] = (int)f;
+    for (int k = 0; k < MR_FV_FPT; ++k) {
+      const int64_t lf = (int64_t)k * blockDim.x + threadIdx.x;
+      for (int q = 0; q < nq && lf < B.nf; ++q) {
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(B.f0 + lf, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) atomicAdd(&hist[ty * P.TX + tx], 1);
       }
+    }
+    __syncthreads();
+    const int vb = P.vbase[B.n0];
+    for (int i = threadIdx.x; i < P.T; i += blockDim.x)
+      if (hist[i]) hist[i] = vb + atomicAdd(&P.cur[(int64_t)B.n0 * P.T + i], hist[i]);  // reserve a block
+    __syncthreads();
+    for (int k = 0; k < MR_FV_FPT; ++k) {
+      const int64_t lf = (int64_t)k * blockDim.x + threadIdx.x;
+      for (int q = 0; q < nq && lf < B.nf; ++q) {
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(B.f0 + lf, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+              const int pos = atomicAdd(&hist[ty * P.TX + tx], 1);
+              if (pos < P.list_cap) P.list[pos] = (int)(B.f0 + lf + (q ? P.NF : 0));
+            }
+      }
+    }
+  } else {
+    for (int k = 0; k < MR_FV_FPT; ++k) {
+      const int64_t lf = (int64_t)k * blockDim.x + threadIdx.x;
+      if (lf >= B.nf) break;
+      const int64_t f = B.f0 + lf;
+      const int n = fv_mesh(B, first32, first, N, f);
+      for (int q = 0; q < nq; ++q) {
+        FaceRec r;
+        int tx0, tx1, ty0, ty1;
+        if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
+          for (int ty = ty0; ty <= ty1; ++ty)
+            for (int tx = tx0; tx <= tx1; ++tx) {
+              const int pos = P.vbase[n] + atomicAdd(&P.cur[(int64_t)n * P.T + ty * P.TX + tx], 1);
+              if (pos < P.list_cap) P.list[pos] = (int)(f + (q ? P.NF : 0));
+            }
+      }
+    }
   }
 }
 
@@ -672,7 +819,48 @@ MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur,
   return true;
 }
 
-#define MR_NONE 0x7fffffff  // "no face" sentinel, larger than any face id
+#define MR_NONE 0x7fffffff  // "no face" sentinel, larger than any face code
+
+// Sort code of a record id: upstream's clipped packed order puts the two triangles of a split
+// face at consecutive ids in place of the face, so the (z, face) tie order is by (face instance,
+// triangle): code = 2 * rid (+1 for the second triangle, record NF + rid). Requires NF < 2^30.
+MR_DEV unsigned rec_code(int id, int64_t NF) {
+  return id < NF ? 2u * (unsigned)id : 2u * (unsigned)(id - NF) + 1u;
+}
+MR_DEV int code_rec(unsigned code, int64_t NF) {
+  return (code & 1u) ? (int)(NF + (code >> 1)) : (int)(code >> 1);
+}
+// The original face instance (pix_to_face) of a record id.
+MR_DEV int rec_orig(int id, int64_t NF) { return id >= NF ? (int)(id - NF) : id; }
+
+// A split face's two triangles at one pixel (upstream clipped_faces_neighbor_idx rule, for the
+// pair as one candidate): if both are kept the second replaces the first iff its distance to the
+// pixel is smaller than the first's |signed distance|; else whichever is kept. Returns the record
+// id and depth of the candidate.
+MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, const FaceRec& r, float x, float y,
+                      float pad, float blur, bool persp, bool clipb, int& cid, float& pz) {
+  const bool second = id >= NF;
+  const int oid = second ? (int)(id - NF) : (int)(id + NF);
+  const FaceRec ro = recs[oid];
+  const FaceRec& r1 = second ? ro : r;
+  const FaceRec& r2 = second ? r : ro;
+  const int id1 = second ? oid : id, id2 = second ? id : oid;
+  FragEval e1, e2;
+  const bool k1 = (r1.flags & FR_VALID) && eval_face(r1, x, y, pad, blur, persp, clipb, e1);
+  const bool k2 = (r2.flags & FR_VALID) && eval_face(r2, x, y, pad, blur, persp, clipb, e2);
+  if (k1 && k2) {
+    const bool use2 = fabsf(e2.sdist) < fabsf(e1.sdist);
+    cid = use2 ? id2 : id1;
+    pz = use2 ? e2.pz : e1.pz;
+    return true;
+  }
+  if (k1 || k2) {
+    cid = k1 ? id1 : id2;
+    pz = k1 ? e1.pz : e2.pz;
+    return true;
+  }
+  return false;
+}
 
 // (z, face) packed so that unsigned order == frag_less order on the depths that are ever
 // kept (pz >= 0; -0 folds onto +0, which the CPU compares equal). The empty key sorts
@@ -689,6 +877,8 @@ struct FwdParams {
   int persp, clipb;
   const int64_t* view_first;  // NULL: shared mode (overflow units scan faces n*F ..)
   int64_t F;                  // faces per view in shared mode (record id = n*F + face)
+  int64_t NF;                 // face instances: the second triangle of a split face is record NF + rid
+  const ClipRec* crec;        // conversions of clipped records (flag FR_CLIP)
   const FaceRec* recs;
   const int* list;
   const int4* units;
@@ -934,14 +1124,28 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
           id = id0;
           r = r1;
         }
+        // pixel rectangle: the record's padded bbox; an overflow unit scans only first triangles
+        // of split faces, so there it covers both triangles of the pair
+        float bx0 = r.xmin, bx1 = r.xmax, by0 = r.ymin, by1 = r.ymax;
+        bool bvalid = (r.flags & FR_VALID) != 0;
+        if (ovf && (r.flags & FR_PAIR)) {
+          const FaceRec ro = P.recs[P.NF + id];
+          if (ro.flags & FR_VALID) {
+            bx0 = bvalid ? smin(bx0, ro.xmin) : ro.xmin;
+            bx1 = bvalid ? smax(bx1, ro.xmax) : ro.xmax;
+            by0 = bvalid ? smin(by0, ro.ymin) : ro.ymin;
+            by1 = bvalid ? smax(by1, ro.ymax) : ro.ymax;
+            bvalid = true;
+          }
+        }
         int cx0, cx1, cy0, cy1;
-        ndc_range_to_pix(r.xmin - pad, r.xmax + pad, W, H, cx0, cx1);
-        ndc_range_to_pix(r.ymin - pad, r.ymax + pad, H, W, cy0, cy1);
+        ndc_range_to_pix(bx0 - pad, bx1 + pad, W, H, cx0, cx1);
+        ndc_range_to_pix(by0 - pad, by1 + pad, H, W, cy0, cy1);
         cx0 = cx0 > x0 ? cx0 : x0;
         cx1 = cx1 < x0 + MR_TS - 1 ? cx1 : x0 + MR_TS - 1;
         cy0 = cy0 > y0 ? cy0 : y0;
         cy1 = cy1 < y0 + MR_TS - 1 ? cy1 : y0 + MR_TS - 1;
-        if ((r.flags & FR_VALID) && cx0 <= cx1 && cy0 <= cy1) {
+        if (bvalid && cx0 <= cx1 && cy0 <= cy1) {
           const int w = cx1 - cx0 + 1;
           np = w * (cy1 - cy0 + 1);
           meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
@@ -999,9 +1203,13 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
           const int lx = loc - ly * w;
           const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
           const FaceRec r = S.rec[m];
+          const int id = S.id[m];
           float pz;
-          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
-            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, S.id[m]));
+          int cid = id;
+          const bool keep = (r.flags & FR_PAIR)
+                                ? pair_keep(P.recs, P.NF, id, r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, cid, pz)
+                                : frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
+          if (keep) atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, (int)rec_code(cid, P.NF)));
         }
       }
       wave_lds_sync();  // the stage is rewritten by the next batch
@@ -1025,10 +1233,10 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
       if (emit) k = atomicMin(dst, MR_KEY_EMPTY);
     }
     if (emit) {
-      const int f = (int)(unsigned)(k & 0xffffffffull);
+      const unsigned code = (unsigned)(k & 0xffffffffull);
       const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
-      const bool hit = f != MR_NONE && px < W && py < H;
-      P.sface[(int64_t)slot * 64 + lane] = hit ? f : -1;
+      const bool hit = code != MR_NONE && px < W && py < H;
+      P.sface[(int64_t)slot * 64 + lane] = hit ? code_rec(code, P.NF) : -1;
     }
     wave_lds_sync();
     ACC(acc_emit);
@@ -1126,14 +1334,19 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
     const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
     const int64_t q = n * HW + (int64_t)py * P.W + px;
     const FaceRec r = P.recs[f];
+    const int fo = rec_orig(f, P.NF);  // the original face instance
     PixGeom G;
-    if (MODE == 1) load_geom(P.srec, (uint32_t)(f - n * P.F), G);  // in parallel with the record
+    if (MODE == 1) load_geom(P.srec, (uint32_t)(fo - n * P.F), G);  // in parallel with the record
     FragEval ev;
     const bool hit = eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp,
                                P.clipb, ev);  // true by construction (same test that kept it)
     if (!hit) continue;
+    if (r.flags & FR_CLIP) {  // near-plane sub-triangle: barycentrics of the original face
+      const ClipRec cr = P.crec[f];
+      clip_unconvert(cr, ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+    }
     if (MODE == 0) {
-      P.p2f[q] = (int64_t)f;
+      P.p2f[q] = (int64_t)fo;
       P.zbuf[q] = ev.pz;
       P.dists[q] = ev.sdist;
       P.bary[3 * q + 0] = ev.b0;
@@ -1151,7 +1364,7 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
         P.rgb[q * CH + 2] = o.rgb[2];
         if (CH == 4) P.rgb[q * CH + 3] = o.alpha;
       }
-      if (P.p2f32) P.p2f32[q] = f;
+      if (P.p2f32) P.p2f32[q] = fo;
     }
   }
 }
@@ -1169,7 +1382,7 @@ static int resident_grid(K kernel, int threads, int fallback_per_cu) {
 
 // Static forward parameters from the settings; the workspace pointers from the carve.
 static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const RasterWS& w, int64_t N,
-                          const int64_t* view_first, int64_t F) {
+                          const int64_t* view_first, int64_t F, int64_t NF) {
   FwdParams P;
   memset(&P, 0, sizeof(P));
   P.N = (int)N; P.H = s->H; P.W = s->W; P.TX = g.TX; P.T = g.T; P.K = s->faces_per_pixel;
@@ -1177,7 +1390,7 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
   P.clipb = s->clip_barycentric_coords;
-  P.view_first = view_first; P.F = F;
+  P.view_first = view_first; P.F = F; P.NF = NF; P.crec = w.crec;
   P.recs = w.recs; P.list = w.list; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
   P.cnt = w.cnt; P.start = w.start; P.vbase = w.vbase; P.list_cap = g.list_cap; P.mfpb = g.mfpb;
   P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
@@ -1237,10 +1450,21 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
 #pragma unroll 1
       for (int j = 0; j < m; ++j) {
         const FaceRec r = rs[j];
+        const int id = ids[j];
         float pz;
-        if (in_img && (r.flags & FR_VALID) &&
-            frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz)) {
-          const unsigned long long key = frag_key(pz, ids[j]);
+        int cid = id;
+        bool keep = false;
+        if (in_img && (r.flags & FR_PAIR)) {
+          // a split face: the pair's candidate is inserted from its own entry (both entries are
+          // listed for every pixel either can keep), or from the first triangle's entry when an
+          // overflow unit scans the view's records (second triangles are not scanned there)
+          keep = pair_keep(P.recs, P.NF, id, r, xf, yf, pad, blur, persp, clipb, cid, pz) &&
+                 (cid == id || (ovf && id < P.NF));
+        } else if (in_img && (r.flags & FR_VALID)) {
+          keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
+        }
+        if (keep) {
+          const unsigned long long key = frag_key(pz, (int)rec_code(cid, P.NF));
           if (key < MR_KEY_EMPTY && (nq < K || key < q[(nq - 1) * 64])) {
             int i = nq < K ? nq : K - 1;
             while (i > 0 && q[(i - 1) * 64] > key) {
@@ -1261,10 +1485,12 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
       int64_t f = -1;
       float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
       if (k < nq) {
-        const int id = (int)(unsigned)(q[k * 64] & 0xffffffffull);
+        const int id = code_rec((unsigned)(q[k * 64] & 0xffffffffull), P.NF);
+        const FaceRec r = P.recs[id];
         FragEval ev;
-        eval_face(P.recs[id], xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
-        f = id; z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
+        eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
+        if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+        f = rec_orig(id, P.NF); z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
       }
       P.p2f[pix + k] = f;
       P.zbuf[pix + k] = z;
@@ -1368,6 +1594,8 @@ MR_DEV void acc_flush(LdsAcc<ACC>& L, float* __restrict__ gdst) {
 struct RasterBwdParams {
   int N, H, W, NBX, K;
   int persp, clipb;
+  int cull, clipz;
+  float zc, blur, bbox_pad;
   const float* fv;
   const int64_t* p2f;
   const float* gz;
@@ -1398,8 +1626,42 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
       r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
       r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
       const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
+      const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
       float g[3][3];
-      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+      int ci = 0;
+      const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};
+      const int nb = P.clipz ? clip_class(vv, P.zc, ci) : 0;
+      if (nb == 1 || nb == 2) {
+        // the face was split at the near plane: rebuild its sub-triangle(s) exactly as the forward
+        // binning did, pick the one that produced this fragment (the forward's pair rule), and chain
+        for (int c = 0; c < 3; ++c)
+          for (int q = 0; q < 3; ++q) g[c][q] = 0.0f;
+        float sv[3][3];
+        ClipRec cr0, cr1;
+        clip_sub(vv, nb, ci, 0, P.zc, P.persp != 0, sv, cr0);
+        FaceRec r0 = make_rec_core(P.cull, P.persp, 0u, sv);
+        int use = 0;
+        FaceRec r1;
+        if (nb == 1) {
+          clip_sub(vv, nb, ci, 1, P.zc, P.persp != 0, sv, cr1);
+          r1 = make_rec_core(P.cull, P.persp, 0u, sv);
+          FragEval e0, e1;
+          const bool k0 = (r0.flags & FR_VALID) && eval_face(r0, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e0);
+          const bool k1 = (r1.flags & FR_VALID) && eval_face(r1, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e1);
+          use = (k0 && k1) ? (fabsf(e1.sdist) < fabsf(e0.sdist) ? 1 : 0) : (k1 ? 1 : 0);
+        }
+        const FaceRec& rs = use ? r1 : r0;
+        const ClipRec& cr = use ? cr1 : cr0;
+        FragEval es;
+        eval_face(rs, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, es);
+        const float bs[3] = {es.b0, es.b1, es.b2};
+        float gs[3], gsub[3][3];
+        clip_gb_sub(cr, gb, gs);
+        raster_bwd_pixel(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
+        clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
+      } else {
+        raster_bwd_pixel(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+      }
       acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
     }
   }
@@ -1492,15 +1754,15 @@ MR_DEV void store_rt_partial(const float (&gR)[9], const float (&gT)[3], float* 
 }
 
 // Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
-// tile pixel the winning face record or -1; the pixel is implied by slot and lane), in two
-// kernels so that each stays small enough (VGPRs) to keep several waves per SIMD:
-//   k_bwd_shade: per covered pixel, recompute fragment + shading and differentiate the
-//                blends / Phong / texture -> 20-float record (grads of z, signed dist,
-//                barycentrics, interpolated point / normal / texel, and the barycentrics);
-//   k_bwd_geom : per covered pixel, rasterizer backward (edge functions, perspective
-//                correction, distances) + projection backward -> per-face rows summed over
-//                runs of equal faces (seg_scatter), and the slot's R/T partial sums.
-// Waves stride over slots (one 8x8 tile, one view each).
+// tile pixel the winning face record or -1; the pixel is implied by slot and lane). Per covered
+// pixel: half 1 recomputes fragment + shading and differentiates the blends / Phong / texture ->
+// a 20-float record (grads of z, signed dist, barycentrics, interpolated point / normal / texel,
+// and the barycentrics) handed to half 2 through the wave's LDS; half 2 runs the rasterizer
+// backward (edge functions, perspective correction, distances; the near-plane clip's chain rule
+// for split faces) + projection backward -> per-face rows summed over runs of equal faces
+// (seg_scatter), and the slot's R/T partial sums. (Measured: the same two halves as two kernels
+// with the record in HBM took 123 us against 102 for the fused kernel.)
+// Waves stride over XCD-contiguous slot ranges (one 8x8 tile, one view each).
 #define MR_BWD_REC 5  // float4s per pixel record
 struct RenderBwdParams {
   int N, H, W, TX, T;
@@ -1518,8 +1780,10 @@ struct RenderBwdParams {
   ShadeParams S;
   const ShadeRec* srec;
   int64_t F;     // faces of the shared mesh: record id rid = n*F + face
+  int64_t NF;    // N * F: the second triangle of a split face is record NF + rid
+  const ClipRec* crec;
+  float zc;      // z_clip_value (clipped records only)
   const ViewRec* views;
-  float4* prec;  // (slots, 64, MR_BWD_REC) per covered pixel
   float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
 };
@@ -1530,131 +1794,6 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
   const int ty = t / P.TX, tx = t - ty * P.TX;
   px = tx * MR_TS + (lane & 7);
   py = ty * MR_TS + (lane >> 3);
-}
-
-__global__ void __launch_bounds__(256) k_bwd_shade(RenderBwdParams P) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nslots = P.ctr[CTR_SLOTS];
-  const int64_t HW = (int64_t)P.H * P.W;
-  // slot s + G's tile and winners are loaded while slot s is processed
-  const int G = gridDim.x * 4;
-  int gt_n = 0, f_n = -1;
-  if (blockIdx.x * 4 + wave < nslots) {
-    gt_n = P.stile[blockIdx.x * 4 + wave];
-    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
-  }
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
-    const int gt = gt_n;
-    const int f = f_n;
-    if (s + G < nslots) {
-      gt_n = P.stile[s + G];
-      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
-    }
-    if (f < 0) continue;
-    int n, px, py;
-    slot_pixel(P, gt, lane, n, px, py);
-    const int64_t pix = n * HW + (int64_t)py * P.W + px;
-    // every load that depends only on the slot entry is issued here, together
-    const FaceRec r = P.recs[f];
-    PixGeom G;
-    load_geom(P.srec, (uint32_t)(f - n * P.F), G);
-    const float gD = P.gD ? P.gD[pix] : 0.0f;
-    const float gS = P.gS ? P.gS[pix] : 0.0f;
-    float gC[3] = {0.f, 0.f, 0.f}, gA = 0.0f;
-    if (P.gRGB) {
-      const float* g = P.gRGB + pix * P.rgb_ch;
-      gC[0] = g[0];
-      gC[1] = g[1];
-      gC[2] = g[2];
-      if (P.rgb_ch == 4) gA = g[3];
-    }
-    FragEval e;
-    float4* o4 = P.prec + ((int64_t)s * 64 + lane) * MR_BWD_REC;
-    if (!eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
-      // unreachable (slots hold kept fragments); a zero record contributes nothing
-      for (int k = 0; k < MR_BWD_REC; ++k) o4[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-      continue;
-    }
-    ShadeOut o;
-    ShadeCache C;
-    shade_fwd(P.S, n, true, G, e.b0, e.b1, e.b2, e.pz, e.sdist, o, C);
-    ShadeGrad SG;
-    shade_bwd(P.S, G, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
-    o4[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
-    o4[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
-    o4[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
-    o4[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
-    o4[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
-  }
-}
-
-template <int ACC>
-__global__ void __launch_bounds__(256) k_bwd_geom(RenderBwdParams P) {
-  __shared__ float lrow[4][64 * ACC];
-  __shared__ int lkey[4][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int nslots = P.ctr[CTR_SLOTS];
-  // slot s + G's tile and winners are loaded while slot s is processed
-  const int G = gridDim.x * 4;
-  int gt_n = 0, f_n = -1;
-  if (blockIdx.x * 4 + wave < nslots) {
-    gt_n = P.stile[blockIdx.x * 4 + wave];
-    f_n = P.sface[(int64_t)(blockIdx.x * 4 + wave) * 64 + lane];
-  }
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += G) {
-    const int gt = gt_n;
-    const int f = f_n;
-    if (s + G < nslots) {
-      gt_n = P.stile[s + G];
-      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
-    }
-    int n, px, py;
-    slot_pixel(P, gt, lane, n, px, py);
-    const ViewRec V = P.views[n];
-    float gR[9], gT[3];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
-    float row[ACC];
-#pragma unroll
-    for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
-    int key = -1;
-    if (f >= 0) {
-      const int face = (int)(f - n * P.F);
-      const FaceRec r = P.recs[f];
-      const float4* p4 = P.prec + ((int64_t)s * 64 + lane) * MR_BWD_REC;
-      const float4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
-      const float4 a4 = ACC == 27 ? p4[4] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
-      const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
-      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
-      const float gb[3] = {a0.z, a0.w, a1.x};
-      const float gP[3] = {a1.y, a1.z, a1.w};
-      const float gNn[3] = {a2.x, a2.y, a2.z};
-      const float b[3] = {a2.w, a3.x, a3.y};
-      const float gt3[3] = {a3.z, a3.w, a4.x};
-      float gfv[3][3];
-      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
-      key = face;
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        float gX[3];
-        project_bwd(V, X[c], gfv[c], gX, gR, gT);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          row[3 * c + k] = b[c] * gP[k] + gX[k];
-          row[9 + 3 * c + k] = b[c] * gNn[k];
-          if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
-        }
-      }
-    }
-    seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
-    // the slot's R/T partial sums (a slot is one view): wave reduction, no atomics
-    store_rt_partial(gR, gT, P.rt_part + (int64_t)s * 12, lane);
-  }
 }
 
 // Both halves in one kernel (the default): the shade backward's 20-float record goes through
@@ -1679,6 +1818,34 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, F
     g[3] = c[1];
     g[4] = c[2];
   }
+}
+
+// Raster backward of a near-plane sub-triangle (record f, flag FR_CLIP): gradients w.r.t. the
+// ORIGINAL face's projected corners. g_orig: gradient w.r.t. the original-face barycentrics (what
+// the shading used); the sub-triangle's barycentrics are recomputed, the raster backward runs on
+// the sub-triangle with C g_orig, and the clip's chain rule maps the sub-corners (and the
+// conversion weights) back to the original corners, which are re-projected from the world corners.
+__attribute__((noinline)) __device__ void clipped_raster_bwd(const RenderBwdParams& P, const FaceRec& r, int f,
+                                                             const ViewRec& V, const float X[3][3], float px,
+                                                             float py, float gz, const float g_orig[3], float gd,
+                                                             float gfv[3][3]) {
+  const ClipRec cr = P.crec[f];
+  FragEval e;
+  eval_face(r, px, py, P.bbox_pad, P.blur, P.persp, P.clipb, e);
+  const float bs[3] = {e.b0, e.b1, e.b2};
+  float gs[3], gsub[3][3];
+  clip_gb_sub(cr, g_orig, gs);
+  raster_bwd_pixel(r, px, py, P.persp, P.clipb, gz, gs, gd, gsub);
+  float v[3][3];
+  for (int c = 0; c < 3; ++c) {
+    float vx, vy, vz, nx, ny;
+    project_point(V, X[c], vx, vy, vz, nx, ny);
+    v[c][0] = nx;
+    v[c][1] = ny;
+    v[c][2] = vz;
+    gfv[c][0] = gfv[c][1] = gfv[c][2] = 0.0f;
+  }
+  clip_bwd_chain(cr, v, P.zc, P.persp != 0, bs, g_orig, gsub, gfv);
 }
 
 // Alpha-channel upstream gradient (RGBA outputs only; the drop-in frame has rgb_ch = 3).
@@ -1743,13 +1910,14 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (f >= 0) {
       PixGeom Gm;
-      load_geom(P.srec, (uint32_t)(f - n * P.F), Gm);
+      load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
       const float gD = gin[0], gS = gin[1];
       float gC[3] = {gin[2], gin[3], gin[4]};
       const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
       FragEval e;
       float4 o[MR_BWD_REC];
       if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
+        if (r.flags & FR_CLIP) clip_unconvert(P.crec[f], e.b0, e.b1, e.b2, e.b0, e.b1, e.b2);
         ShadeOut so;
         ShadeCache C;
         BACC(1);
@@ -1784,7 +1952,7 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
     int key = -1;
     if (f >= 0) {
-      const int face = (int)(f - n * P.F);
+      const int face = (int)(rec_orig(f, P.NF) - n * P.F);
       const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
       const float4 a3 = lrec[wave][3][lane];
       const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1798,7 +1966,10 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       const float gt3[3] = {a3.z, a3.w, a4.x};
       float gfv[3][3];
       BACC(4);
-      raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+      if (r.flags & FR_CLIP)
+        clipped_raster_bwd(P, r, f, V, X, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), a0.x, gb, a0.y, gfv);
+      else
+        raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
       key = face;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -2067,7 +2238,17 @@ int32_t mr_debug_set_prof(void* buf) {
 }
 #endif
 
-int32_t mr_version(void) { return 1; }
+int32_t mr_version(void) { return 2; }
+
+int32_t mr_struct_size(int32_t which) {
+  switch (which) {
+    case 0: return (int32_t)sizeof(mr_view_t);
+    case 1: return (int32_t)sizeof(mr_raster_settings_t);
+    case 2: return (int32_t)sizeof(mr_shade_params_t);
+    case 3: return (int32_t)sizeof(mr_mesh_t);
+    default: return -1;
+  }
+}
 
 static int check_settings(const mr_raster_settings_t* s) {
   if (!s) return set_err(MR_EINVAL, "settings is NULL");
@@ -2093,6 +2274,10 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
   P.cull = s->cull_backfaces;
+  P.clipz = s->clip_z != 0;
+  P.zc = s->z_clip_value;
+  P.NF = 0;  // set by the caller
+  P.crec = w.crec;
   P.list_cap = g.list_cap;
   P.recs = w.recs;
   P.cnt = w.cnt;
@@ -2132,20 +2317,22 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
-  FwdParams P = make_fwd(s, g, w, N, first, 0);
+  FwdParams P = make_fwd(s, g, w, N, first, 0, Fb);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.view_count = count;
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
+  SP.NF = Fb;
+  const int fvb = ceil_div(Ftot, 256 * MR_FV_FPT);
   if (Ftot > 0) {
-    if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
-    else MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
+    if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<fvb, 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
+    else MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<false><<<fvb, 256, 0, st>>>(SP, face_verts, Ftot, first, N)));
     MR_CHECK_LAUNCH("k_bin_count_fv");
   }
   if ((rc = launch_scan(w, N, g, count, 0, st))) return rc;
   if (Ftot > 0) {
-    if (lds) MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<true><<<ceil_div(Ftot, 256), 256, shm, st>>>(SP, Ftot, first, N)));
-    else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, Ftot, first, N)));
+    if (lds) MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<true><<<fvb, 256, shm, st>>>(SP, Ftot, first, N)));
+    else MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_fv<false><<<fvb, 256, 0, st>>>(SP, Ftot, first, N)));
     MR_CHECK_LAUNCH("k_bin_fill_fv");
   }
   if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
@@ -2166,6 +2353,8 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
   RasterBwdParams P;
   P.N = (int)N; P.H = s->H; P.W = s->W; P.NBX = ceil_div(s->W, MR_BT); P.K = s->faces_per_pixel;
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
+  P.cull = s->cull_backfaces; P.clipz = s->clip_z != 0; P.zc = s->z_clip_value;
+  P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.fv = fv; P.p2f = p2f; P.gz = gz; P.gb = gb; P.gd = gd; P.gfv = gfv;
   dim3 grid(P.NBX * ceil_div(s->H, MR_BT), (unsigned)N);
   MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd<<<grid, 256, 0, st>>>(P)));
@@ -2349,7 +2538,8 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, m->F);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   SetupParams SP = make_setup(s, g, w);
-  FwdParams P = make_fwd(s, g, w, N, nullptr, m->F);
+  SP.NF = N * m->F;
+  FwdParams P = make_fwd(s, g, w, N, nullptr, m->F, N * m->F);
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = w.srec;
   P.out_flags = sp->out_flags;
@@ -2360,8 +2550,7 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   const int64_t nzero = (int64_t)(zero_bytes(N, g) / sizeof(int));
   MR_TIMED(KID_SHADE_REC, st, (k_shade_rec_zero<<<(unsigned)(ceil_div(m->F, 256) + ceil_div(nzero, 1024)), 256, 0, st>>>(P.S, m->F, w.srec, w.cnt, nzero)));
   MR_CHECK_LAUNCH("k_shade_rec_zero");
-  static const int fpt_env = getenv("MR_BIN_FPT") ? atoi(getenv("MR_BIN_FPT")) : 0;
-  const int fpt = fpt_env > 0 ? fpt_env : MR_BIN_FPT;
+  const int fpt = MR_BIN_FPT;
   dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
@@ -2385,7 +2574,6 @@ size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, 
   size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);                 // gface
   off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);                    // gnu
   off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);                  // rt_part
-  off = align_up(off + sizeof(float4) * MR_BWD_REC * 64 * (size_t)NT, 256);    // prec
   return off;
 }
 
@@ -2442,8 +2630,6 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   float* gnu = (float*)(b + off);
   off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
   float* rt_part = (float*)(b + off);
-  off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);
-  float4* prec = (float4*)(b + off);
   if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
@@ -2463,33 +2649,22 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = w.srec;
   P.F = m->F;
+  P.NF = N * m->F;
+  P.crec = w.crec;
+  P.zc = s->z_clip_value;
   P.views = (const ViewRec*)views;
-  P.prec = prec;
   P.gface = gface;
   P.rt_part = rt_part;
-  static int g1 = 0, g2 = 0, g3 = 0;
-  if (!g1) g1 = resident_grid(k_bwd_shade, 256, 3);
-  if (!g2) g2 = resident_grid(k_bwd_geom<18>, 256, 3);
-  if (!g3) g3 = resident_grid(k_bwd_geom<27>, 256, 3);
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
   };
-  static const bool split = getenv("MR_BWD_SPLIT") != nullptr;  // two-kernel variant, for comparison
-  if (split) {
-    MR_TIMED(KID_BWD_SHADE, st, (k_bwd_shade<<<cap(g1), 256, 0, st>>>(P)));
-    MR_CHECK_LAUNCH("k_bwd_shade");
-    if (vcol) MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<27><<<cap(g3), 256, 0, st>>>(P)));
-    else MR_TIMED(KID_BWD_GEOM, st, (k_bwd_geom<18><<<cap(g2), 256, 0, st>>>(P)));
-    MR_CHECK_LAUNCH("k_bwd_geom");
-  } else {
-    static int f18 = 0, f27 = 0;
-    if (!f18) f18 = resident_grid(k_bwd_fused<18>, 256, 3);
-    if (!f27) f27 = resident_grid(k_bwd_fused<27>, 256, 2);
-    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27><<<cap(f27), 256, 0, st>>>(P)));
-    else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18><<<cap(f18), 256, 0, st>>>(P)));
-    MR_CHECK_LAUNCH("k_bwd_fused");
-  }
+  static int f18 = 0, f27 = 0;
+  if (!f18) f18 = resident_grid(k_bwd_fused<18>, 256, 3);
+  if (!f27) f27 = resident_grid(k_bwd_fused<27>, 256, 2);
+  if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27><<<cap(f27), 256, 0, st>>>(P)));
+  else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18><<<cap(f18), 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_bwd_fused");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V * MR_VL, 256);
   if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv)));

@@ -64,7 +64,9 @@ def vertex_adjacency(faces: torch.Tensor, V: int):
     return mesh_topology(faces, V)[1:]
 
 
-def raster_settings_struct(H, W, K=1, blur=0.0, persp=True, clip=False, cull=False, max_faces_per_bin=None):
+def raster_settings_struct(H, W, K=1, blur=0.0, persp=True, clip=False, cull=False, max_faces_per_bin=None,
+                           z_clip=None):
+    """mr_raster_settings_t; z_clip = z_clip_value of the near-plane clip (None: no clipping)."""
     s = MrRasterSettings()
     s.H, s.W, s.faces_per_pixel = int(H), int(W), int(K)
     s.blur_radius = float(blur)
@@ -72,12 +74,14 @@ def raster_settings_struct(H, W, K=1, blur=0.0, persp=True, clip=False, cull=Fal
     s.clip_barycentric_coords = int(bool(clip))
     s.cull_backfaces = int(bool(cull))
     s.max_faces_per_bin = int(max_faces_per_bin or 0)
+    s.clip_z = 0 if z_clip is None else 1
+    s.z_clip_value = 0.0 if z_clip is None else float(z_clip)
     return s
 
 
 # --------------------------------------------------------------------------- rasterize (PyTorch3D _C boundary)
 def rasterize_meshes_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=False, cull=False,
-                         max_faces_per_bin=None):
+                         max_faces_per_bin=None, z_clip=None):
     _require_cuda(face_verts, first, count)
     L = _lib.load()
     fv = face_verts.detach().float().contiguous()
@@ -85,7 +89,7 @@ def rasterize_meshes_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=Tr
     count = count.to(torch.int64).contiguous()
     N = first.numel()
     Ftot = fv.shape[0]
-    s = raster_settings_struct(H, W, K, blur, persp, clip, cull, max_faces_per_bin)
+    s = raster_settings_struct(H, W, K, blur, persp, clip, cull, max_faces_per_bin, z_clip)
     dev = fv.device
     p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
     zbuf = torch.empty((N, H, W, K), dtype=torch.float32, device=dev)
@@ -98,11 +102,12 @@ def rasterize_meshes_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=Tr
     return p2f, zbuf, bary, dists
 
 
-def rasterize_meshes_bwd(face_verts, p2f, gz, gb, gd, H, W, K=1, persp=True, clip=False):
+def rasterize_meshes_bwd(face_verts, p2f, gz, gb, gd, H, W, K=1, persp=True, clip=False, blur=0.0, cull=False,
+                         z_clip=None):
     L = _lib.load()
     fv = face_verts.detach().float().contiguous()
     N = p2f.shape[0]
-    s = raster_settings_struct(H, W, K, 0.0, persp, clip)
+    s = raster_settings_struct(H, W, K, blur, persp, clip, cull, None, z_clip)
     g = torch.empty_like(fv)
     check(L.mr_rasterize_meshes_backward(ptr(fv), ptr(p2f.contiguous()), ptr(gz.float().contiguous()),
                                          ptr(gb.float().contiguous()), ptr(gd.float().contiguous()), N,
@@ -114,23 +119,23 @@ class RasterizeFaceVerts(torch.autograd.Function):
     """Drop-in for PyTorch3D's _RasterizeFaceVerts (upstream mesh/rasterize_meshes.py)."""
 
     @staticmethod
-    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, mfpb):
+    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, mfpb, z_clip=None):
         p2f, zbuf, bary, dists = rasterize_meshes_fwd(face_verts, first, count, H, W, K, blur, persp, clip, cull,
-                                                      mfpb)
+                                                      mfpb, z_clip)
         ctx.save_for_backward(face_verts, p2f)
-        ctx.cfg = (H, W, K, persp, clip)
+        ctx.cfg = (H, W, K, persp, clip, blur, cull, z_clip)
         ctx.mark_non_differentiable(p2f)
         return p2f, zbuf, bary, dists
 
     @staticmethod
     def backward(ctx, _gp, gz, gb, gd):
         fv, p2f = ctx.saved_tensors
-        H, W, K, persp, clip = ctx.cfg
+        H, W, K, persp, clip, blur, cull, z_clip = ctx.cfg
         gz = torch.zeros_like(p2f, dtype=torch.float32) if gz is None else gz
         gb = torch.zeros(p2f.shape + (3,), device=p2f.device) if gb is None else gb
         gd = torch.zeros_like(p2f, dtype=torch.float32) if gd is None else gd
-        g = rasterize_meshes_bwd(fv, p2f, gz, gb, gd, H, W, K, persp, clip)
-        return (g,) + (None,) * 10
+        g = rasterize_meshes_bwd(fv, p2f, gz, gb, gd, H, W, K, persp, clip, blur, cull, z_clip)
+        return (g,) + (None,) * 11
 
 
 # --------------------------------------------------------------------------- projection
@@ -242,7 +247,7 @@ class ShadeConfig:
 
     def raster_struct(self):
         return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,
-                                      self.max_faces_per_bin)
+                                      self.max_faces_per_bin, self.z_clip)
 
     def shade_struct(self):
         sp = MrShadeParams()

@@ -19,8 +19,9 @@ argument meaning and outputs:
   ``MeshRenderer`` runs the K-deep HIP rasterizer and then the shader's modular pass over the
   stored fragments (soft_shading.py), exactly as upstream composes them.
 
-Rasterization always runs on the HIP kernels; there is no CPU fallback. Settings the MI355X path
-does not implement yet (near-plane clipping, cull_to_frustum) raise ``NotImplementedError``
+Rasterization always runs on the HIP kernels; there is no CPU fallback. Near-plane clipping
+(``z_clip_value``, znear / 2 for FoV cameras: upstream clip_faces) runs inside the HIP binning. The
+one setting the MI355X path does not implement (cull_to_frustum) raises ``NotImplementedError``
 rather than returning different numbers.
 """
 from __future__ import annotations
@@ -148,17 +149,10 @@ def _z_clip_value(cameras: CamerasBase, rs: RasterizationSettings):
     return None
 
 
-def _check_no_clipping(face_verts: torch.Tensor, z_clip, cull_to_frustum):
-    """upstream clip_faces is the identity when no vertex lies in front of the clip plane and
-    nothing is culled; anything else needs face splitting -> refuse."""
+def _check_cull_to_frustum(cull_to_frustum):
+    """Near-plane clipping (clip_faces) runs inside the HIP binning; frustum culling does not."""
     if cull_to_frustum:
         raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
-    if z_clip is None or face_verts.numel() == 0:
-        return
-    if bool((face_verts[..., 2] < z_clip).any()):
-        raise NotImplementedError(
-            f"geometry crosses the near clip plane z={z_clip}: triangle clipping (clip_faces) is not "
-            "implemented on the MI355X path yet")
 
 
 def _views(meshes: Meshes, cameras: CamerasBase, hw, kwargs):
@@ -205,14 +199,17 @@ class MeshRasterizer(torch.nn.Module):
         rs = kwargs.get("raster_settings", self.raster_settings)
         H, W = rs.hw()
         fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
-        _check_no_clipping(fv, _z_clip_value(cameras, rs), rs.cull_to_frustum)
+        _check_cull_to_frustum(rs.cull_to_frustum)
         persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
         clip = rs.blur_radius > 0.0 if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
         first = meshes.mesh_to_faces_packed_first_idx().to(fv.device)
         count = meshes.num_faces_per_mesh().to(fv.device)
+        # near-plane clipping (z_clip_value = znear / 2 for FoV cameras) happens inside the HIP
+        # binning: split faces are rasterized and mapped back to the original faces in-kernel
         p2f, zbuf, bary, dists = RasterizeFaceVerts.apply(fv, first, count, H, W, int(rs.faces_per_pixel),
                                                           float(rs.blur_radius), persp, clip,
-                                                          bool(rs.cull_backfaces), rs.max_faces_per_bin)
+                                                          bool(rs.cull_backfaces), rs.max_faces_per_bin,
+                                                          _z_clip_value(cameras, rs))
         return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
 
 
@@ -338,9 +335,6 @@ class MeshRenderer(torch.nn.Module):
         H, W = rs.hw()
         cfg = self._config(cameras, rs, H, W, kwargs)
         R, T, _ = _views(meshes, cameras, (H, W), kwargs)
-        if cfg.z_clip is not None:
-            _check_no_clipping(self.rasterizer.transform(meshes, cameras=cameras, R=R, T=T,
-                                                         raster_settings=rs).detach(), cfg.z_clip, False)
         # specular camera position: cameras.get_camera_center() without the R/T kwargs (upstream
         # shading.py), i.e. from the camera object's own R, T
         out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg)

@@ -49,6 +49,8 @@ def lib():
         L.orc_raster_fwd_ex.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, i32, i32, i32, i32, i32, i32,
                                         vp, vp, vp, vp]
         L.orc_raster_fwd_ex.restype = None
+        L.orc_raster_fwd_pairs.argtypes = [vp, vp, vp, vp, i32, i32, i32, i32, f32, i32, i32, i32, vp, vp, vp, vp]
+        L.orc_raster_fwd_pairs.restype = None
         L.orc_raster_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]
         L.orc_raster_bwd.restype = None
         L.orc_project_faces.argtypes = [vp, vp, i64, vp, i32, vp]
@@ -64,8 +66,10 @@ def _p(t):
 
 # ---------------------------------------------------------------- rasterizer
 def raster_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=False, cull=False, neighbor=None,
-               window=None):
-    """window = (y0, y1, x0, x1): rasterize only those pixels (others stay background)."""
+               window=None, pair_mode=0):
+    """window = (y0, y1, x0, x1): rasterize only those pixels (others stay background).
+    pair_mode = 1: split faces resolved as one candidate per pair (the MI355X rule; see
+    orc_raster_fwd_pairs) instead of the CPU's order-dependent neighbour rule."""
     fv = face_verts.detach().float().contiguous().cpu()
     first = first.to(torch.int64).contiguous().cpu()
     count = count.to(torch.int64).contiguous().cpu()
@@ -75,6 +79,12 @@ def raster_fwd(face_verts, first, count, H, W, K=1, blur=0.0, persp=True, clip=F
     bary = torch.empty((N, H, W, K, 3))
     dists = torch.empty((N, H, W, K))
     nb = None if neighbor is None else neighbor.to(torch.int64).contiguous().cpu()
+    if pair_mode:
+        assert window is None
+        lib().orc_raster_fwd_pairs(_p(fv), _p(first), _p(count), None if nb is None else _p(nb), N, H, W, K,
+                                   float(blur), int(persp), int(clip), int(cull), _p(p2f), _p(zbuf), _p(bary),
+                                   _p(dists))
+        return p2f, zbuf, bary, dists
     wy0, wy1, wx0, wx1 = window if window is not None else (0, 0, 0, 0)
     lib().orc_raster_fwd_ex(_p(fv), _p(first), _p(count), None if nb is None else _p(nb), N, H, W, K, float(blur),
                             int(persp), int(clip), int(cull), wy0, wy1, wx0, wx1, _p(p2f), _p(zbuf), _p(bary),
@@ -95,9 +105,10 @@ class RasterizeRef(torch.autograd.Function):
     """_RasterizeFaceVerts restated on the C oracle."""
 
     @staticmethod
-    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, neighbor=None, window=None):
+    def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, neighbor=None, window=None,
+                pair_mode=0):
         p2f, zbuf, bary, dists = raster_fwd(face_verts, first, count, H, W, K, blur, persp, clip, cull, neighbor,
-                                            window)
+                                            window, pair_mode)
         ctx.save_for_backward(face_verts, p2f)
         ctx.persp, ctx.clip = persp, clip
         ctx.mark_non_differentiable(p2f)
@@ -107,7 +118,7 @@ class RasterizeRef(torch.autograd.Function):
     def backward(ctx, _gp, gz, gb, gd):
         fv, p2f = ctx.saved_tensors
         g = raster_bwd(fv, p2f, gz, gb, gd, ctx.persp, ctx.clip)
-        return g, None, None, None, None, None, None, None, None, None, None, None
+        return g, None, None, None, None, None, None, None, None, None, None, None, None
 
 
 def project_faces_c(verts, faces, views):

@@ -156,6 +156,96 @@ static inline int finite9(const float* fv) {
  * Outputs (N,H,W,K): p2f i64, zbuf f32, dists f32; bary (N,H,W,K,3).
  * Background: -1 everywhere (as torch::full(..., -1)).
  */
+/* Per-(pixel, face) evaluation of the naive loop body; returns 1 if kept (fills *o). */
+static int eval_pixel_face(const float* fv, v2f p, float bbox_pad, float blur_radius, int perspective_correct,
+                           int clip_barycentric_coords, int cull_backfaces, frag_t* o, float* dist_out) {
+  if (!finite9(fv)) return 0;
+  const float x0 = fv[0], y0 = fv[1], z0 = fv[2];
+  const float x1 = fv[3], y1 = fv[4], z1 = fv[5];
+  const float x2 = fv[6], y2 = fv[7], z2 = fv[8];
+  const v2f v0 = {x0, y0}, v1 = {x1, y1}, v2 = {x2, y2};
+  const float face_area = edge_fn(v0, v1, v2);
+  if (cull_backfaces && face_area < 0.0f) return 0;
+  if ((double)face_area <= K_EPS_D && (double)face_area >= -1.0f * K_EPS_D) return 0;
+  const float xmin = smin(x0, smin(x1, x2)), xmax = smax(x0, smax(x1, x2));
+  const float ymin = smin(y0, smin(y1, y2)), ymax = smax(y0, smax(y1, y2));
+  const float zmax = smax(z0, smax(z1, z2));
+  if (zmax < 0.0f) return 0;
+  if (p.x > xmax + bbox_pad || p.x < xmin - bbox_pad || p.y > ymax + bbox_pad || p.y < ymin - bbox_pad) return 0;
+  float b0[3], b[3], bc[3];
+  bary_fwd(p, v0, v1, v2, b0);
+  if (perspective_correct) persp_fwd(b0, z0, z1, z2, b);
+  else memcpy(b, b0, sizeof(b));
+  if (clip_barycentric_coords) clip_fwd(b, bc);
+  else memcpy(bc, b, sizeof(bc));
+  const float pz = bc[0] * z0 + bc[1] * z1 + bc[2] * z2;
+  if (pz < 0.0f) return 0;
+  const float dist = pt_tri_dist(p, v0, v1, v2);
+  const int inside = b[0] > 0.0f && b[1] > 0.0f && b[2] > 0.0f;
+  if (!inside && dist >= blur_radius) return 0;
+  o->z = pz; o->d = inside ? -dist : dist;
+  o->b0 = bc[0]; o->b1 = bc[1]; o->b2 = bc[2];
+  *dist_out = dist;
+  return 1;
+}
+
+/*
+ * The MI355X kernels' resolution of a split face's two triangles (pair_mode = 1): evaluated
+ * together at the pixel as ONE candidate (the second if both are kept and its distance is below
+ * the first's |signed distance|, else whichever is kept), inserted like any face. Identical to
+ * the CPU rule (pair_mode = 0) except when the first triangle was not among the K kept faces at
+ * the moment the second is visited (it lost to K nearer faces earlier in packed order): there the
+ * CPU keeps the second as a normal face. Documented deviation.
+ */
+void orc_raster_fwd_pairs(const float* face_verts, const int64_t* mesh_first, const int64_t* mesh_count,
+                          const int64_t* neighbor, int N, int H, int W, int K, float blur_radius,
+                          int perspective_correct, int clip_barycentric_coords, int cull_backfaces, int64_t* p2f,
+                          float* zbuf, float* bary, float* dists) {
+  const float bbox_pad = sqrtf(blur_radius);
+#pragma omp parallel for collapse(2) schedule(dynamic, 1)
+  for (int n = 0; n < N; ++n) {
+    for (int yi = 0; yi < H; ++yi) {
+      frag_t* q = (frag_t*)malloc(sizeof(frag_t) * (size_t)(K + 1));
+      const int64_t f0 = mesh_first[n], f1 = mesh_first[n] + mesh_count[n];
+      const float yf = pix_to_ndc(H - 1 - yi, H, W);
+      for (int xi = 0; xi < W; ++xi) {
+        const v2f p = {pix_to_ndc(W - 1 - xi, W, H), yf};
+        int qn = 0;
+        for (int64_t f = f0; f < f1; ++f) {
+          const int64_t nb = neighbor ? neighbor[f] : -1;
+          if (nb != -1 && nb < f) continue;  /* the second triangle: resolved with the first */
+          frag_t c;
+          float dist;
+          int kept = eval_pixel_face(face_verts + f * 9, p, bbox_pad, blur_radius, perspective_correct,
+                                     clip_barycentric_coords, cull_backfaces, &c, &dist);
+          c.f = f;
+          if (nb != -1) {
+            frag_t c2;
+            float dist2;
+            const int k2 = eval_pixel_face(face_verts + nb * 9, p, bbox_pad, blur_radius, perspective_correct,
+                                           clip_barycentric_coords, cull_backfaces, &c2, &dist2);
+            c2.f = nb;
+            if (k2 && (!kept || dist2 < fabsf(c.d))) c = c2;
+            kept = kept || k2;
+          }
+          if (!kept) continue;
+          q[qn++] = c;
+          if (qn > K) { frag_sort(q, qn); --qn; }
+        }
+        frag_sort(q, qn);
+        const int64_t pix = (((int64_t)n * H + yi) * W + xi) * K;
+        for (int k = 0; k < K; ++k) {
+          const int v = k < qn;
+          p2f[pix + k] = v ? q[k].f : -1; zbuf[pix + k] = v ? q[k].z : -1.0f; dists[pix + k] = v ? q[k].d : -1.0f;
+          bary[(pix + k) * 3 + 0] = v ? q[k].b0 : -1.0f; bary[(pix + k) * 3 + 1] = v ? q[k].b1 : -1.0f;
+          bary[(pix + k) * 3 + 2] = v ? q[k].b2 : -1.0f;
+        }
+      }
+      free(q);
+    }
+  }
+}
+
 void orc_raster_fwd_ex(const float* face_verts, const int64_t* mesh_first, const int64_t* mesh_count,
                        const int64_t* neighbor, int N, int H, int W, int K, float blur_radius,
                        int perspective_correct, int clip_barycentric_coords, int cull_backfaces, int wy0, int wy1,

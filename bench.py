@@ -48,9 +48,10 @@ def canonical_views(verts, n_total, H, W, dist_m=0.5, fov_deg=60.0, seed=0):
     return R_cv, t_cv, K
 
 
-def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
-    """Reference CPU path restated (oracle: C naive rasterizer + torch-CPU shading/autograd)
-    on a bounded sample: n_views frames, 1 warm-up + `reps` timed fwd+bwd passes."""
+def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3):
+    """Reference CPU path restated (oracle: C naive rasterizer + torch-CPU shading/autograd) on a
+    bounded sample of the same workload: `n_views` frames, 1 warm-up + `reps` timed fwd+bwd passes
+    on all host cores, then one view, one timed pass on 1 core."""
     import numpy as np
 
     from oracle import oracle as O
@@ -59,30 +60,45 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=2):
     img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
     tex = ("uv", torch.from_numpy(d["verts_uvs"]).float(), torch.from_numpy(d["faces_uvs"]).long(), img)
     s = min(H, W) / 2.0
-    intr = torch.tensor([[K[0, 0] / s, (W / 2.0 - K[0, 2]) / s, K[1, 1] / s, (H / 2.0 - K[1, 2]) / s]]).float()
-    intr = intr.expand(n_views, 4).contiguous()
+    intr1 = torch.tensor([[K[0, 0] / s, (W / 2.0 - K[0, 2]) / s, K[1, 1] / s, (H / 2.0 - K[1, 2]) / s]]).float()
     gen = torch.Generator().manual_seed(1)
     gD = torch.rand(n_views, H, W, generator=gen) * 2 - 1
     gS = torch.rand(n_views, H, W, generator=gen) * 2 - 1
     gC = torch.rand(n_views, H, W, 3, generator=gen) * 2 - 1
+
+    def one_pass(nv):
+        v = verts.clone().requires_grad_(True)
+        Rc = R_cv[:nv].clone().requires_grad_(True)
+        tc = t_cv[:nv].clone().requires_grad_(True)
+        Rp, Tp = opencv_to_pytorch3d(Rc, tc)
+        out = O.render_ref(v, faces, Rp, Tp, intr1.expand(nv, 4).contiguous(), H, W, texture=tex)
+        torch.autograd.backward([out["depth"], out["sil"], out["rgba"][..., :3]], [gD[:nv], gS[:nv], gC[:nv]])
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
+    threads = min(omp, cores)
+    tt = torch.get_num_threads()
+    O.set_threads(threads)
     times = []
     for it in range(reps + 1):
         t0 = time.perf_counter()
-        v = verts.clone().requires_grad_(True)
-        Rc = R_cv[:n_views].clone().requires_grad_(True)
-        tc = t_cv[:n_views].clone().requires_grad_(True)
-        Rp, Tp = opencv_to_pytorch3d(Rc, tc)
-        out = O.render_ref(v, faces, Rp, Tp, intr, H, W, texture=tex)
-        torch.autograd.backward([out["depth"], out["sil"], out["rgba"][..., :3]], [gD, gS, gC])
+        one_pass(n_views)
         if it > 0:
             times.append(time.perf_counter() - t0)
     sec = sum(times) / len(times)
-    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores
-    return {"value": n_views / sec, "unit": "frames/s", "cores": min(omp, cores), "kind": "port",
+    # 1 core: C rasterizer and torch both single-threaded, one view, one timed pass
+    O.set_threads(1)
+    torch.set_num_threads(1)
+    t0 = time.perf_counter()
+    one_pass(1)
+    sec1 = time.perf_counter() - t0
+    torch.set_num_threads(tt)
+    O.set_threads(threads)
+    return {"value": n_views / sec, "unit": "frames/s", "cores": threads, "kind": "port",
+            "value_1core": round(1.0 / sec1, 4),
             "sample": f"{n_views} views of the same workload (cow, {H}x{W}, fwd+bwd), 1 warm-up + {reps} timed "
-                      f"passes, {sec:.2f} s/pass; C naive rasterizer (OpenMP {min(omp, cores)} threads) + "
-                      f"torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
+                      f"passes, {sec:.2f} s/pass: C naive rasterizer (OpenMP {threads} threads) + torch-CPU "
+                      f"shading/autograd ({tt} threads); 1 core: 1 view, 1 timed pass, {sec1:.2f} s"}
 
 
 # Algorithmic bytes per launch: what each kernel must move at minimum for the

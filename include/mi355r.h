@@ -171,6 +171,31 @@ int32_t mr_render_backward_opencv(const mr_mesh_t* mesh, const float* vnormals_r
                                   void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_verts,
                                   float* grad_R_cv, float* grad_t_cv, float* grad_vcolors, void* stream);
 
+/* ---------------- soft shading over stored fragments (K >= 1) ---------------- */
+/* SoftPhongShader (out_flags = MR_OUT_RGB: phong_shading + softmax_rgb_blend) or SoftSilhouetteShader
+ * (MR_OUT_SIL: sigmoid_alpha_blend, rgb = 1) applied to the fragments of mr_rasterize_meshes
+ * (pix_to_face (N,H,W,K) packed ids n*F + f of ONE mesh shared by the N views, zbuf, bary
+ * (original-face barycentrics), dists). rgba (N,H,W,4) is written. The workspace holds per-face
+ * shading records and must be passed unchanged to the backward. */
+size_t mr_shade_fragments_workspace(int64_t F);
+int32_t mr_shade_fragments_forward(const mr_mesh_t* mesh, const int64_t* pix_to_face, const float* zbuf,
+                                   const float* bary, const float* dists, int64_t N, int32_t H, int32_t W, int32_t K,
+                                   const float* cam_centers, int64_t num_cam_centers, const mr_shade_params_t* sp,
+                                   float* rgba, void* workspace, size_t workspace_bytes, void* stream);
+/* Backward from grad_rgba (N,H,W,4): grad_zbuf / grad_dists (N,H,W,K), grad_bary (N,H,W,K,3) (for
+ * mr_rasterize_meshes_backward), grad_verts (V,3) of the attribute path (interpolated world positions and
+ * vertex normals), grad_vcolors (V,3; tex_kind 1), grad_tex_rgba (Ht,Wt,4) and grad_verts_uvs
+ * (num_verts_uvs,2) (tex_kind 2; either may be NULL). All are overwritten. */
+size_t mr_shade_fragments_backward_workspace(int64_t V, int64_t F);
+int32_t mr_shade_fragments_backward(const mr_mesh_t* mesh, const float* vnormals_raw, const int64_t* pix_to_face,
+                                    const float* zbuf, const float* bary, const float* dists, int64_t N, int32_t H,
+                                    int32_t W, int32_t K, const float* cam_centers, int64_t num_cam_centers,
+                                    const mr_shade_params_t* sp, const float* grad_rgba, const void* fwd_workspace,
+                                    void* bwd_workspace, size_t bwd_workspace_bytes, float* grad_zbuf,
+                                    float* grad_bary, float* grad_dists, float* grad_verts, float* grad_vcolors,
+                                    float* grad_tex_rgba, float* grad_verts_uvs, int64_t num_verts_uvs,
+                                    void* stream);
+
 /* ---------------- instrumentation ---------------- */
 /* Work counters left in `workspace` by the last mr_render_forward / mr_rasterize_meshes that used it
  * (same N, total faces, H, W, max_faces_per_bin). Synchronises `stream`; for benchmarks and tools.

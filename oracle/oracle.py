@@ -53,10 +53,17 @@ def lib():
         L.orc_raster_fwd_pairs.restype = None
         L.orc_raster_bwd.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, i32, vp]
         L.orc_raster_bwd.restype = None
+        L.orc_set_threads.argtypes = [i32]
+        L.orc_set_threads.restype = None
         L.orc_project_faces.argtypes = [vp, vp, i64, vp, i32, vp]
         L.orc_project_faces.restype = None
         _lib = L
     return _lib
+
+
+def set_threads(n: int) -> None:
+    """Threads of the C rasterizer (OpenMP) — the CPU baseline's core count."""
+    lib().orc_set_threads(int(n))
 
 
 def _p(t):

@@ -509,3 +509,15 @@ void orc_project_faces(const float* verts, const int32_t* faces, int64_t F, cons
 }
 
 int orc_version(void) { return 1; }
+
+/* OpenMP threads of the restated CPU rasterizer (bench.py's 1-core CPU baseline). */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+void orc_set_threads(int n) {
+#ifdef _OPENMP
+  omp_set_num_threads(n > 0 ? n : 1);
+#else
+  (void)n;
+#endif
+}

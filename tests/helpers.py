@@ -1,6 +1,7 @@
 """Shared test scaffolding: canonical camera batches for any asset."""
 import math
 
+import numpy as np
 import torch
 
 from torch_renderer_amd.assets import load_asset_arrays
@@ -63,5 +64,10 @@ def report(name, got, ref, tol=1e-4, rel_above_one=True):
     scale = ref.abs().max().item() if ref.numel() else 0.0
     bar = tol * max(1.0, scale) if rel_above_one else tol
     print(f"[parity] {name}: max|err| = {err:.3e}, scale = {scale:.3e}, bar = {bar:.3e}")
+    if err > bar:
+        i = int((got - ref).abs().reshape(-1).argmax())
+        idx = np.unravel_index(i, tuple(got.shape))
+        print(f"[parity]   worst at {tuple(int(x) for x in idx)}: got {got.reshape(-1)[i].item():.6e} "
+              f"ref {ref.reshape(-1)[i].item():.6e}; #entries over bar: {int(((got - ref).abs() > bar).sum())}")
     assert err <= bar, f"{name}: max abs err {err:.3e} > {bar:.3e} (scale {scale:.3e})"
     return err, scale

@@ -1,0 +1,102 @@
+"""The HIP soft shader over stored fragments (mr_shade_fragments_forward / _backward: SoftPhongShader
+and SoftSilhouetteShader for any faces_per_pixel) fed the oracle's OWN
+fragments, so the shading is isolated from rasterization: images within 1e-4 of the oracle's
+torch restatement of phong_shading + softmax_rgb_blend / sigmoid_alpha_blend, and gradients
+w.r.t. zbuf, barycentrics, dists, vertex positions (interpolated points and normals), vertex
+colours and the texture map within the bars of tests/helpers.report. Fragments: K-deep with
+deform_mesh_with_color.py's blur = ln(1/1e-4 - 1) * 1e-4 and barycentric clipping."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import oracle as O
+from tests.helpers import canonical_views, mesh_arrays, report
+from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
+from torch_renderer_amd.cameras import PerspectiveCameras
+from torch_renderer_amd.mesh_renderer import (BlendParams, Fragments, Materials, PointLights, SoftPhongShader,
+                                              SoftSilhouetteShader)
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+BLUR = math.log(1.0 / 1e-4 - 1.0) * 1e-4
+
+
+def _leaf(t):
+    return t.detach().clone().requires_grad_(True)
+
+
+@pytest.mark.parametrize("K", [1, 3, 8, 50])
+@pytest.mark.parametrize("texture", ["vertex", "uv"])
+@pytest.mark.parametrize("shader", ["phong", "silhouette"])
+def test_hip_shader_on_oracle_fragments(K, texture, shader):
+    H, W, N = 40, 48, 2
+    name = "teapot" if texture == "vertex" else "cow"
+    verts, faces, d = mesh_arrays(name)
+    R, T, intr, _ = canonical_views(verts, N, H, W)
+    ref = O.render_ref(verts, faces, R, T, intr, H, W, K=K, blur=BLUR, clip=True)
+    assert (ref["p2f"][..., min(K, 3) - 1] >= 0).any()
+    p2f = ref["p2f"]
+    g = torch.Generator().manual_seed(K)
+    light = {"kind": "point", "location": (0.3, 0.8, -2.5), "ambient": (0.5, 0.4, 0.3), "diffuse": (0.3, 0.4, 0.5),
+             "specular": (0.2, 0.25, 0.3)}
+    mat = {"ambient": (1.0, 0.9, 0.8), "diffuse": (1.0, 1.0, 0.7), "specular": (0.6, 1.0, 1.0), "shininess": 32.0}
+    cc = torch.tensor([[0.1, -0.2, 0.3]])
+    bg = (0.1, 0.2, 0.3)
+    # oracle shading on leaves
+    zb, ba, di = _leaf(ref["zbuf"]), _leaf(ref["bary"]), _leaf(ref["dists"])
+    vr = _leaf(verts)
+    local = p2f.clone()
+    local[p2f >= 0] = p2f[p2f >= 0] % faces.shape[0]
+    if texture == "vertex":
+        vcr = _leaf(torch.rand(verts.shape, generator=g))
+        texels = O.sample_textures_vertex(local, ba, vcr, faces)
+        tex_gpu_src = vcr
+    else:
+        img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
+        mr = _leaf(img * 0.9 + 0.05)
+        vuv = torch.from_numpy(d["verts_uvs"]).float()
+        fuv = torch.from_numpy(d["faces_uvs"]).long()
+        texels = O.sample_textures_uv(local, ba, vuv, fuv, mr)
+    if shader == "phong":
+        colors = O.phong_colors(local, ba, vr, faces, texels, light, mat, cc)
+        out_ref = O.softmax_rgb_blend(colors, p2f, zb, di, 1e-4, 1e-4, bg)
+    else:
+        sil = O.sigmoid_alpha(p2f, di, 1e-4)
+        out_ref = torch.cat([torch.ones(sil.shape + (3,)), sil[..., None]], -1)
+    go = torch.rand(out_ref.shape, generator=g) - 0.5
+    (out_ref * go).sum().backward()
+    # HIP shader on the same fragments
+    zg, bgp, dg = (_leaf(t.to(DEV)) for t in (ref["zbuf"], ref["bary"], ref["dists"]))
+    vg = _leaf(verts.to(DEV))
+    if texture == "vertex":
+        vcg = _leaf(tex_gpu_src.detach().to(DEV))
+        tex = TexturesVertex([vcg])
+    else:
+        mg = _leaf(mr.detach().to(DEV))
+        tex = TexturesUV(maps=[mg], faces_uvs=[fuv.to(DEV)], verts_uvs=[vuv.to(DEV)])
+    meshes = Meshes([vg], [faces.to(DEV)], tex).extend(N)
+    cams = PerspectiveCameras(device=DEV, R=torch.eye(3)[None], T=-cc @ torch.eye(3))
+    blend = BlendParams(sigma=1e-4, gamma=1e-4, background_color=bg)
+    frags = Fragments(p2f.to(DEV), zg, bgp, dg)
+    if shader == "phong":
+        lights = PointLights(location=[light["location"]], ambient_color=[light["ambient"]],
+                             diffuse_color=[light["diffuse"]], specular_color=[light["specular"]])
+        mats = Materials(ambient_color=[mat["ambient"]], diffuse_color=[mat["diffuse"]],
+                         specular_color=[mat["specular"]], shininess=mat["shininess"])
+        out = SoftPhongShader(device=DEV, cameras=cams, lights=lights, materials=mats, blend_params=blend)(frags, meshes)
+    else:
+        out = SoftSilhouetteShader(blend_params=blend)(frags, meshes, cameras=cams)
+    tag = f"K={K} {texture} {shader}"
+    report(f"{tag} rgba", out, out_ref)
+    (out * go.to(DEV)).sum().backward()
+    report(f"{tag} grad dists", dg.grad, di.grad)
+    if shader == "phong":
+        report(f"{tag} grad zbuf", zg.grad, zb.grad)
+        report(f"{tag} grad bary", bgp.grad, ba.grad)
+        report(f"{tag} grad verts", vg.grad, vr.grad)
+        if texture == "vertex":
+            report(f"{tag} grad vcolors", vcg.grad, vcr.grad)
+        else:
+            report(f"{tag} grad map", mg.grad, mr.grad)

@@ -200,3 +200,20 @@ def test_golden_fixtures_reproduce(fname):
     assert np.array_equal(zbuf.numpy().view(np.int32), d["zbuf"].view(np.int32))
     assert np.array_equal(bary.numpy().view(np.int32), d["bary"].view(np.int32))
     assert np.array_equal(dists.numpy().view(np.int32), d["dists"].view(np.int32))
+
+
+def test_oracle_under_address_and_ub_sanitizers():
+    """the C restatement built with -fsanitize=address,undefined and driven through
+    every entry point (forward, neighbour rule, pair mode, window, K > 1, blur, backward,
+    projection) runs clean."""
+    import os
+    import shutil
+    import subprocess
+
+    here = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+    if shutil.which(os.environ.get("CC", "gcc")) is None:
+        pytest.skip("no C compiler")
+    subprocess.run(["make", "-s", "-C", here, "asan"], check=True)
+    r = subprocess.run([os.path.join(here, "asan_driver")], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "ERROR" not in r.stderr and "runtime error" not in r.stderr, r.stderr

@@ -86,6 +86,13 @@ _SIGS = [
     ("mr_render_backward_opencv", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _I64, _VP, _I64,
                                          ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP,
                                          _VP, _VP, _VP, _SZ, _VP, _VP, _VP, _VP, _VP]),
+    ("mr_shade_fragments_workspace", _SZ, [_I64]),
+    ("mr_shade_fragments_forward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _VP, _VP, _I64, _I32, _I32, _I32, _VP,
+                                          _I64, ctypes.POINTER(MrShadeParams), _VP, _VP, _SZ, _VP]),
+    ("mr_shade_fragments_backward_workspace", _SZ, [_I64, _I64]),
+    ("mr_shade_fragments_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _VP, _VP, _VP, _I64, _I32, _I32, _I32,
+                                           _VP, _I64, ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _SZ, _VP, _VP,
+                                           _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_timing_enable", _I32, [_I32]),
     ("mr_timing_read", _I32, [_VP, _VP, _I32]),

@@ -61,14 +61,14 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade(unused)", "k_bwd_geom(unused)", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
-                                              "k_rt_vgrad_a"};
+                                              "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -1657,10 +1657,10 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
         const float bs[3] = {es.b0, es.b1, es.b2};
         float gs[3], gsub[3][3];
         clip_gb_sub(cr, gb, gs);
-        raster_bwd_pixel(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
+        raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
         clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
       } else {
-        raster_bwd_pixel(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+        raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
       }
       acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
     }
@@ -1835,7 +1835,7 @@ __attribute__((noinline)) __device__ void clipped_raster_bwd(const RenderBwdPara
   const float bs[3] = {e.b0, e.b1, e.b2};
   float gs[3], gsub[3][3];
   clip_gb_sub(cr, g_orig, gs);
-  raster_bwd_pixel(r, px, py, P.persp, P.clipb, gz, gs, gd, gsub);
+  raster_bwd_pixel<true>(r, px, py, P.persp, P.clipb, gz, gs, gd, gsub);
   float v[3][3];
   for (int c = 0; c < 3; ++c) {
     float vx, vy, vz, nx, ny;
@@ -1969,7 +1969,7 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       if (r.flags & FR_CLIP)
         clipped_raster_bwd(P, r, f, V, X, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), a0.x, gb, a0.y, gfv);
       else
-        raster_bwd_pixel(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+        raster_bwd_pixel<true>(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
       key = face;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -2222,6 +2222,234 @@ __global__ void __launch_bounds__(256) k_project_faces_bwd(const float* __restri
   if (threadIdx.x < 12) {
     const int i = threadIdx.x;
     atomicAdd(&gviews[n * 12 + i], ((red[0][i] + red[1][i]) + red[2][i]) + red[3][i]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 5. K-deep soft shading over stored fragments (SoftPhongShader / SoftSilhouetteShader on the
+//    output of mr_rasterize_meshes with faces_per_pixel = K; SURVEY §8f rank 1:
+//    deform_mesh_with_color.py:153-159 K = 50, renderer_comparison_with_pyrender.py:174-179).
+//    One thread per pixel walks its K fragments: Phong colour per fragment (interpolation,
+//    texture, lighting) and upstream's softmax_rgb_blend / sigmoid_alpha_blend across them.
+//    The backward returns the fragments' gradients (zbuf, bary, dists: into the rasterizer's
+//    backward) and the attribute gradients: per-face rows (world position, normal, vertex colour;
+//    summed over runs of equal faces per wave and fragment layer), texture-map texels and uvs.
+// ---------------------------------------------------------------------------
+struct FragShadeParams {
+  int N, H, W, K;
+  int64_t F;   // faces of the shared mesh; p2f holds packed ids n*F + f
+  int sil;     // 1: sigmoid_alpha_blend (rgb = 1); 0: Phong + softmax_rgb_blend
+  const int64_t* p2f;
+  const float* zbuf;
+  const float* bary;
+  const float* dists;
+  ShadeParams S;
+  const ShadeRec* srec;
+  float* rgba;          // (N,H,W,4)
+  const float* g_rgba;  // backward
+  float* g_zbuf;
+  float* g_bary;
+  float* g_dists;
+  float* gface;         // (F, ACC)
+  float* gmap;          // (Ht, Wt, 4) or null
+  float* guv;           // (Vt, 2) or null
+};
+
+// z_inv and the softmax weights exp((z_inv - zmax) / gamma) use IEEE division and expf here: with
+// gamma = 1e-4 the weights amplify z_inv's rounding 10^4-fold (K > 1 has z_inv < zmax).
+// Pass over the pixel's K fragments: z_inv max (masked entries count as 0, as upstream's
+// `z_inv * mask`), its first index, and (Phong) the blend sums; alpha product split into the
+// product of the non-zero factors and the count / index of zero factors (for the backward's
+// product-of-the-others).
+struct FragSums {
+  float zmax_raw, zmax;  // max_k z_inv (with masked zeros), clamped at 1e-10
+  int kmax;
+  float alpha_nz;        // product of the non-zero (1 - prob) factors
+  int nzero, kzero;
+  float numw[3], denw;   // sum_k w_k c_k, sum_k w_k
+};
+
+MR_DEV float frag_prob(float d, float inv_sigma) { return sigmoidf_((-d) * inv_sigma); }
+
+MR_DEV void frag_sums(const FragShadeParams& P, int64_t pix, int n, FragSums& R, bool colours) {
+  const ShadeParams& S = P.S;
+  const int64_t base = pix * P.K;
+  R.zmax_raw = 0.0f;
+  R.kmax = 0;
+  if (!P.sil) {
+    for (int k = 0; k < P.K; ++k) {
+      const bool m = P.p2f[base + k] >= 0;
+      const float zi = ((S.zfar - P.zbuf[base + k]) / (S.zfar - S.znear)) * (m ? 1.0f : 0.0f);
+      if (k == 0 || zi > R.zmax_raw) {
+        R.zmax_raw = zi;
+        R.kmax = k;
+      }
+    }
+  }
+  R.zmax = smax(R.zmax_raw, 1e-10f);
+  R.alpha_nz = 1.0f;
+  R.nzero = 0;
+  R.kzero = -1;
+  R.denw = 0.0f;
+  R.numw[0] = R.numw[1] = R.numw[2] = 0.0f;
+  const float isig = P.sil ? S.inv_sigma_sil : S.inv_sigma_rgb;
+  for (int k = 0; k < P.K; ++k) {
+    const int64_t f = P.p2f[base + k];
+    if (f < 0) continue;  // masked: prob 0, factor 1, weight 0
+    const float prob = frag_prob(P.dists[base + k], isig);
+    const float one_m = 1.0f - prob;
+    if (one_m == 0.0f) {
+      ++R.nzero;
+      R.kzero = k;
+    } else {
+      R.alpha_nz *= one_m;
+    }
+    if (P.sil || !colours) continue;
+    const float zi = (S.zfar - P.zbuf[base + k]) / (S.zfar - S.znear);
+    const float w = prob * expf((zi - R.zmax) / S.gamma);
+    PixGeom G;
+    load_geom(P.srec, (uint32_t)(f - (int64_t)n * P.F), G);
+    const float* b = P.bary + 3 * (base + k);
+    float col[3];
+    PhongCache C;
+    phong_fwd(S, n, G, b[0], b[1], b[2], col, C);
+    for (int c = 0; c < 3; ++c) R.numw[c] += w * col[c];
+    R.denw += w;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_frag_shade_fwd(FragShadeParams P) {
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t HW = (int64_t)P.H * P.W;
+  if (pix >= (int64_t)P.N * HW) return;
+  const int n = (int)(pix / HW);
+  FragSums R;
+  frag_sums(P, pix, n, R, true);
+  const float alpha = R.nzero ? 0.0f : R.alpha_nz;
+  float4 o;
+  if (P.sil) {
+    o = make_float4(1.0f, 1.0f, 1.0f, 1.0f - alpha);
+  } else {
+    const ShadeParams& S = P.S;
+    const float delta = smax(expf((1e-10f - R.zmax) / S.gamma), 1e-10f);
+    const float rden = frcp(R.denw + delta);
+    o = make_float4((R.numw[0] + delta * S.bg[0]) * rden, (R.numw[1] + delta * S.bg[1]) * rden,
+                    (R.numw[2] + delta * S.bg[2]) * rden, 1.0f - alpha);
+  }
+  ((float4*)P.rgba)[pix] = o;
+}
+
+template <int ACC>
+__global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
+  __shared__ float lrow[4][64 * ACC];
+  __shared__ int lkey[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t pix = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t HW = (int64_t)P.H * P.W;
+  const bool act = pix < (int64_t)P.N * HW;  // inactive lanes still join the uniform scatters
+  const int n = act ? (int)(pix / HW) : 0;
+  const ShadeParams& S = P.S;
+  FragSums R;
+  float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float g_num[3] = {0.f, 0.f, 0.f}, g_den = 0.0f, g_zmax = 0.0f, g_alpha = 0.0f;
+  if (act) {
+    frag_sums(P, pix, n, R, true);
+    g4 = ((const float4*)P.g_rgba)[pix];
+    g_alpha = -g4.w;  // A = 1 - alpha
+    if (!P.sil) {
+      const float ex = expf((1e-10f - R.zmax) / S.gamma);
+      const float delta = smax(ex, 1e-10f);
+      const float den = R.denw + delta;
+      const float rden = frcp(den);
+      const float gr[3] = {g4.x, g4.y, g4.z};
+      float g_delta = 0.0f;
+      for (int c = 0; c < 3; ++c) {
+        const float num = R.numw[c] + delta * S.bg[c];
+        g_num[c] = gr[c] * rden;
+        g_den += -gr[c] * num * (rden * rden);
+        g_delta += g_num[c] * S.bg[c];
+      }
+      g_delta += g_den;
+      // through the weights' exp((z_inv - zmax) / gamma): sum_k g_w_k w_k, with
+      // g_w_k = g_num . c_k + g_den, is g_num . numw + g_den * denw
+      const float gwe = ((g_num[0] * R.numw[0] + g_num[1] * R.numw[1]) + g_num[2] * R.numw[2]) + g_den * R.denw;
+      g_zmax = -(gwe * S.inv_gamma);
+      if (ex >= 1e-10f) g_zmax += -((g_delta * ex) * S.inv_gamma);
+      if (!(R.zmax_raw >= 1e-10f)) g_zmax = 0.0f;  // clamp(min=eps) blocks it
+    }
+  }
+  const int64_t base = pix * P.K;
+  const float isig = P.sil ? S.inv_sigma_sil : S.inv_sigma_rgb;
+#pragma unroll 1
+  for (int k = 0; k < P.K; ++k) {  // uniform over the wave (seg_scatter inside)
+    const int64_t f = act ? P.p2f[base + k] : -1;
+    float row[ACC];
+#pragma unroll
+    for (int q = 0; q < ACC; ++q) row[q] = 0.0f;
+    int key = -1;
+    if (f >= 0) {
+      const float d = P.dists[base + k];
+      const float prob = frag_prob(d, isig);
+      const float one_m = 1.0f - prob;
+      const float others = R.nzero == 0 ? R.alpha_nz * frcp(one_m) : (R.nzero == 1 && R.kzero == k ? R.alpha_nz : 0.0f);
+      float g_prob = g_alpha * (-others);
+      float gz = 0.0f;
+      float gb[3] = {0.f, 0.f, 0.f};
+      if (!P.sil) {
+        const int face = (int)(f - (int64_t)n * P.F);
+        const float zi = (S.zfar - P.zbuf[base + k]) / (S.zfar - S.znear);
+        const float E = expf((zi - R.zmax) / S.gamma);
+        const float w = prob * E;
+        PixGeom G;
+        load_geom(P.srec, (uint32_t)face, G);
+        const float* b = P.bary + 3 * (base + k);
+        float col[3];
+        PhongCache C;
+        phong_fwd(S, n, G, b[0], b[1], b[2], col, C);
+        const float g_w = ((g_num[0] * col[0] + g_num[1] * col[1]) + g_num[2] * col[2]) + g_den;
+        const float gcol[3] = {g_num[0] * w, g_num[1] * w, g_num[2] * w};
+        g_prob += g_w * E;
+        float g_zi = (g_w * prob) * E * S.inv_gamma;
+        if (k == R.kmax) g_zi += g_zmax;
+        gz = -(g_zi * S.inv_zrange);
+        float gP[3], gNn[3], gtex[3], guv[2];
+        phong_bwd(S, G, C, gcol, gb, gP, gNn, gtex, guv);
+        key = face;
+        for (int c = 0; c < 3; ++c)
+          for (int q = 0; q < 3; ++q) {
+            row[3 * c + q] = b[c] * gP[q];
+            row[9 + 3 * c + q] = b[c] * gNn[q];
+            if (ACC == 27) row[18 + 3 * c + q] = b[c] * gtex[q];
+          }
+        if (S.tex_kind == 2) {
+          if (P.gmap) tex_map_bwd(S, C.tap, gtex, P.gmap);
+          if (P.guv) {
+            const int32_t* fu = S.faces_uvs + 3 * (int64_t)face;
+            for (int c = 0; c < 3; ++c) {
+              if (guv[0] != 0.0f) atomicAdd(&P.guv[2 * (int64_t)fu[c]], b[c] * guv[0]);
+              if (guv[1] != 0.0f) atomicAdd(&P.guv[2 * (int64_t)fu[c] + 1], b[c] * guv[1]);
+            }
+          }
+        }
+      } else if (k == R.kmax) {
+        // silhouette: no depth dependence
+      }
+      const float gd = -((g_prob * (prob * (1.0f - prob))) * isig);
+      P.g_zbuf[base + k] = gz;
+      P.g_dists[base + k] = gd;
+      P.g_bary[3 * (base + k)] = gb[0];
+      P.g_bary[3 * (base + k) + 1] = gb[1];
+      P.g_bary[3 * (base + k) + 2] = gb[2];
+    } else if (act) {
+      P.g_zbuf[base + k] = 0.0f;
+      P.g_dists[base + k] = 0.0f;
+      P.g_bary[3 * (base + k)] = 0.0f;
+      P.g_bary[3 * (base + k) + 1] = 0.0f;
+      P.g_bary[3 * (base + k) + 2] = 0.0f;
+    }
+    if (!P.sil && S.light_kind == 0) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
+    else if (ACC == 27 && !P.sil) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
   }
 }
 
@@ -2677,6 +2905,107 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");
+  return MR_OK;
+}
+
+// ---------------- K-deep soft shading over stored fragments ----------------
+static int check_frags(const mr_mesh_t* m, const mr_shade_params_t* sp, const int64_t* p2f, const float* zbuf,
+                       const float* bary, const float* dists, int64_t N, int32_t H, int32_t W, int32_t K) {
+  int rc = check_mesh(m, sp);
+  if (rc) return rc;
+  if (N <= 0 || N > 65535 || H <= 0 || W <= 0 || K < 1 || K > MR_KMAX) return set_err(MR_EINVAL, "bad fragment sizes");
+  if (N * (int64_t)H * W * K >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W*K >= 2^31");
+  if (!p2f || !zbuf || !bary || !dists) return set_err(MR_EINVAL, "NULL fragment tensor");
+  const int of = sp->out_flags & (MR_OUT_SIL | MR_OUT_RGB);
+  if (of != MR_OUT_SIL && of != MR_OUT_RGB) return set_err(MR_EINVAL, "out_flags: exactly one of MR_OUT_SIL, MR_OUT_RGB");
+  return MR_OK;
+}
+
+static FragShadeParams make_frag(const mr_mesh_t* m, const mr_shade_params_t* sp, const float* cc, int64_t ncc,
+                                 const int64_t* p2f, const float* zbuf, const float* bary, const float* dists,
+                                 int64_t N, int32_t H, int32_t W, int32_t K, const void* ws) {
+  FragShadeParams P;
+  memset(&P, 0, sizeof(P));
+  P.N = (int)N; P.H = H; P.W = W; P.K = K;
+  P.F = m->F;
+  P.sil = (sp->out_flags & MR_OUT_SIL) ? 1 : 0;
+  P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
+  P.S = make_shade(m, sp, cc, ncc);
+  P.srec = (const ShadeRec*)ws;
+  return P;
+}
+
+size_t mr_shade_fragments_workspace(int64_t F) { return align_up(sizeof(ShadeRec) * (size_t)(F > 0 ? F : 1), 256); }
+
+int32_t mr_shade_fragments_forward(const mr_mesh_t* m, const int64_t* p2f, const float* zbuf, const float* bary,
+                                   const float* dists, int64_t N, int32_t H, int32_t W, int32_t K,
+                                   const float* cc, int64_t ncc, const mr_shade_params_t* sp, float* rgba,
+                                   void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_frags(m, sp, p2f, zbuf, bary, dists, N, H, W, K);
+  if (rc) return rc;
+  if (!rgba || !ws) return set_err(MR_EINVAL, "NULL output / workspace");
+  if (ws_bytes < mr_shade_fragments_workspace(m->F)) return set_err(MR_EWORKSPACE, "workspace too small");
+  if (sp->light_kind == 0 && (!cc || (ncc != 1 && ncc != N))) return set_err(MR_EINVAL, "camera centres");
+  hipStream_t st = (hipStream_t)stream;
+  FragShadeParams P = make_frag(m, sp, cc, ncc, p2f, zbuf, bary, dists, N, H, W, K, ws);
+  P.rgba = rgba;
+  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, (ShadeRec*)ws)));
+  MR_CHECK_LAUNCH("k_shade_rec");
+  MR_TIMED(KID_FRAG_SHADE, st, (k_frag_shade_fwd<<<ceil_div(N * (int64_t)H * W, 256), 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_frag_shade_fwd");
+  return MR_OK;
+}
+
+size_t mr_shade_fragments_backward_workspace(int64_t V, int64_t F) {
+  size_t off = align_up(sizeof(float) * 27 * (size_t)(F > 0 ? F : 1), 256);  // gface
+  return align_up(off + sizeof(float) * 3 * (size_t)(V > 0 ? V : 1), 256);    // gnu
+}
+
+int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const int64_t* p2f, const float* zbuf,
+                                    const float* bary, const float* dists, int64_t N, int32_t H, int32_t W,
+                                    int32_t K, const float* cc, int64_t ncc, const mr_shade_params_t* sp,
+                                    const float* grad_rgba, const void* fwd_ws, void* bws, size_t bws_bytes,
+                                    float* g_zbuf, float* g_bary, float* g_dists, float* g_verts, float* g_vcolors,
+                                    float* g_tex_rgba, float* g_verts_uvs, int64_t num_verts_uvs, void* stream) {
+  int rc = check_frags(m, sp, p2f, zbuf, bary, dists, N, H, W, K);
+  if (rc) return rc;
+  if (!grad_rgba || !fwd_ws || !bws || !g_zbuf || !g_bary || !g_dists || !g_verts)
+    return set_err(MR_EINVAL, "NULL argument");
+  if (bws_bytes < mr_shade_fragments_backward_workspace(m->V, m->F)) return set_err(MR_EWORKSPACE, "backward workspace too small");
+  if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
+  hipStream_t st = (hipStream_t)stream;
+  const bool vcol = m->tex_kind == 1;
+  const int ACC = vcol ? 27 : 18;
+  float* gface = (float*)bws;
+  float* gnu = (float*)((char*)bws + align_up(sizeof(float) * 27 * (size_t)m->F, 256));
+  if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
+  if (g_tex_rgba && m->tex_kind == 2 &&
+      hipMemsetAsync(g_tex_rgba, 0, sizeof(float) * 4 * (size_t)m->tex_h * m->tex_w, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
+  if (g_verts_uvs && m->tex_kind == 2 && num_verts_uvs > 0 &&
+      hipMemsetAsync(g_verts_uvs, 0, sizeof(float) * 2 * (size_t)num_verts_uvs, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
+  FragShadeParams P = make_frag(m, sp, cc, ncc, p2f, zbuf, bary, dists, N, H, W, K, fwd_ws);
+  P.g_rgba = grad_rgba;
+  P.g_zbuf = g_zbuf; P.g_bary = g_bary; P.g_dists = g_dists;
+  P.gface = gface;
+  P.gmap = m->tex_kind == 2 ? g_tex_rgba : nullptr;
+  P.guv = m->tex_kind == 2 ? g_verts_uvs : nullptr;
+  const int grid = ceil_div(N * (int64_t)H * W, 256);
+  if (vcol) MR_TIMED(KID_FRAG_SHADE_BWD, st, (k_frag_shade_bwd<27><<<grid, 256, 0, st>>>(P)));
+  else MR_TIMED(KID_FRAG_SHADE_BWD, st, (k_frag_shade_bwd<18><<<grid, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_frag_shade_bwd");
+  // vertex gradients of the attribute rows (interpolated positions and normals, vertex colours)
+  const int use_n = sp->light_kind == 0 && !P.sil;
+  const int vb = ceil_div(m->V * MR_VL, 256);
+  if (use_n) {
+    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
+    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
+    MR_CHECK_LAUNCH("k_rt_vgrad_a");
+  }
+  if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, g_verts, g_vcolors);
+  else k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, g_verts, g_vcolors);
+  MR_CHECK_LAUNCH("k_vgrad_b");
   return MR_OK;
 }
 

@@ -384,6 +384,10 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
 }
 
 // ---------------- rasterizer backward (geometry_utils.h) ----------------
+// FAST = false: IEEE divisions in the CPU's operand order (mr_rasterize_meshes_backward: per-fragment
+// gradients bitwise equal to the CPU restatement, which matters on sliver faces whose gradients
+// scale with 1/area^2); FAST = true: 1-ulp reciprocals (the fused render backward).
+template <bool FAST> MR_DEV float bdiv(float a, float b) { return FAST ? a * frcp(b) : a / b; }
 MR_DEV void edge_bwd(float px, float py, float ax, float ay, float bx, float by, float g, float d[6]) {
   // returns (dp.x, dp.y, da.x, da.y, db.x, db.y)
   d[0] = (by - ay) * g;
@@ -395,29 +399,30 @@ MR_DEV void edge_bwd(float px, float py, float ax, float ay, float bx, float by,
 }
 
 // BarycentricCoordsBackward -> dv[0..2] (x,y)
+template <bool FAST>
 MR_DEV void bary_bwd(float px, float py, const FaceRec& r, const float g[3], float dv[3][2]) {
   const float area = r.area;
-  const float area_inv = frcp(area);
-  const float area2_inv = area_inv * area_inv;
+  const float area2 = area * area;
+  const float area_inv = bdiv<FAST>(1.0f, area);
   const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
   const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
   const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
   float de[6], da[6];
   // w0: e0 over (p, v1, v2); area over (v2, v0, v1)
   edge_bwd(px, py, r.x1, r.y1, r.x2, r.y2, g[0] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[0] * (-e0 * area2_inv), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[0] * bdiv<FAST>(-e0, area2), da);
   float v0x = da[2], v0y = da[3];
   float v1x = de[2] + da[4], v1y = de[3] + da[5];
   float v2x = de[4] + da[0], v2y = de[5] + da[1];
   // w1: e1 over (p, v2, v0)
   edge_bwd(px, py, r.x2, r.y2, r.x0, r.y0, g[1] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[1] * (-e1 * area2_inv), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[1] * bdiv<FAST>(-e1, area2), da);
   const float w1v0x = de[4] + da[2], w1v0y = de[5] + da[3];
   const float w1v1x = da[4], w1v1y = da[5];
   const float w1v2x = de[2] + da[0], w1v2y = de[3] + da[1];
   // w2: e2 over (p, v0, v1)
   edge_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g[2] * area_inv, de);
-  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[2] * (-e2 * area2_inv), da);
+  edge_bwd(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1, g[2] * bdiv<FAST>(-e2, area2), da);
   const float w2v0x = de[2] + da[2], w2v0y = de[3] + da[3];
   const float w2v1x = de[4] + da[4], w2v1y = de[5] + da[5];
   const float w2v2x = da[0], w2v2y = da[1];
@@ -429,14 +434,14 @@ MR_DEV void bary_bwd(float px, float py, const FaceRec& r, const float g[3], flo
   dv[2][1] = (v2y + w1v2y) + w2v2y;
 }
 
+template <bool FAST>
 MR_DEV void persp_bwd(float w0, float w1, float w2, float z0, float z1, float z2, const float go[3], float gb[3],
                       float gzv[3]) {
   const float t0 = w0 * z1 * z2, t1 = w1 * z0 * z2, t2 = w2 * z0 * z1;
   const float d = smax(t0 + t1 + t2, (float)MR_KEPS_D);
-  const float rd = frcp(d);
   const float gdt = -t0 * go[0] - t1 * go[1] - t2 * go[2];
-  const float gd = gdt * (rd * rd);
-  const float g0 = gd + go[0] * rd, g1 = gd + go[1] * rd, g2 = gd + go[2] * rd;
+  const float gd = bdiv<FAST>(gdt, d * d);
+  const float g0 = gd + bdiv<FAST>(go[0], d), g1 = gd + bdiv<FAST>(go[1], d), g2 = gd + bdiv<FAST>(go[2], d);
   gb[0] = g0 * z1 * z2;
   gb[1] = g1 * z0 * z2;
   gb[2] = g2 * z0 * z1;
@@ -445,23 +450,24 @@ MR_DEV void persp_bwd(float w0, float w1, float w2, float z0, float z1, float z2
   gzv[2] = g0 * w0 * z1 + g1 * w1 * z0;
 }
 
+template <bool FAST>
 MR_DEV void clip_bwd(float c0, float c1, float c2, const float go[3], float gb[3]) {
   const float w0 = smax(c0, 0.0f), w1 = smax(c1, 0.0f), w2 = smax(c2, 0.0f);
   const float s = smax(w0 + w1 + w2, 1e-5f);
-  const float rs = frcp(s);
   const float num = w0 * go[0] + w1 * go[1] + w2 * go[2];
-  const float gs = -num * (rs * rs);
-  gb[0] = c0 > 0.0f ? go[0] * rs + gs : 0.0f;
-  gb[1] = c1 > 0.0f ? go[1] * rs + gs : 0.0f;
-  gb[2] = c2 > 0.0f ? go[2] * rs + gs : 0.0f;
+  const float gs = bdiv<FAST>(-num, s * s);
+  gb[0] = c0 > 0.0f ? bdiv<FAST>(go[0], s) + gs : 0.0f;
+  gb[1] = c1 > 0.0f ? bdiv<FAST>(go[1], s) + gs : 0.0f;
+  gb[2] = c2 > 0.0f ? bdiv<FAST>(go[2], s) + gs : 0.0f;
 }
 
+template <bool FAST>
 MR_DEV void pt_line_bwd(float px, float py, float ax, float ay, float bx, float by, float g, float& gax,
                         float& gay, float& gbx, float& gby) {
   const float dx = bx - ax, dy = by - ay;
   const float t_bot = dx * dx + dy * dy;
   const float t_top = dx * (px - ax) + dy * (py - ay);
-  const float t = fdiv(t_top, t_bot);
+  const float t = bdiv<FAST>(t_top, t_bot);
   const float tt = smin(smax(t, 0.0f), 1.0f);
   const float qx = (1.0f - tt) * ax + tt * bx, qy = (1.0f - tt) * ay + tt * by;
   const float ex = qx - px, ey = qy - py;
@@ -488,59 +494,60 @@ MR_DEV float pt_line_dist_fast(float px, float py, float ax, float ay, float bx,
   return ex * ex + ey * ey;
 }
 
+template <bool FAST>
 MR_DEV void pt_tri_bwd(float px, float py, const FaceRec& r, float g, float gv[3][2]) {
-  const float e01 = pt_line_dist_fast(px, py, r.x0, r.y0, r.x1, r.y1);
-  const float e02 = pt_line_dist_fast(px, py, r.x0, r.y0, r.x2, r.y2);
-  const float e12 = pt_line_dist_fast(px, py, r.x1, r.y1, r.x2, r.y2);
+  const float e01 = FAST ? pt_line_dist_fast(px, py, r.x0, r.y0, r.x1, r.y1) : pt_line_dist(px, py, r.x0, r.y0, r.x1, r.y1);
+  const float e02 = FAST ? pt_line_dist_fast(px, py, r.x0, r.y0, r.x2, r.y2) : pt_line_dist(px, py, r.x0, r.y0, r.x2, r.y2);
+  const float e12 = FAST ? pt_line_dist_fast(px, py, r.x1, r.y1, r.x2, r.y2) : pt_line_dist(px, py, r.x1, r.y1, r.x2, r.y2);
   for (int c = 0; c < 3; ++c) gv[c][0] = gv[c][1] = 0.0f;
   if (e01 <= e02 && e01 <= e12)
-    pt_line_bwd(px, py, r.x0, r.y0, r.x1, r.y1, g, gv[0][0], gv[0][1], gv[1][0], gv[1][1]);
+    pt_line_bwd<FAST>(px, py, r.x0, r.y0, r.x1, r.y1, g, gv[0][0], gv[0][1], gv[1][0], gv[1][1]);
   else if (e02 <= e01 && e02 <= e12)
-    pt_line_bwd(px, py, r.x0, r.y0, r.x2, r.y2, g, gv[0][0], gv[0][1], gv[2][0], gv[2][1]);
+    pt_line_bwd<FAST>(px, py, r.x0, r.y0, r.x2, r.y2, g, gv[0][0], gv[0][1], gv[2][0], gv[2][1]);
   else if (e12 <= e01 && e12 <= e02)
-    pt_line_bwd(px, py, r.x1, r.y1, r.x2, r.y2, g, gv[1][0], gv[1][1], gv[2][0], gv[2][1]);
+    pt_line_bwd<FAST>(px, py, r.x1, r.y1, r.x2, r.y2, g, gv[1][0], gv[1][1], gv[2][0], gv[2][1]);
 }
 
 // RasterizeMeshesBackward for one (pixel, face): grads of (zbuf, bary, dists)
 // -> grad of the face's NDC vertices gfv[corner][x,y,z].
+template <bool FAST>
 MR_DEV void raster_bwd_pixel(const FaceRec& r, float px, float py, bool persp, bool clipb, float gz, const float gb_up[3],
                              float gd, float gfv[3][3]) {
   const float e0 = edge_fn(px, py, r.x1, r.y1, r.x2, r.y2);
   const float e1 = edge_fn(px, py, r.x2, r.y2, r.x0, r.y0);
   const float e2 = edge_fn(px, py, r.x0, r.y0, r.x1, r.y1);
-  // forward quantities recomputed for the derivative (fast reciprocals: the signs, hence
-  // `inside`, are exact; the values feed gradients only)
-  const float ra = frcp(r.area);
-  const float w0 = e0 * ra, w1 = e1 * ra, w2 = e2 * ra;
+  // forward quantities recomputed for the derivative (with FAST, 1-ulp reciprocals: the signs,
+  // hence `inside`, stay exact; the values feed gradients only)
+  const float w0 = bdiv<FAST>(e0, r.area), w1 = bdiv<FAST>(e1, r.area), w2 = bdiv<FAST>(e2, r.area);
   float c0, c1, c2, b0, b1, b2;
   if (persp) {
     const float t0 = w0 * r.z1 * r.z2, t1 = w1 * r.z0 * r.z2, t2 = w2 * r.z0 * r.z1;
-    const float rd = frcp(smax(t0 + t1 + t2, (float)MR_KEPS_D));
-    c0 = t0 * rd; c1 = t1 * rd; c2 = t2 * rd;
+    const float d = smax(t0 + t1 + t2, (float)MR_KEPS_D);
+    c0 = bdiv<FAST>(t0, d); c1 = bdiv<FAST>(t1, d); c2 = bdiv<FAST>(t2, d);
   } else { c0 = w0; c1 = w1; c2 = w2; }
   if (clipb) {
     const float u0 = smax(c0, 0.0f), u1 = smax(c1, 0.0f), u2 = smax(c2, 0.0f);
-    const float rs = frcp(smax(u0 + u1 + u2, 1e-5f));
-    b0 = u0 * rs; b1 = u1 * rs; b2 = u2 * rs;
+    const float sm = smax(u0 + u1 + u2, 1e-5f);
+    b0 = bdiv<FAST>(u0, sm); b1 = bdiv<FAST>(u1, sm); b2 = bdiv<FAST>(u2, sm);
   } else { b0 = c0; b1 = c1; b2 = c2; }
   const bool inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
   const float sign = inside ? -1.0f : 1.0f;
   float dd[3][2];
-  pt_tri_bwd(px, py, r, sign * gd, dd);
+  pt_tri_bwd<FAST>(px, py, r, sign * gd, dd);
   float g0[3] = {gb_up[0] + gz * r.z0, gb_up[1] + gz * r.z1, gb_up[2] + gz * r.z2};
   float dz[3] = {0.0f, 0.0f, 0.0f};
   if (clipb) {
     float t[3];
-    clip_bwd(c0, c1, c2, g0, t);
+    clip_bwd<FAST>(c0, c1, c2, g0, t);
     g0[0] = t[0]; g0[1] = t[1]; g0[2] = t[2];
   }
   if (persp) {
     float t[3];
-    persp_bwd(w0, w1, w2, r.z0, r.z1, r.z2, g0, t, dz);
+    persp_bwd<FAST>(w0, w1, w2, r.z0, r.z1, r.z2, g0, t, dz);
     g0[0] = t[0]; g0[1] = t[1]; g0[2] = t[2];
   }
   float db[3][2];
-  bary_bwd(px, py, r, g0, db);
+  bary_bwd<FAST>(px, py, r, g0, db);
   const float bc[3] = {b0, b1, b2};
   for (int c = 0; c < 3; ++c) {
     gfv[c][0] = db[c][0] + dd[c][0];
@@ -573,4 +580,120 @@ MR_DEV void project_bwd(const ViewRec& V, const float X[3], const float gn[3], f
     for (int bb = 0; bb < 3; ++bb) gR[3 * a + bb] += X[a] * gv[bb];
   }
   for (int bb = 0; bb < 3; ++bb) gT[bb] += gv[bb];
+}
+
+// ---------------- per-fragment Phong colour (K-deep soft shading) ----------------
+// phong_shading for one (pixel, k) fragment: colour = (ambient + diffuse) * texel + specular,
+// the same terms as shade_fwd's colour part, without the blend (softmax_rgb_blend couples the K
+// fragments and is done by the caller). b = original-face barycentrics.
+struct PhongCache {
+  float P[3], Nn[3], nh[3], nlen, nden, l[3], lh[3], llen, lden, v[3], vh[3], vlen, vden;
+  float cosd, r[3], vr, as, texel[3], amb[3], diff[3];
+  TexTap tap;
+};
+
+MR_DEV void phong_fwd(const ShadeParams& S, int n, const PixGeom& G, float b0, float b1, float b2, float col[3],
+                      PhongCache& C) {
+  for (int k = 0; k < 3; ++k) {
+    C.P[k] = interp3(b0, b1, b2, G.X[0][k], G.X[1][k], G.X[2][k]);
+    C.amb[k] = S.mat_amb[k] * S.light_amb[k];
+  }
+  if (S.tex_kind == 2) {
+    const float u = interp3(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
+    const float v = interp3(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
+    tex_sample(S, u, v, C.texel, C.tap);
+  } else if (S.tex_kind == 1) {
+    for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);
+  } else {
+    C.texel[0] = C.texel[1] = C.texel[2] = 1.0f;
+  }
+  float spec[3] = {0.f, 0.f, 0.f};
+  if (S.light_kind == 0) {
+    for (int k = 0; k < 3; ++k) C.Nn[k] = interp3(b0, b1, b2, G.Nv[0][k], G.Nv[1][k], G.Nv[2][k]);
+    normalize3(C.Nn, C.nh, C.nlen, C.nden);
+    for (int k = 0; k < 3; ++k) C.l[k] = S.light_loc[k] - C.P[k];
+    normalize3(C.l, C.lh, C.llen, C.lden);
+    C.cosd = dot3(C.nh, C.lh);
+    const float angle = C.cosd > 0.0f ? C.cosd : 0.0f;
+    const float* cc = S.cam_centers + (int64_t)n * S.cam_center_stride;
+    for (int k = 0; k < 3; ++k) C.v[k] = cc[k] - C.P[k];
+    normalize3(C.v, C.vh, C.vlen, C.vden);
+    for (int k = 0; k < 3; ++k) C.r[k] = -C.lh[k] + 2.0f * (C.cosd * C.nh[k]);
+    C.vr = dot3(C.vh, C.r);
+    C.as = (C.vr > 0.0f ? C.vr : 0.0f) * (C.cosd > 0.0f ? 1.0f : 0.0f);
+    const float spow = fpow(C.as, S.shininess);
+    for (int k = 0; k < 3; ++k) {
+      C.diff[k] = S.mat_diff[k] * (S.light_diff[k] * angle);
+      spec[k] = S.mat_spec[k] * (S.light_spec[k] * spow);
+    }
+  } else {
+    for (int k = 0; k < 3; ++k) C.diff[k] = 0.0f;
+  }
+  for (int k = 0; k < 3; ++k) col[k] = (C.amb[k] + C.diff[k]) * C.texel[k] + spec[k];
+}
+
+// Backward of phong_fwd given the colour gradient gcol: gradients w.r.t. the barycentrics (gb),
+// the interpolated world point (gP), the interpolated (unnormalised) normal (gNn), the texel
+// (gtex) and the interpolated uv (guv; UV textures).
+MR_DEV void phong_bwd(const ShadeParams& S, const PixGeom& G, const PhongCache& C, const float gcol[3], float gb[3],
+                      float gP[3], float gNn[3], float gtex[3], float guv[2]) {
+  for (int k = 0; k < 3; ++k) {
+    gtex[k] = gcol[k] * (C.amb[k] + C.diff[k]);
+    gP[k] = gNn[k] = 0.0f;
+  }
+  if (S.light_kind == 0) {
+    float gangle = 0.0f, gspow = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      gangle += gcol[k] * C.texel[k] * S.mat_diff[k] * S.light_diff[k];
+      gspow += gcol[k] * S.mat_spec[k] * S.light_spec[k];
+    }
+    const float gas = (C.as > 0.0f) ? gspow * S.shininess * fpow(C.as, S.shininess - 1.0f) : 0.0f;
+    const float gvr = (C.vr > 0.0f && C.cosd > 0.0f) ? gas : 0.0f;
+    float gvh[3], gr[3], glh[3], gnh[3];
+    for (int k = 0; k < 3; ++k) {
+      gvh[k] = gvr * C.r[k];
+      gr[k] = gvr * C.vh[k];
+    }
+    float gcos = 2.0f * dot3(gr, C.nh);
+    for (int k = 0; k < 3; ++k) {
+      glh[k] = -gr[k];
+      gnh[k] = 2.0f * C.cosd * gr[k];
+    }
+    gcos += (C.cosd > 0.0f) ? gangle : 0.0f;
+    for (int k = 0; k < 3; ++k) {
+      gnh[k] += gcos * C.lh[k];
+      glh[k] += gcos * C.nh[k];
+    }
+    float gl[3], gvv[3];
+    normalize3_bwd(C.Nn, C.nlen, C.nden, gnh, gNn);
+    normalize3_bwd(C.l, C.llen, C.lden, glh, gl);
+    normalize3_bwd(C.v, C.vlen, C.vden, gvh, gvv);
+    for (int k = 0; k < 3; ++k) gP[k] = -gl[k] - gvv[k];
+  }
+  guv[0] = guv[1] = 0.0f;
+  for (int c = 0; c < 3; ++c) {
+    gb[c] = dot3(G.X[c], gP);
+    if (S.light_kind == 0) gb[c] += dot3(G.Nv[c], gNn);
+  }
+  if (S.tex_kind == 2) {
+    tex_sample_bwd(S, C.tap, gtex, guv[0], guv[1]);
+    for (int c = 0; c < 3; ++c) gb[c] += G.uv[c][0] * guv[0] + G.uv[c][1] * guv[1];
+  } else if (S.tex_kind == 1) {
+    for (int c = 0; c < 3; ++c) gb[c] += dot3(G.col[c], gtex);
+  }
+}
+
+// Gradient of the bilinear texel w.r.t. the (flipped, RGBA-padded) map: the four taps' weights
+// times gtex, added into gmap (Ht, Wt, 4) with float atomics (taps outside the map carry none).
+MR_DEV void tex_map_bwd(const ShadeParams& S, const TexTap& t, const float gtex[3], float* __restrict__ gmap) {
+  const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
+  const float w[4] = {(x1 - t.ix) * (y1 - t.iy), (t.ix - x0) * (y1 - t.iy), (x1 - t.ix) * (t.iy - y0),
+                      (t.ix - x0) * (t.iy - y0)};
+  const int xs[4] = {t.x0, t.x0 + 1, t.x0, t.x0 + 1}, ys[4] = {t.y0, t.y0, t.y0 + 1, t.y0 + 1};
+  for (int q = 0; q < 4; ++q) {
+    if (xs[q] < 0 || ys[q] < 0 || xs[q] >= S.tex_w || ys[q] >= S.tex_h || w[q] == 0.0f) continue;
+    float* dst = gmap + 4 * ((int64_t)(S.tex_h - 1 - ys[q]) * S.tex_w + xs[q]);  // torch.flip(maps, [H])
+    for (int c = 0; c < 3; ++c)
+      if (gtex[c] != 0.0f) atomicAdd(dst + c, w[q] * gtex[c]);
+  }
 }

@@ -420,3 +420,100 @@ def render_stats():
     check(_lib.load().mr_workspace_stats(ptr(ws), N, Ft, H, W, mfpb, ctypes.cast(out, ctypes.c_void_p),
                                          _lib.stream_handle(ws.device)))
     return {"entries": out[0], "units": out[1], "tiles": out[2], "covered": out[3]}
+
+
+# --------------------------------------------------------------------------- soft shading of stored fragments
+def _padded_rgba(tex_map):
+    """(Ht, Wt, 4) float32 copy of a (Ht, Wt, C) map as the kernels sample it (16-B texels)."""
+    Ht, Wt, C = tex_map.shape
+    rgba = torch.zeros((Ht, Wt, 4), dtype=torch.float32, device=tex_map.device)
+    rgba[..., :min(C, 3)] = tex_map.detach()[..., :3].float()
+    return rgba
+
+
+class ShadeFragments(torch.autograd.Function):
+    """SoftPhongShader / SoftSilhouetteShader over stored Fragments of ONE mesh shared by the N
+    views (pix_to_face = n*F + f), any faces_per_pixel: mr_shade_fragments_forward / _backward
+    (upstream mesh/shader.py, shading.py, blending.py).
+
+    Differentiable inputs: zbuf, bary, dists (gradients go to the rasterizer's backward), verts
+    (interpolated world positions and vertex normals), vcolors (TexturesVertex), tex_map and
+    verts_uvs (TexturesUV)."""
+
+    @staticmethod
+    def forward(ctx, zbuf, bary, dists, verts, vcolors, tex_map, verts_uvs, p2f, faces, faces_uvs, cam_centers,
+                cfg: ShadeConfig):
+        _require_cuda(zbuf, bary, dists, verts, p2f, faces)
+        L = _lib.load()
+        dev = verts.device
+        N, H, W, K = p2f.shape
+        v = verts.detach().float().contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
+        sil = not cfg.want_rgb
+        vn = raw = None
+        if cfg.light_kind == 0 and not sil:
+            vn, raw = _vertex_normals(v, f, vptr, vadj)
+        vcol = vcolors.detach().float().contiguous() if vcolors is not None else None
+        tex = TextureArgs(0)
+        if vcol is not None:
+            tex = TextureArgs(1)
+        elif tex_map is not None:
+            tex = TextureArgs(2, verts_uvs.detach().float().contiguous(), faces_uvs.to(torch.int32).contiguous(),
+                              _padded_rgba(tex_map))
+        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol)
+        sp = cfg.shade_struct()
+        sp.out_flags = _lib.MR_OUT_SIL if sil else _lib.MR_OUT_RGB
+        sp.rgb_channels = 4
+        if sil:
+            sp.light_kind = 1  # the silhouette blend reads no lighting (no vertex normals needed)
+        cc = cam_centers.float().contiguous().reshape(-1, 3)
+        frag = [t.contiguous() for t in (p2f, zbuf.detach().float(), bary.detach().float(), dists.detach().float())]
+        wsb = L.mr_shade_fragments_workspace(f.shape[0])
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        rgba = torch.empty((N, H, W, 4), device=dev)
+        check(L.mr_shade_fragments_forward(ctypes.byref(mesh), *(ptr(t) for t in frag), N, H, W, K, ptr(cc),
+                                           cc.shape[0], ctypes.byref(sp), ptr(rgba), ptr(ws), wsb,
+                                           _lib.stream_handle(dev)))
+        keep = [v, f, vptr, vadj, cc, ws] + frag + [t if t is not None else torch.empty(0, device=dev)
+                                                    for t in (vn, raw, vcol, tex.verts_uvs, tex.faces_uvs,
+                                                              tex.tex_rgba)]
+        ctx.save_for_backward(*keep)
+        ctx.cfg, ctx.tex_kind = cfg, tex.kind
+        ctx.map_shape = None if tex_map is None else tuple(tex_map.shape)
+        ctx.n_uv = 0 if verts_uvs is None else int(verts_uvs.shape[0])
+        return rgba
+
+    @staticmethod
+    def backward(ctx, g):
+        (v, f, vptr, vadj, cc, ws, p2f, zbuf, bary, dists, vn, raw, vcol, vuv, fuv, rgba_map) = ctx.saved_tensors
+        cfg = ctx.cfg
+        L = _lib.load()
+        dev = v.device
+        N, H, W, K = p2f.shape
+        e = lambda t: t if t.numel() else None  # noqa: E731
+        tex = TextureArgs(ctx.tex_kind, e(vuv), e(fuv), e(rgba_map))
+        mesh = _mesh_struct(v, f, vptr, vadj, e(vn), tex, e(vcol))
+        sp = cfg.shade_struct()
+        sp.out_flags = _lib.MR_OUT_RGB if cfg.want_rgb else _lib.MR_OUT_SIL
+        sp.rgb_channels = 4
+        if not cfg.want_rgb:
+            sp.light_kind = 1
+        bwb = L.mr_shade_fragments_backward_workspace(v.shape[0], f.shape[0])
+        bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
+        gz, gd = torch.empty_like(zbuf), torch.empty_like(dists)
+        gb = torch.empty_like(bary)
+        gv = torch.empty_like(v)
+        gc = torch.empty_like(vcol) if vcol.numel() else None
+        need_map = ctx.tex_kind == 2 and ctx.needs_input_grad[5]
+        need_uv = ctx.tex_kind == 2 and ctx.needs_input_grad[6]
+        gmap = torch.empty_like(rgba_map) if need_map else None
+        guv = torch.empty((ctx.n_uv, 2), device=dev) if need_uv else None
+        check(L.mr_shade_fragments_backward(ctypes.byref(mesh), ptr(e(raw)), ptr(p2f), ptr(zbuf), ptr(bary), ptr(dists),
+                                            N, H, W, K, ptr(cc), cc.shape[0], ctypes.byref(sp),
+                                            ptr(g.float().contiguous()), ptr(ws), ptr(bws), bwb, ptr(gz), ptr(gb),
+                                            ptr(gd), ptr(gv), ptr(gc), ptr(gmap), ptr(guv), ctx.n_uv,
+                                            _lib.stream_handle(dev)))
+        gm = gmap[..., :ctx.map_shape[-1]] if gmap is not None else None
+        if gm is not None and ctx.map_shape[-1] > 3:
+            gm = torch.cat([gmap[..., :3], torch.zeros(ctx.map_shape[:2] + (ctx.map_shape[-1] - 3,), device=dev)], -1)
+        return gz, gb, gd, gv, gc, gm, guv, None, None, None, None, None

@@ -15,9 +15,10 @@ argument meaning and outputs:
   raster + shade + blend, ``mr_render_forward``) and returns the shader's (N,H,W,4) image,
   differentiable w.r.t. vertex positions, R, T and vertex colours.
 
-* With ``faces_per_pixel > 1`` or ``blur_radius > 0`` (soft rasterization)
-  ``MeshRenderer`` runs the K-deep HIP rasterizer and then the shader's modular pass over the
-  stored fragments (soft_shading.py), exactly as upstream composes them.
+* With ``faces_per_pixel > 1`` or ``blur_radius > 0`` (soft rasterization),
+  or a texture map that needs gradients, ``MeshRenderer`` runs the K-deep HIP rasterizer and then
+  the shader over the stored fragments on the HIP kernels (``mr_shade_fragments_*``: per-fragment
+  Phong, softmax_rgb_blend / sigmoid_alpha_blend, analytic backward), as upstream composes them.
 
 Rasterization always runs on the HIP kernels; there is no CPU fallback. Near-plane clipping
 (``z_clip_value``, znear / 2 for FoV cameras: upstream clip_faces) runs inside the HIP binning. The
@@ -220,6 +221,83 @@ def rasterize(meshes: Meshes, cameras: CamerasBase, raster_settings: Rasterizati
 
 
 # --------------------------------------------------------------------------- shaders / renderer
+def _shade_config(sh, cameras, H, W, kwargs):
+    """Lighting / material / blend part of a ShadeConfig for shader `sh`. Per-call ``lights=``,
+    ``materials=``, ``blend_params=`` override the shader's own, as upstream SoftPhongShader.forward
+    does (the reference passes ``lights=`` on every call: mesh_deformer.py:153,197,
+    deform_mesh_with_color.py:185,342)."""
+    bp = kwargs.get("blend_params", sh.blend_params)
+    znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
+    zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
+    cfg = ShadeConfig(H=H, W=W, sigma_rgb=float(bp.sigma), gamma=float(bp.gamma), background=_bg_triple(bp),
+                      znear=float(znear), zfar=float(zfar), sigma_sil=float(bp.sigma), want_depth=False)
+    if isinstance(sh, SoftSilhouetteShader):
+        cfg.want_rgb = False
+        cfg.want_sil = True
+        return cfg
+    if not isinstance(sh, SoftPhongShader):
+        raise NotImplementedError(f"shader {type(sh).__name__} is not implemented on the MI355X path")
+    lights = kwargs.get("lights", sh.lights)
+    mats = kwargs.get("materials", sh.materials)
+    if isinstance(lights, AmbientLights):
+        cfg.light_kind = 1
+        cfg.light_ambient = lights.ambient_color
+    elif isinstance(lights, PointLights):
+        cfg.light_kind = 0
+        cfg.light_location = lights.location_tuple()
+        cfg.light_ambient = lights.ambient_color
+        cfg.light_diffuse = lights.diffuse_color
+        cfg.light_specular = lights.specular_color
+    else:
+        raise NotImplementedError(f"lights of type {type(lights).__name__}")
+    cfg.mat_ambient, cfg.mat_diffuse, cfg.mat_specular = (mats.ambient_color, mats.diffuse_color,
+                                                          mats.specular_color)
+    cfg.shininess = mats.shininess
+    cfg.want_sil = False
+    cfg.rgb_channels = 4
+    return cfg
+
+
+def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_center):
+    """The shader over stored fragments on the HIP kernels (mr_shade_fragments_*): one launch for a
+    batch of one shared mesh, one per mesh for a batch of distinct meshes. Returns (N,H,W,4)."""
+    from .kernels import ShadeFragments
+    from .structures import TexturesUV, TexturesVertex
+
+    p2f = fragments.pix_to_face
+    N = p2f.shape[0]
+    tex = meshes.textures
+    if cfg.want_rgb and tex is None:
+        raise ValueError("Meshes does not have textures")  # upstream Meshes.sample_textures
+    cc = cam_center.to(p2f.device).float().reshape(-1, 3)
+
+    def one(i0, i1, verts, faces, tex_i, first):
+        vc = tmap = vuv = fuv = None
+        if cfg.want_rgb and isinstance(tex_i, TexturesVertex):
+            vc = tex_i.verts_features_list()[0]
+            if vc.shape[-1] != 3:
+                raise NotImplementedError("TexturesVertex: only 3-channel features are supported")
+        elif cfg.want_rgb and isinstance(tex_i, TexturesUV):
+            tmap, fuv, vuv = tex_i.maps_list()[0], tex_i.faces_uvs_list()[0], tex_i.verts_uvs_list()[0]
+        elif cfg.want_rgb:
+            raise NotImplementedError(f"textures of type {type(tex_i).__name__}")
+        q = p2f[i0:i1]
+        if first:
+            q = torch.where(q >= 0, q - first, q)
+        c = cc[i0:i1] if cc.shape[0] > 1 else cc
+        return ShadeFragments.apply(fragments.zbuf[i0:i1], fragments.bary_coords[i0:i1], fragments.dists[i0:i1],
+                                    verts, vc, tmap, vuv, q.contiguous(), faces, fuv, c, cfg)
+
+    if meshes.is_shared():
+        return one(0, N, meshes.shared_verts(), meshes.shared_faces(), tex, 0)
+    firsts = meshes.mesh_to_faces_packed_first_idx().tolist()
+    outs = []
+    for i in range(N):
+        mi = meshes[i]
+        outs.append(one(i, i + 1, mi.shared_verts(), mi.shared_faces(), mi.textures, int(firsts[i])))
+    return torch.cat(outs, 0)
+
+
 class _SoftShader(torch.nn.Module):
     def __init__(self, device="cpu", cameras=None, lights=None, materials=None, blend_params=None):
         super().__init__()
@@ -229,29 +307,22 @@ class _SoftShader(torch.nn.Module):
         self.blend_params = blend_params if blend_params is not None else BlendParams()
 
     def forward(self, fragments, meshes, **kwargs):
-        raise NotImplementedError(f"{type(self).__name__} cannot shade stored fragments")
+        cameras = kwargs.get("cameras", self.cameras)
+        H, W = fragments.pix_to_face.shape[1:3]
+        cfg = _shade_config(self, cameras, H, W, kwargs)
+        if cfg.want_rgb and cameras is None:
+            raise ValueError("Cameras must be specified either at initialization or in the forward pass")
+        from .cameras import cached_camera_center
+
+        cc = cached_camera_center(cameras, fragments.pix_to_face.device) if cameras is not None else \
+            torch.zeros(1, 3, device=fragments.pix_to_face.device)
+        return shade_fragments(fragments, meshes, cfg, cc)
 
 
 class SoftPhongShader(_SoftShader):
-    """upstream mesh/shader.py SoftPhongShader: phong_shading + softmax_rgb_blend -> RGBA.
-
-    Called on stored Fragments (any faces_per_pixel) it runs the modular soft pass of
-    soft_shading.py; inside MeshRenderer with K = 1 and blur = 0 the fused launch shades instead."""
-
-    def forward(self, fragments, meshes, **kwargs):
-        from . import soft_shading as S
-
-        cameras = kwargs.get("cameras", self.cameras)
-        if cameras is None:
-            raise ValueError("Cameras must be specified either at initialization or in the forward pass")
-        lights = kwargs.get("lights", self.lights)
-        materials = kwargs.get("materials", self.materials)
-        bp = kwargs.get("blend_params", self.blend_params)
-        texels = S.sample_textures(meshes, fragments)
-        colors = S.phong_shading(meshes, fragments, texels, lights, materials, cameras.get_camera_center())
-        znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
-        zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
-        return S.softmax_rgb_blend(colors, fragments, bp, znear=float(znear), zfar=float(zfar))
+    """upstream mesh/shader.py SoftPhongShader: phong_shading + softmax_rgb_blend -> RGBA, on stored
+    Fragments of any faces_per_pixel (HIP: mr_shade_fragments_*); inside MeshRenderer with K = 1 and
+    blur = 0 the fused one-launch render shades instead."""
 
 
 class SoftSilhouetteShader(_SoftShader):
@@ -259,11 +330,6 @@ class SoftSilhouetteShader(_SoftShader):
 
     def __init__(self, blend_params=None):
         super().__init__(blend_params=blend_params)
-
-    def forward(self, fragments, meshes, **kwargs):
-        from . import soft_shading as S
-
-        return S.sigmoid_alpha_blend(fragments, kwargs.get("blend_params", self.blend_params))
 
 
 class MeshRenderer(torch.nn.Module):
@@ -275,45 +341,16 @@ class MeshRenderer(torch.nn.Module):
         self.shader = shader
 
     def _config(self, cameras, rs, H, W, kwargs):
-        """ShadeConfig of one fused call. Per-call ``lights=``, ``materials=``, ``blend_params=``
-        override the shader's own, as upstream SoftPhongShader.forward does (the reference passes
-        ``lights=`` on every call: mesh_deformer.py:153,197, deform_mesh_with_color.py:185,342)."""
+        """ShadeConfig of one fused call: the shader's (and per-call) lighting / blending plus the
+        rasterization settings."""
         if rs.cull_to_frustum:
             raise NotImplementedError("cull_to_frustum is not implemented on the MI355X path yet")
-        sh = self.shader
-        bp = kwargs.get("blend_params", sh.blend_params)
-        persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
-        clip = False if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
-        znear = kwargs.get("znear", getattr(cameras, "znear", 1.0))
-        zfar = kwargs.get("zfar", getattr(cameras, "zfar", 100.0))
-        cfg = ShadeConfig(H=H, W=W, persp=persp, clip=clip, cull=bool(rs.cull_backfaces),
-                          max_faces_per_bin=rs.max_faces_per_bin, sigma_rgb=float(bp.sigma), gamma=float(bp.gamma),
-                          background=_bg_triple(bp), znear=float(znear), zfar=float(zfar),
-                          sigma_sil=float(bp.sigma), want_depth=False, z_clip=_z_clip_value(cameras, rs))
-        if isinstance(sh, SoftSilhouetteShader):
-            cfg.want_rgb = False
-            cfg.want_sil = True
-            return cfg
-        if not isinstance(sh, SoftPhongShader):
-            raise NotImplementedError(f"shader {type(sh).__name__} is not implemented on the MI355X path")
-        lights = kwargs.get("lights", sh.lights)
-        mats = kwargs.get("materials", sh.materials)
-        if isinstance(lights, AmbientLights):
-            cfg.light_kind = 1
-            cfg.light_ambient = lights.ambient_color
-        elif isinstance(lights, PointLights):
-            cfg.light_kind = 0
-            cfg.light_location = lights.location_tuple()
-            cfg.light_ambient = lights.ambient_color
-            cfg.light_diffuse = lights.diffuse_color
-            cfg.light_specular = lights.specular_color
-        else:
-            raise NotImplementedError(f"lights of type {type(lights).__name__}")
-        cfg.mat_ambient, cfg.mat_diffuse, cfg.mat_specular = (mats.ambient_color, mats.diffuse_color,
-                                                              mats.specular_color)
-        cfg.shininess = mats.shininess
-        cfg.want_sil = False
-        cfg.rgb_channels = 4
+        cfg = _shade_config(self.shader, cameras, H, W, kwargs)
+        cfg.persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
+        cfg.clip = False if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
+        cfg.cull = bool(rs.cull_backfaces)
+        cfg.max_faces_per_bin = rs.max_faces_per_bin
+        cfg.z_clip = _z_clip_value(cameras, rs)
         return cfg
 
     def forward(self, meshes_world: Meshes, **kwargs) -> torch.Tensor:

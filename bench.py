@@ -147,6 +147,8 @@ def main():
     ap.add_argument("--cpu-views", type=int, default=2)
     ap.add_argument("--eager", action="store_true",
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
+    ap.add_argument("--texture", choices=("uv", "white"), default="uv",
+                    help="experiments only: 'white' drops the UV texture (not the benchmark workload)")
     ap.add_argument("--mode", choices=("render", "fragments"), default="render",
                     help="render: the headline fwd+bwd step; fragments: the rasterizer alone "
                          "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline)")
@@ -183,7 +185,11 @@ def main():
     R_cv = R_cv.to(dev).contiguous().requires_grad_(True)
     t_cv = t_cv.to(dev).contiguous().requires_grad_(True)
     verts = meshes.shared_verts().clone().requires_grad_(True)
-    bmesh = Meshes([verts], [faces], meshes.textures).extend(nv)
+    tex = meshes.textures
+    if args.texture == "white":
+        from torch_renderer_amd.structures import TexturesVertex
+        tex = TexturesVertex([torch.ones_like(verts).detach()])
+    bmesh = Meshes([verts], [faces], tex).extend(nv)
     renderer = DepthColorRender(K.to(dev), (H, W), device=dev)
     gen = torch.Generator().manual_seed(1 + rank)
     gD = (torch.rand(nv, H, W, generator=gen) * 2 - 1).to(dev)

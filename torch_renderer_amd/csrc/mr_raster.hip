@@ -838,6 +838,14 @@ MR_DEV int rec_orig(int id, int64_t NF) { return id >= NF ? (int)(id - NF) : id;
 // pixel is smaller than the first's |signed distance|; else whichever is kept. Returns the record
 // id and depth of the candidate.
 MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, const FaceRec& r, float x, float y,
+                      float pad, float blur, bool persp, bool clipb, int& cid, float& pz);
+// The pixels of one lane's tile rectangle for a split face's triangle (k_tile_raster, rare path;
+// out of line so that its registers do not weigh on the pixel-pair loop).
+__attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
+                                                           const FaceRec* srec, const int* sid, const float* xs,
+                                                           const float* ys, unsigned long long* key, int lane,
+                                                           int prect, float pad, float blur, bool persp, bool clipb);
+MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, const FaceRec& r, float x, float y,
                       float pad, float blur, bool persp, bool clipb, int& cid, float& pz) {
   const bool second = id >= NF;
   const int oid = second ? (int)(id - NF) : (int)(id + NF);
@@ -1043,7 +1051,24 @@ MR_DEV FaceRec load_rec_if(const FaceRec* __restrict__ recs, bool c, int id) {
   return r;
 }
 
-template <int MODE, int CH>
+__attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
+                                                           const FaceRec* srec, const int* sid, const float* xs,
+                                                           const float* ys, unsigned long long* key, int lane,
+                                                           int prect, float pad, float blur, bool persp, bool clipb) {
+  const FaceRec r = srec[lane];
+  const int id = sid[lane];
+  for (int yy = (prect >> 6) & 7; yy <= ((prect >> 9) & 7); ++yy)
+    for (int xx = prect & 7; xx <= ((prect >> 3) & 7); ++xx) {
+      float pz;
+      int cid;
+      if (pair_keep(recs, NF, id, r, xs[xx], ys[yy], pad, blur, persp, clipb, cid, pz))
+        atomicMin(&key[yy * MR_TS + xx], frag_key(pz, (int)rec_code(cid, NF)));
+    }
+}
+
+// CLIP: near-plane clipping on (split faces may be present); the CLIP = false instantiation
+// carries none of their code, so the common launch keeps its register budget.
+template <int MODE, int CH, bool CLIP>
 __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 waves / SIMD: <= 96 VGPRs
   __shared__ WaveStage stage[4];
   const int lane = threadIdx.x & 63;
@@ -1113,7 +1138,7 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
 #pragma unroll 1
     for (int eb = 0; eb < U.z; eb += 64) {
       const int e = eb + lane;
-      int np = 0, meta = 0;
+      int np = 0, meta = 0, prect = 0;
       if (e < U.z) {
         int id;
         FaceRec r;
@@ -1128,7 +1153,7 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
         // of split faces, so there it covers both triangles of the pair
         float bx0 = r.xmin, bx1 = r.xmax, by0 = r.ymin, by1 = r.ymax;
         bool bvalid = (r.flags & FR_VALID) != 0;
-        if (ovf && (r.flags & FR_PAIR)) {
+        if (CLIP && ovf && (r.flags & FR_PAIR)) {
           const FaceRec ro = P.recs[P.NF + id];
           if (ro.flags & FR_VALID) {
             bx0 = bvalid ? smin(bx0, ro.xmin) : ro.xmin;
@@ -1146,9 +1171,13 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
         cy0 = cy0 > y0 ? cy0 : y0;
         cy1 = cy1 < y0 + MR_TS - 1 ? cy1 : y0 + MR_TS - 1;
         if (bvalid && cx0 <= cx1 && cy0 <= cy1) {
-          const int w = cx1 - cx0 + 1;
-          np = w * (cy1 - cy0 + 1);
-          meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
+          if (CLIP && (r.flags & FR_PAIR)) {  // a split face's triangle: its own per-lane loop after the passes
+            prect = 0x1000 | (cx0 - x0) | ((cx1 - x0) << 3) | ((cy0 - y0) << 6) | ((cy1 - y0) << 9);
+          } else {
+            const int w = cx1 - cx0 + 1;
+            np = w * (cy1 - cy0 + 1);
+            meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
+          }
         }
         S.rec[lane] = r;
         S.id[lane] = id;
@@ -1203,14 +1232,14 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
           const int lx = loc - ly * w;
           const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
           const FaceRec r = S.rec[m];
-          const int id = S.id[m];
           float pz;
-          int cid = id;
-          const bool keep = (r.flags & FR_PAIR)
-                                ? pair_keep(P.recs, P.NF, id, r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, cid, pz)
-                                : frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
-          if (keep) atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, (int)rec_code(cid, P.NF)));
+          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
+            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
         }
+      }
+      if (CLIP && __builtin_expect(__ballot(prect != 0) != 0ull, 0)) {
+        // near-plane split faces (rare): each such lane walks its rectangle, resolving the pair
+        if (prect) raster_pair_rect(P.recs, P.NF, S.rec, S.id, S.xs, S.ys, S.key, lane, prect, pad, blur, persp, clipb);
       }
       wave_lds_sync();  // the stage is rewritten by the next batch
       ACC(acc_pass);
@@ -1236,7 +1265,7 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
       const unsigned code = (unsigned)(k & 0xffffffffull);
       const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
       const bool hit = code != MR_NONE && px < W && py < H;
-      P.sface[(int64_t)slot * 64 + lane] = hit ? code_rec(code, P.NF) : -1;
+      P.sface[(int64_t)slot * 64 + lane] = hit ? (CLIP ? code_rec(code, P.NF) : (int)(code >> 1)) : -1;
     }
     wave_lds_sync();
     ACC(acc_emit);
@@ -1520,12 +1549,14 @@ static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipS
 
 // Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
 template <int MODE, int CH>
-static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st) {
+static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st, bool clip) {
   P.fill = 1;
-  static int rgrid = 0, sgrid = 0;
-  if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH>, 256, 7);
+  static int rgrid = 0, rgrid_c = 0, sgrid = 0;
+  if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH, false>, 256, 7);
+  if (!rgrid_c) rgrid_c = resident_grid(k_tile_raster<MODE, CH, true>, 256, 7);
   if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
-  MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH><<<rgrid, 256, 0, st>>>(P)));
+  if (clip) MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, true><<<rgrid_c, 256, 0, st>>>(P)));
+  else MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, false><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
   const int64_t slots_cap = N * (int64_t)g.T;
   int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
@@ -1820,30 +1851,27 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, F
   }
 }
 
-// Raster backward of a near-plane sub-triangle (record f, flag FR_CLIP): gradients w.r.t. the
-// ORIGINAL face's projected corners. g_orig: gradient w.r.t. the original-face barycentrics (what
-// the shading used); the sub-triangle's barycentrics are recomputed, the raster backward runs on
-// the sub-triangle with C g_orig, and the clip's chain rule maps the sub-corners (and the
-// conversion weights) back to the original corners, which are re-projected from the world corners.
-__attribute__((noinline)) __device__ void clipped_raster_bwd(const RenderBwdParams& P, const FaceRec& r, int f,
-                                                             const ViewRec& V, const float X[3][3], float px,
-                                                             float py, float gz, const float g_orig[3], float gd,
-                                                             float gfv[3][3]) {
+// Near-plane sub-triangle (record f, flag FR_CLIP): gfv holds the raster backward w.r.t. the
+// sub-triangle's corners (run with C g_orig); map it to the ORIGINAL face's projected corners
+// through the clip's chain rule (sub-corners and the conversion weights), the original corners
+// re-projected from the world corners. g_orig: gradient w.r.t. the original-face barycentrics.
+MR_DEV void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f, const ViewRec& V, const float X[3][3],
+                          float px, float py, const float g_orig[3], float gfv[3][3]) {
   const ClipRec cr = P.crec[f];
   FragEval e;
   eval_face(r, px, py, P.bbox_pad, P.blur, P.persp, P.clipb, e);
   const float bs[3] = {e.b0, e.b1, e.b2};
-  float gs[3], gsub[3][3];
-  clip_gb_sub(cr, g_orig, gs);
-  raster_bwd_pixel<true>(r, px, py, P.persp, P.clipb, gz, gs, gd, gsub);
-  float v[3][3];
+  float v[3][3], gsub[3][3];
   for (int c = 0; c < 3; ++c) {
     float vx, vy, vz, nx, ny;
     project_point(V, X[c], vx, vy, vz, nx, ny);
     v[c][0] = nx;
     v[c][1] = ny;
     v[c][2] = vz;
-    gfv[c][0] = gfv[c][1] = gfv[c][2] = 0.0f;
+    for (int q = 0; q < 3; ++q) {
+      gsub[c][q] = gfv[c][q];
+      gfv[c][q] = 0.0f;
+    }
   }
   clip_bwd_chain(cr, v, P.zc, P.persp != 0, bs, g_orig, gsub, gfv);
 }
@@ -1966,10 +1994,12 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       const float gt3[3] = {a3.z, a3.w, a4.x};
       float gfv[3][3];
       BACC(4);
-      if (r.flags & FR_CLIP)
-        clipped_raster_bwd(P, r, f, V, X, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), a0.x, gb, a0.y, gfv);
-      else
-        raster_bwd_pixel<true>(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.persp, P.clipb, a0.x, gb, a0.y, gfv);
+      const bool clipped = (r.flags & FR_CLIP) != 0;
+      const float pxf = col_ndc(px, P.H, P.W), pyf = row_ndc(py, P.H, P.W);
+      float gbr[3] = {gb[0], gb[1], gb[2]};
+      if (clipped) clip_gb_sub(P.crec[f], gb, gbr);  // near-plane sub-triangle: C g_orig
+      raster_bwd_pixel<true>(r, pxf, pyf, P.persp, P.clipb, a0.x, gbr, a0.y, gfv);
+      if (__builtin_expect(clipped, 0)) clipped_chain(P, r, f, V, X, pxf, pyf, gb, gfv);
       key = face;
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -2564,7 +2594,7 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
     MR_CHECK_LAUNCH("k_bin_fill_fv");
   }
   if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
-  return launch_raster_and_shade<0, 3>(P, g, N, st);
+  return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
 }
 
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
@@ -2793,8 +2823,8 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   else
     MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F, fpt)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
-  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st);
-  return launch_raster_and_shade<1, 3>(P, g, N, st);
+  if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
+  return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
 }
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {

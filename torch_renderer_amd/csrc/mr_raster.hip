@@ -1735,13 +1735,14 @@ MR_DEV float wave_sum_f_dpp(float x) {
 
 // Sum ACC-float rows over runs of equal `key` in lane order (segmented DPP scan; the
 // covered-pixel list is row-major, so a face's pixels along a row are consecutive lanes).
-// The run totals are staged in the wave's LDS rows and added with float atomics whose
-// lanes cover consecutive components of consecutive runs (contiguous 4*ACC-byte rows per
-// run instead of one scattered dword per lane and instruction). Lanes with key < 0 carry
-// zero rows. Uniform call (full EXEC). (Measured alternative: one LDS row per distinct face
-// filled with LDS float atomics — slower, 124 vs 102 us, the same-address LDS atomics serialise.)
+// seg_stage leaves the run totals in the wave's LDS rows and returns their count; seg_flush
+// adds them with float atomics whose lanes cover consecutive components of consecutive runs
+// (contiguous 4*ACC-byte rows per run instead of one scattered dword per lane and instruction).
+// Lanes with key < 0 carry zero rows. Uniform calls (full EXEC). (Measured alternative: one LDS
+// row per distinct face filled with LDS float atomics — slower, 124 vs 102 us, the same-address
+// LDS atomics serialise.)
 template <int ACC>
-MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float* lrow, int* lkey) {
+MR_DEV int seg_stage(int key, float (&v)[ACC], float* lrow, int* lkey) {
   const int lane = threadIdx.x & 63;
   const int prev = dpp_wave_shr1(key, -2);  // lane 0: no predecessor
   const bool head = lane == 0 || key != prev;
@@ -1758,7 +1759,11 @@ MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float
     for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
   }
   wave_lds_sync();
-  const int nt = __popcll(m);
+  return __popcll(m);
+}
+template <int ACC>
+MR_DEV void seg_flush(int nt, float* __restrict__ dst, const float* lrow, const int* lkey) {
+  const int lane = threadIdx.x & 63;
   for (int j = lane; j < nt * ACC; j += 64) {
     const int r = j / ACC;
     const float x = lrow[j];
@@ -1770,10 +1775,14 @@ MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float
   }
   wave_lds_sync();
 }
+template <int ACC>
+MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float* lrow, int* lkey) {
+  seg_flush<ACC>(seg_stage<ACC>(key, v, lrow, lkey), dst, lrow, lkey);
+}
 
-// The slot's 12 R/T partial sums (wave-wide DPP sums, fixed order: deterministic) written by
-// lanes 0..11 with one store instruction. Uniform call (full EXEC).
-MR_DEV void store_rt_partial(const float (&gR)[9], const float (&gT)[3], float* __restrict__ out, int lane) {
+// The slot's 12 R/T partial sums (wave-wide DPP sums, fixed order: deterministic), lane i
+// holding sum i (lanes 0..11); stored later by one store instruction. Uniform call (full EXEC).
+MR_DEV float rt_partial(const float (&gR)[9], const float (&gT)[3], int lane) {
   float o = 0.0f;
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -1781,7 +1790,7 @@ MR_DEV void store_rt_partial(const float (&gR)[9], const float (&gT)[3], float* 
     const float s = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
     o = lane == i ? s : o;
   }
-  if (lane < 12) out[lane] = o;
+  return o;
 }
 
 // Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
@@ -1909,6 +1918,8 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   FaceRec r_c;
   float g_c[5];
   bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
+  int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
+  float rt_prev = 0.0f;
 #ifdef MR_PROF
   unsigned long long pacc[7] = {0, 0, 0, 0, 0, 0, 0}, nit = 0;
   unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -1970,6 +1981,25 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     __builtin_amdgcn_sched_barrier(0);  // keep half 2's loads out of half 1's register peak
     // ---- half 2: raster + projection backward, per-face runs, R/T partials
     const ViewRec V = P.views[n];
+    // world corners (first 36 B of the ShadeRec), issued BEFORE the previous slot's deferred
+    // atomics: vmcnt retires in issue order, so a load issued after them would wait the
+    // atomics' ~3k-cycle completion; issued before, its wait is a precise count
+    float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0, w2 = w0;
+    const int face = f >= 0 ? (int)(rec_orig(f, P.NF) - n * P.F) : 0;
+    if (f >= 0) {
+      const float4* x4 = (const float4*)(P.srec + face);
+      w0 = x4[0];
+      w1 = x4[1];
+      w2 = x4[2];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
+    // half 1 and the corners above are already in flight or consumed
+    if (nt_prev >= 0) {
+      seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+      if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
+    }
+    __builtin_amdgcn_sched_barrier(0);
     float gR[9], gT[3];
 #pragma unroll
     for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
@@ -1980,12 +2010,9 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
     int key = -1;
     if (f >= 0) {
-      const int face = (int)(rec_orig(f, P.NF) - n * P.F);
       const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
       const float4 a3 = lrec[wave][3][lane];
       const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4* x4 = (const float4*)(P.srec + face);  // world corners X[9] = first 36 B
-      const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
       const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
       const float gb[3] = {a0.z, a0.w, a1.x};
       const float gP[3] = {a1.y, a1.z, a1.w};
@@ -2014,12 +2041,17 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       }
     }
     BACC(5);
-    seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
+    nt_prev = seg_stage<ACC>(key, row, lrow[wave], lkey[wave]);
+    rt_prev = rt_partial(gR, gT, lane);
+    s_prev = s;
     BACC(6);
-    store_rt_partial(gR, gT, P.rt_part + (int64_t)s * 12, lane);
 #ifdef MR_PROF
     ++nit;
 #endif
+  }
+  if (nt_prev >= 0) {
+    seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+    if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
   }
 #ifdef MR_PROF
   {

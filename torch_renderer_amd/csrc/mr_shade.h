@@ -74,9 +74,28 @@ struct TexTap {
   bool gx_ok, gy_ok;  // border-clip gradient pass-through
   int x0, y0;
 };
-MR_DEV float4 tex_fetch(const ShadeParams& S, int xc, int yc) {
-  if (xc < 0 || yc < 0 || xc >= S.tex_w || yc >= S.tex_h) return make_float4(0.f, 0.f, 0.f, 0.f);
-  return S.tex[(int64_t)(S.tex_h - 1 - yc) * S.tex_w + xc];  // torch.flip(maps, [H])
+// The four bilinear taps (x0|x0+1, y0|y0+1); out-of-range taps read as zero. The addresses are
+// clamped and all four loads issued unconditionally, then the values selected: written as
+// guarded loads, the compiler sinks each into its own branch with a load + wait per tap. The
+// empty asm consumes the loaded values unconditionally, so the loads cannot be sunk.
+MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b, float4& c, float4& d) {
+  const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
+  bool ok[4];
+  float4 v[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int xc = xs[i & 1], yc = ys[i >> 1];
+    ok[i] = (unsigned)xc < (unsigned)S.tex_w && (unsigned)yc < (unsigned)S.tex_h;
+    const int x = ok[i] ? xc : 0, y = ok[i] ? yc : S.tex_h - 1;
+    v[i] = S.tex[(int64_t)(S.tex_h - 1 - y) * S.tex_w + x];  // torch.flip(maps, [H])
+  }
+  asm volatile("" ::"v"(v[0].x), "v"(v[0].y), "v"(v[0].z), "v"(v[1].x), "v"(v[1].y), "v"(v[1].z), "v"(v[2].x),
+               "v"(v[2].y), "v"(v[2].z), "v"(v[3].x), "v"(v[3].y), "v"(v[3].z));
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  a = ok[0] ? v[0] : z;
+  b = ok[1] ? v[1] : z;
+  c = ok[2] ? v[2] : z;
+  d = ok[3] ? v[3] : z;
 }
 MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t) {
   const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
@@ -93,8 +112,8 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   const float nw = (x1 - ix) * (y1 - iy), ne = (ix - x0) * (y1 - iy);
   const float sw = (x1 - ix) * (iy - y0), se = (ix - x0) * (iy - y0);
-  const float4 a = tex_fetch(S, t.x0, t.y0), b = tex_fetch(S, t.x0 + 1, t.y0);
-  const float4 c = tex_fetch(S, t.x0, t.y0 + 1), d = tex_fetch(S, t.x0 + 1, t.y0 + 1);
+  float4 a, b, c, d;
+  tex_taps(S, t.x0, t.y0, a, b, c, d);
   out[0] = ((a.x * nw + b.x * ne) + c.x * sw) + d.x * se;
   out[1] = ((a.y * nw + b.y * ne) + c.y * sw) + d.y * se;
   out[2] = ((a.z * nw + b.z * ne) + c.z * sw) + d.z * se;
@@ -102,8 +121,8 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
 // d(texel)/d(u,v) contracted with g (3 channels) -> (gu, gv)
 MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[3], float& gu, float& gv) {
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
-  const float4 a = tex_fetch(S, t.x0, t.y0), b = tex_fetch(S, t.x0 + 1, t.y0);
-  const float4 c = tex_fetch(S, t.x0, t.y0 + 1), d = tex_fetch(S, t.x0 + 1, t.y0 + 1);
+  float4 a, b, c, d;
+  tex_taps(S, t.x0, t.y0, a, b, c, d);
   const float ga = (g[0] * a.x + g[1] * a.y) + g[2] * a.z;
   const float gb = (g[0] * b.x + g[1] * b.y) + g[2] * b.z;
   const float gc = (g[0] * c.x + g[1] * c.y) + g[2] * c.z;

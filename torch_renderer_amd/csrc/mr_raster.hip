@@ -1761,17 +1761,30 @@ MR_DEV int seg_stage(int key, float (&v)[ACC], float* lrow, int* lkey) {
   wave_lds_sync();
   return __popcll(m);
 }
+// Straight-line (unrolled, uniform skips): as a loop, the waitcnt pass drains every pending load
+// (s_waitcnt vmcnt(0)) in the loop preheader, i.e. waits on the prefetches issued just before.
 template <int ACC>
 MR_DEV void seg_flush(int nt, float* __restrict__ dst, const float* lrow, const int* lkey) {
-  const int lane = threadIdx.x & 63;
-  for (int j = lane; j < nt * ACC; j += 64) {
-    const int r = j / ACC;
-    const float x = lrow[j];
+  // lane id through an opaque copy: the unrolled blocks' row/column indices are invariant in the
+  // caller's slot loop, and hoisted out of it they would stay live across the whole loop
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int tot = nt * ACC;  // <= 64 * ACC
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) {
+    if (64 * i < tot) {
+      const int j = 64 * i + lane;
+      if (j < tot) {
+        const int r = j / ACC;
+        const float x = lrow[j];
 #ifndef MR_EXP_NOATOMIC
-    if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
+        if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
 #else
-    if (x == 1234.5f) dst[0] = x;  // experiment build: keep the reduction, drop the atomics
+        if (x == 1234.5f) dst[0] = x;  // experiment build: keep the reduction, drop the atomics
 #endif
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one row block at a time (no hoisting: register peak)
   }
   wave_lds_sync();
 }
@@ -1840,24 +1853,32 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // the wave's LDS instead of HBM (80 B written + 80 B read per covered pixel), and the slot,
 // winners and face record are fetched once. Peak VGPRs stay those of the larger half: the
 // LDS hand-off ends the first half's live ranges.
-// Face record and upstream gradients (depth, silhouette, RGB) of one slot pixel; zeros when the
-// pixel is uncovered or the slot is past the end (f < 0).
+// Face record and upstream gradients (depth, silhouette, RGB) of one slot pixel. The loads are
+// unconditional (record 0 / a zero buffer when the lane has no fragment or an output has no
+// gradient; such values are never used): written as guarded loads they become branches whose
+// phi copies wait on the load right away, which defeats the prefetch.
+__device__ float g_zero4[4];
 MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, FaceRec& r, float g[5]) {
-#pragma unroll
-  for (int i = 0; i < 5; ++i) g[i] = 0.0f;
-  if (f < 0) return;
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
-  r = P.recs[f];
-  if (P.gD) g[0] = P.gD[pix];
-  if (P.gS) g[1] = P.gS[pix];
-  if (P.gRGB) {
-    const float* c = P.gRGB + pix * P.rgb_ch;
-    g[2] = c[0];
-    g[3] = c[1];
-    g[4] = c[2];
-  }
+  r = P.recs[f < 0 ? 0 : f];
+  const float* pD = P.gD ? P.gD + pix : g_zero4;
+  const float* pS = P.gS ? P.gS + pix : g_zero4;
+  const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
+  g[0] = *pD;
+  g[1] = *pS;
+  g[2] = pC[0];
+  g[3] = pC[1];
+  g[4] = pC[2];
+}
+
+// A zero the compiler cannot see through, in a VGPR: a load indexed by it is a per-lane load
+// whose wait sits at the first use, not a scalar-ised load + readfirstlane waited on at once.
+MR_DEV int lane_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
 }
 
 // Near-plane sub-triangle (record f, flag FR_CLIP): gfv holds the raster backward w.r.t. the
@@ -1906,18 +1927,17 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   // Three-deep software pipeline (the kernel runs at 2 waves/SIMD, so a wave must hide its own
   // latency): while slot s is processed, the face record and upstream gradients of slot s + G
   // and the tile id and winner of slot s + 2G are in flight.
-  int gt_c = 0, f_c = -1, gt_n = 0, f_n = -1;
-  if (s < send) {
-    gt_c = P.stile[s];
-    f_c = P.sface[(int64_t)s * 64 + lane];
-  }
-  if (s + G < send) {
-    gt_n = P.stile[s + G];
-    f_n = P.sface[(int64_t)(s + G) * 64 + lane];
-  }
+  // gt_* are per-lane copies of the (uniform) tile id, made uniform where they are consumed
+  // Prefetches past the wave's last slot read a clamped (valid) slot and are never consumed.
+  const int lz = lane_zero();
+  const int slast = max(nslots - 1, 0);
+  int sc = min(s, slast);
+  int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
+  sc = min(s + G, slast);
+  int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
   FaceRec r_c;
   float g_c[5];
-  bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
+  bwd_slot_inputs(P, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
 #ifdef MR_PROF
@@ -1929,20 +1949,17 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
 #define BACC(i) do {} while (0)
 #endif
   for (; s < send; s += G) {
-    const int gt = gt_c, f = f_c;
+    const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c;
     const FaceRec r = r_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
     gt_c = gt_n;
     f_c = f_n;
-    bwd_slot_inputs(P, gt_c, f_c, lane, r_c, g_c);
-    gt_n = 0;
-    f_n = -1;
-    if (s + 2 * G < send) {
-      gt_n = P.stile[s + 2 * G];
-      f_n = P.sface[(int64_t)(s + 2 * G) * 64 + lane];
-    }
+    bwd_slot_inputs(P, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c);
+    sc = min(s + 2 * G, slast);
+    gt_n = P.stile[sc + lz];
+    f_n = P.sface[(int64_t)sc * 64 + lane];
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
     BACC(0);
@@ -1984,14 +2001,10 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
     // world corners (first 36 B of the ShadeRec), issued BEFORE the previous slot's deferred
     // atomics: vmcnt retires in issue order, so a load issued after them would wait the
     // atomics' ~3k-cycle completion; issued before, its wait is a precise count
-    float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0, w2 = w0;
+    // (unconditional: face 0 for lanes without a fragment, see bwd_slot_inputs)
     const int face = f >= 0 ? (int)(rec_orig(f, P.NF) - n * P.F) : 0;
-    if (f >= 0) {
-      const float4* x4 = (const float4*)(P.srec + face);
-      w0 = x4[0];
-      w1 = x4[1];
-      w2 = x4[2];
-    }
+    const float4* x4 = (const float4*)(P.srec + face);
+    const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
     __builtin_amdgcn_sched_barrier(0);
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed

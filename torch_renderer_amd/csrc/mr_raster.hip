@@ -576,21 +576,34 @@ __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float
   extern __shared__ __attribute__((aligned(16))) int hist[];
   __shared__ __attribute__((aligned(16))) float sfv[9 * 256 * MR_FV_FPT];
   __shared__ int first32[MR_FV_NMAX];
+#ifdef MR_EXP_FV_DIRECT
+  const FvBlock B = fv_block_setup(fv, Ftot, first, N, first32, sfv, false);
+#else
   const FvBlock B = fv_block_setup(fv, Ftot, first, N, first32, sfv, true);
+#endif
   const bool lds = LDS && B.n0 == B.n1;  // uniform over the workgroup
   if (lds) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
     __syncthreads();
   }
-  int mine = 0;
+  // entry totals: of the first mesh (mine) and, in a workgroup that straddles meshes, of the
+  // last (mine1) — one block-wide sum each; only meshes strictly inside the workgroup's face run
+  // (small meshes) take a per-face atomic. (Per-face atomics on the few total counters of a
+  // straddling workgroup serialise at the L2: they made this kernel 10x slower.)
+  int mine = 0, mine1 = 0;
   for (int k = 0; k < MR_FV_FPT; ++k) {
     const int64_t lf = (int64_t)k * blockDim.x + threadIdx.x;
     if (lf >= B.nf) break;
     const int64_t f = B.f0 + lf;
     const int n = fv_mesh(B, first32, first, N, f);
     float v[3][3];
+#ifdef MR_EXP_FV_DIRECT
+    for (int c = 0; c < 3; ++c)
+      for (int q = 0; q < 3; ++q) v[c][q] = fv[9 * f + 3 * c + q];
+#else
     for (int c = 0; c < 3; ++c)
       for (int q = 0; q < 3; ++q) v[c][q] = sfv[9 * lf + 3 * c + q];
+#endif
     FaceRec r2;
     const FaceRec r = build_records(P, f, (uint32_t)f, v, r2);
     P.recs[f] = r;
@@ -607,11 +620,16 @@ __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float
           }
       }
     }
-    if (lds) mine += m;
+    if (n == B.n0) mine += m;
+    else if (n == B.n1) mine1 += m;
     else if (m) atomicAdd(&P.vtot[n], m);
   }
+  block_add_256(mine, &P.vtot[B.n0]);  // also the barrier before the histogram flush
+  if (B.n1 != B.n0) {
+    __syncthreads();  // block_add_256's partials are reused
+    block_add_256(mine1, &P.vtot[B.n1]);
+  }
   if (lds) {
-    block_add_256(mine, &P.vtot[B.n0]);
     for (int i = threadIdx.x; i < P.T; i += blockDim.x)
       if (hist[i]) atomicAdd(&P.cnt[(int64_t)B.n0 * P.T + i], hist[i]);
   }
@@ -711,10 +729,13 @@ struct ScanParams {
 //  * the 64 keys of a slot that several units share start at EMPTY (they merge by atomicMin)
 //    and its count-down starts at units - 1 (the unit that takes it to -1 appends the pixels).
 #define MR_KEY_EMPTY ((0x7f800000ull << 32) | 0x7fffffffull)
+#define MR_SCAN_MULTI 4096  // multi-unit slots of one view whose keys the block initialises
 __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
   __shared__ int part[16];
   __shared__ long long red[16];
   __shared__ int base[2];
+  __shared__ int nmulti;
+  __shared__ int multi_slot[MR_SCAN_MULTI];
   const int n = blockIdx.x, t = threadIdx.x, lane = t & 63, wave = t >> 6;
   // vb = sum of vtot[m < n]
   long long s = 0;
@@ -755,6 +776,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
     base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
     P.vslot[n] = base[1];
     P.vslot[gridDim.x + n] = as;
+    nmulti = 0;
   }
   __syncthreads();
   // pass 2: units, slots, key init for shared slots
@@ -776,12 +798,20 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
     }
     if (nu > 1) {
       P.tdone[slot] = nu - 1;
-      for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
+      const int k = atomicAdd(&nmulti, 1);
+      if (k < MR_SCAN_MULTI) multi_slot[k] = slot;
+      else
+        for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
     }
     u0 += nu;
     slot += cc > 0 ? 1 : 0;
     ex += cc;
   }
+  // the 64 keys of every multi-unit slot, written by the whole block (a slot's 512 B by 64
+  // consecutive threads) instead of 64 serial stores by the tile's thread
+  __syncthreads();
+  const int nm = min(nmulti, MR_SCAN_MULTI);
+  for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
 }
 
 // ---------------------------------------------------------------------------
@@ -2623,7 +2653,11 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   FwdParams P = make_fwd(s, g, w, N, first, 0, Fb);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.view_count = count;
+#ifdef MR_EXP_FV_NOLDS
+  const bool lds = false;
+#else
   const bool lds = g.T <= MR_LDS_HIST;
+#endif
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   SP.NF = Fb;
   const int fvb = ceil_div(Ftot, 256 * MR_FV_FPT);

@@ -56,6 +56,18 @@ struct __attribute__((aligned(16))) FaceRec {
   uint32_t face;                             // mesh face index (into faces array)
 };
 enum : uint32_t { FR_VALID = 1u, FR_FAST = 2u, FR_CLIP = 4u, FR_PAIR = 8u };
+// Record load as four 16-B vector loads straight into registers (an aggregate copy through a
+// computed index may be lowered to a memcpy through scratch).
+MR_DEV FaceRec load_rec(const FaceRec* __restrict__ recs, int64_t id) {
+  const float4* q = (const float4*)(recs + id);
+  const float4 a = q[0], b = q[1], c = q[2], d = q[3];
+  FaceRec r;
+  r.x0 = a.x; r.y0 = a.y; r.z0 = a.z; r.x1 = a.w;
+  r.y1 = b.x; r.z1 = b.y; r.x2 = b.z; r.y2 = b.w;
+  r.z2 = c.x; r.area = c.y; r.xmin = c.z; r.xmax = c.w;
+  r.ymin = d.x; r.ymax = d.y; r.flags = __float_as_uint(d.z); r.face = __float_as_uint(d.w);
+  return r;
+}
 // FR_CLIP: the record is a sub-triangle of a face clipped at the near plane (its ClipRec holds
 // the barycentric conversion to the original face). FR_PAIR: one of the two triangles a face
 // with one corner behind the plane is split into; record id rid (< NF) is the first, NF + rid the

@@ -272,6 +272,14 @@ MR_DEV void block_add_256(int v, int* dst) {
   }
 }
 
+// A zero the compiler cannot see through, in a VGPR: a load indexed by it is a per-lane load
+// whose wait sits at the first use, not a scalar-ised load + readfirstlane waited on at once.
+MR_DEV int lane_zero() {
+  int z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+}
+
 // Wave-local LDS hand-off (the 64 lanes of one wave write, then every lane reads). A wave's
 // LDS operations execute in program order, so a wavefront-scope fence (no instructions, a
 // compiler barrier) is all the ordering needed. A workgroup-scope fence here would emit
@@ -822,6 +830,19 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
 // (blur == 0, FR_FAST) the edge signs reject before any division: a pixel whose edge
 // functions do not all carry the area's strict sign has some w_i <= 0, hence c_i <= 0
 // (all z > 0), hence is not inside, hence eval_face rejects it too.
+// The cheap prefix of frag_keep (bbox, and on the fast path the edge signs): false only where
+// frag_keep is false too, so the pairs it passes are a superset of the kept fragments.
+MR_DEV bool frag_cand(const FaceRec& r, float x, float y, float pad, bool fast) {
+  if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) return false;
+  if (!fast) return true;
+  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
+  const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
+  const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
+  return r.area > 0.0f ? inp : inn;
+}
+
 MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur, bool persp, bool clipb,
                       bool fast, float& pz) {
   if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) return false;
@@ -955,6 +976,7 @@ struct WaveStage {
   int mark[64];  // pass-local: pair slot -> entry lane that starts there
   unsigned long long key[64];
   float xs[MR_TS], ys[MR_TS];
+  int queue[128];  // ring of candidate pairs: face lane << 6 | tile row << 3 | tile column
 };
 
 // Background values of every output (view-independent: a pixel without a face has zero
@@ -1068,18 +1090,6 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
   for (int c = gw; c < nchunks; c += G) fill_chunk<MODE, CH>(P, bg, c / cpv, c - (c / cpv) * cpv, vec);
 }
 
-MR_DEV FaceRec load_rec_if(const FaceRec* __restrict__ recs, bool c, int id) {
-  FaceRec r;
-  if (c) {
-    r = recs[id];
-  } else {
-    r.x0 = r.y0 = r.z0 = r.x1 = r.y1 = r.z1 = r.x2 = r.y2 = r.z2 = 0.0f;
-    r.area = r.xmin = r.xmax = r.ymin = r.ymax = 0.0f;
-    r.flags = 0u;
-    r.face = 0u;
-  }
-  return r;
-}
 
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
                                                            const FaceRec* srec, const int* sid, const float* xs,
@@ -1098,8 +1108,11 @@ __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __rest
 
 // CLIP: near-plane clipping on (split faces may be present); the CLIP = false instantiation
 // carries none of their code, so the common launch keeps its register budget.
+#ifndef MR_RASTER_WAVES
+#define MR_RASTER_WAVES 4  // waves / SIMD: 5 -> <= 96 VGPRs, 4 -> <= 128
+#endif
 template <int MODE, int CH, bool CLIP>
-__global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 waves / SIMD: <= 96 VGPRs
+__global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams P) {
   __shared__ WaveStage stage[4];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1136,13 +1149,18 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
   // u + 3Gp are in flight (unit records are wave-uniform scalar loads). Each link of the
   // unit -> list entry -> record chain so gets a whole unit of work to land in, and a unit
   // starts with its records in registers. (Overflow units fetch their records in the batch.)
-  const int4 z4 = make_int4(0, 0, 0, -1);
-  int4 U1 = ub + jw < ue ? P.units[ub + jw] : z4;
-  int4 U2 = ub + jw + Gp < ue ? P.units[ub + jw + Gp] : z4;
-  int4 U3 = ub + jw + 2 * Gp < ue ? P.units[ub + jw + 2 * Gp] : z4;
-  int id1 = ub + jw < ue && U1.y >= 0 && lane < U1.z ? P.list[U1.y + lane] : 0;
-  int id2 = ub + jw + Gp < ue && U2.y >= 0 && lane < U2.z ? P.list[U2.y + lane] : 0;
-  FaceRec r1 = load_rec_if(P.recs, ub + jw < ue && U1.y >= 0 && lane < U1.z, id1);
+  // The prefetches are unconditional loads of clamped (valid) indices whose results are only
+  // used when the unit / entry exists (guarded loads become branches whose phi copies wait on
+  // the load at once), and the unit records travel as per-lane copies made uniform where they
+  // are consumed (a uniform load is otherwise scalarised: load + readfirstlane + wait at issue).
+  const int lz = lane_zero();
+  const int ulast = max(ue - 1, 0);
+  int4 U1v = P.units[min(ub + jw, ulast) + lz];
+  int4 U2v = P.units[min(ub + jw + Gp, ulast) + lz];
+  int4 U3v = P.units[min(ub + jw + 2 * Gp, ulast) + lz];
+  int id1 = P.list[(ub + jw < ue && U1v.y >= 0 && lane < U1v.z) ? U1v.y + lane : 0];
+  int id2 = P.list[(ub + jw + Gp < ue && U2v.y >= 0 && lane < U2v.z) ? U2v.y + lane : 0];
+  FaceRec r1 = load_rec(P.recs, (ub + jw < ue && U1v.y >= 0 && lane < U1v.z) ? id1 : 0);
 #ifdef MR_PROF
   unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, npass = 0, nunit = 0;
   unsigned long long tp0 = __builtin_amdgcn_s_memtime();
@@ -1153,7 +1171,8 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
 #endif
 #pragma unroll 1
   for (int u = ub + jw; u < ue; u += Gp) {
-    const int4 U = U1;
+    const int4 U = make_int4(__builtin_amdgcn_readfirstlane(U1v.x), __builtin_amdgcn_readfirstlane(U1v.y),
+                             __builtin_amdgcn_readfirstlane(U1v.z), __builtin_amdgcn_readfirstlane(U1v.w));
     const int id0 = id1;
     const int n = U.x / P.T, t = U.x - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
@@ -1163,7 +1182,6 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
     S.key[lane] = MR_KEY_EMPTY;
     S.mark[lane] = -1;
     const bool ovf = U.y < 0;
-    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
     wave_lds_sync();
 #pragma unroll 1
     for (int eb = 0; eb < U.z; eb += 64) {
@@ -1172,7 +1190,8 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
       if (e < U.z) {
         int id;
         FaceRec r;
-        if (ovf) {
+        if (ovf) {  // (the view's first record loaded here: a load hoisted to the unit's start is waited on there)
+          const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
           id = (int)(vfirst + e);
           r = P.recs[id];
         } else {  // a listed unit has <= 64 entries: its records are already here
@@ -1213,12 +1232,12 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
         S.id[lane] = id;
       }
       if (eb == 0) {  // advance the pipeline (after this unit's records are consumed)
-        r1 = load_rec_if(P.recs, u + Gp < ue && U2.y >= 0 && lane < U2.z, id2);
+        r1 = load_rec(P.recs, (u + Gp < ue && U2v.y >= 0 && lane < U2v.z) ? id2 : 0);
         id1 = id2;
-        U1 = U2;
-        id2 = u + 2 * Gp < ue && U3.y >= 0 && lane < U3.z ? P.list[U3.y + lane] : 0;
-        U2 = U3;
-        U3 = u + 3 * Gp < ue ? P.units[u + 3 * Gp] : z4;
+        U1v = U2v;
+        id2 = P.list[(u + 2 * Gp < ue && U3v.y >= 0 && lane < U3v.z) ? U3v.y + lane : 0];
+        U2v = U3v;
+        U3v = P.units[min(u + 3 * Gp, ulast) + lz];
       }
       // pair numbering
       ACC(acc_load);
@@ -1232,6 +1251,24 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
       S.meta[lane] = meta | pexcl;
+      // Two phases: every pass runs the cheap test (bbox + edge signs) on 64 (face, pixel) pairs
+      // and appends the candidates to the wave's LDS ring; whenever 64 candidates are queued a
+      // full wave evaluates them exactly (divisions, perspective correction, depth) and merges
+      // the keys. Evaluated in place, a pass would run the exact path whenever any one lane of
+      // it needed it, i.e. almost always, for ~20-30% useful lanes.
+      int qhead = 0, qtail = 0;  // ring positions (wave-uniform)
+      auto eval_queued = [&](int cnt) {
+        wave_lds_sync();
+        if (lane < cnt) {
+          const int pk = S.queue[(qhead + lane) & 127];
+          const int m = pk >> 6, sy = (pk >> 3) & 7, sx = pk & 7;
+          const FaceRec r = S.rec[m];
+          float pz;
+          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
+            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
+        }
+        qhead += cnt;
+      };
 #pragma unroll 1
       for (int pb = 0; pb < NP; pb += 64) {
 #ifdef MR_PROF
@@ -1249,6 +1286,8 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
         if (lane == 0) m = straddle;
         m = wave_incl_max(m);
         const int q = pb + lane;
+        bool cand = false;
+        int pk = 0;
         if (q < NP) {
           // one (face, pixel) pair per lane
           const int mt = S.meta[m];
@@ -1262,11 +1301,15 @@ __global__ void __launch_bounds__(256, 5) k_tile_raster(FwdParams P) {  // 5 wav
           const int lx = loc - ly * w;
           const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
           const FaceRec r = S.rec[m];
-          float pz;
-          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
-            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
+          cand = frag_cand(r, S.xs[sx], S.ys[sy], pad, fast_ok && (r.flags & FR_FAST));
+          pk = (m << 6) | (sy << 3) | sx;
         }
+        const unsigned long long cb = __ballot(cand);
+        if (cand) S.queue[(qtail + __popcll(cb & ((1ull << lane) - 1ull))) & 127] = pk;
+        qtail += __popcll(cb);
+        if (qtail - qhead >= 64) eval_queued(64);
       }
+      if (qtail > qhead) eval_queued(qtail - qhead);
       if (CLIP && __builtin_expect(__ballot(prect != 0) != 0ull, 0)) {
         // near-plane split faces (rare): each such lane walks its rectangle, resolving the pair
         if (prect) raster_pair_rect(P.recs, P.NF, S.rec, S.id, S.xs, S.ys, S.key, lane, prect, pad, blur, persp, clipb);
@@ -1892,7 +1935,7 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, F
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
-  r = P.recs[f < 0 ? 0 : f];
+  r = load_rec(P.recs, f < 0 ? 0 : f);
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + pix : g_zero4;
   const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
@@ -1901,14 +1944,6 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, F
   g[2] = pC[0];
   g[3] = pC[1];
   g[4] = pC[2];
-}
-
-// A zero the compiler cannot see through, in a VGPR: a load indexed by it is a per-lane load
-// whose wait sits at the first use, not a scalar-ised load + readfirstlane waited on at once.
-MR_DEV int lane_zero() {
-  int z;
-  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-  return z;
 }
 
 // Near-plane sub-triangle (record f, flag FR_CLIP): gfv holds the raster backward w.r.t. the

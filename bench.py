@@ -126,13 +126,18 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
 
 # Forward fragment pass (everything from projected geometry to the three images): API-minimum
 # bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
-FORWARD_KERNELS = ("k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
-                   "k_shade<1>")
+FORWARD_KERNELS = ("k_setup_zero", "k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill",
+                   "k_tile_raster", "k_shade<1>")
 
 
-# SURVEY.md §8d API-minimum traffic of the whole fwd+bwd path per frame
-def path_bytes_per_frame(H, W, F, tex_texels, views):
-    return 96 * H * W + 108 * F + 12 * tex_texels / views
+# Minimum HBM traffic of the fused fwd+bwd step per frame: the three images written once (20 B/px:
+# depth, silhouette, rgb), the upstream gradients of the covered pixels read once (20 B each; the
+# backward never touches an uncovered pixel's gradient, its contribution is zero), the mesh in and
+# its vertex gradients out (108 B/face) and the texture read once (12 B/texel), amortised over the
+# views. (SURVEY §8d's 96 B/px also charged the modular path's fragment tensors, which the fused
+# path never materialises, and the gradients of every pixel.)
+def path_bytes_per_frame(H, W, F, tex_texels, views, covered):
+    return 20 * H * W + 20 * covered / views + 108 * F + 12 * tex_texels / views
 
 
 def main():
@@ -300,7 +305,7 @@ def main():
                 "frac": round(fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)} if fwd_us > 0 else None
     kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2),
                    "share": round(v[1] / sum(x[1] for x in kt.values()), 3)} for k, v in kt.items()}
-    pb = path_bytes_per_frame(H, W, Fn, d["texture_u8"].shape[0] * d["texture_u8"].shape[1], nv)
+    pb = path_bytes_per_frame(H, W, Fn, d["texture_u8"].shape[0] * d["texture_u8"].shape[1], nv, wstats["covered"])
     path_roof = {"bytes_per_frame": int(pb), "achieved": round(value * pb / 1e9, 1), "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": round(value * pb / 1e9 / HBM_PEAK_GBS, 4)}
     cpu = None

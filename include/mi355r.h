@@ -90,6 +90,11 @@ typedef struct mr_mesh {
   const int32_t* faces_uvs;  /* (F,3) */
   const float* tex_rgba;     /* (Ht,Wt,4) float, image row 0 first (flip done in-kernel) */
   int32_t tex_h, tex_w;
+  /* Optional (mr_render_forward only): when non-NULL the forward computes the vertex normals
+   * itself into vnormals_out (V,3) and their un-normalised sums into vraw_out (V,3), in its first
+   * launch, instead of reading `vnormals` (saves the separate mr_vertex_normals launch). */
+  float* vnormals_out;
+  float* vraw_out;
 } mr_mesh_t;
 
 const char* mr_last_error(void);

@@ -35,7 +35,7 @@ def test_all_header_symbols_exported(lib):
 
 
 def test_version_and_workspace_queries(lib):
-    assert lib.mr_version() == 2  # 2: mr_raster_settings_t gained clip_z / z_clip_value
+    assert lib.mr_version() == 3  # 2: mr_raster_settings_t gained clip_z / z_clip_value; 3: mr_mesh_t vnormals_out
     a = lib.mr_render_workspace(64, 5856, 512, 512, 0)
     b = lib.mr_render_workspace(8, 5856, 512, 512, 0)
     assert a > b > 0

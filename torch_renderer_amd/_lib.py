@@ -54,7 +54,8 @@ class MrMesh(ctypes.Structure):
                 ("F", ctypes.c_int64), ("vadj_ptr", ctypes.c_void_p), ("vadj", ctypes.c_void_p),
                 ("vnormals", ctypes.c_void_p), ("tex_kind", ctypes.c_int32), ("vcolors", ctypes.c_void_p),
                 ("verts_uvs", ctypes.c_void_p), ("faces_uvs", ctypes.c_void_p), ("tex_rgba", ctypes.c_void_p),
-                ("tex_h", ctypes.c_int32), ("tex_w", ctypes.c_int32)]
+                ("tex_h", ctypes.c_int32), ("tex_w", ctypes.c_int32), ("vnormals_out", ctypes.c_void_p),
+                ("vraw_out", ctypes.c_void_p)]
 
 
 # (name, restype, argtypes) — mirrors include/mi355r.h

@@ -61,14 +61,14 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade(unused)", "k_bwd_geom(unused)", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
-                                              "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd"};
+                                              "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -455,9 +455,20 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
 }
 
 template <bool LDS>
-__global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F, int fpt) {
+__global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F, int fpt, int nviews, ShadeParams S,
+                                                        ShadeRec* __restrict__ srec) {
   extern __shared__ __attribute__((aligned(16))) int hist[];
   const int n = blockIdx.y;
+  if (n == nviews) {  // extra row: the mesh's per-face ShadeRecs (k_setup_zero wrote the normals)
+    for (int k = 0; k < fpt; ++k) {
+      const int64_t f = ((int64_t)blockIdx.x * fpt + k) * blockDim.x + threadIdx.x;
+      if (f >= F) break;
+      ShadeRec R;
+      make_shade_rec(S, (uint32_t)f, R);
+      srec[f] = R;
+    }
+    return;
+  }
   const int64_t f0 = (int64_t)blockIdx.x * fpt * blockDim.x + threadIdx.x;
   // q = 0: the face instance's record; q = 1: the second triangle of a split face (FR_PAIR)
   auto rec_q = [&](int64_t f, int q, FaceRec& r) -> bool {
@@ -1368,21 +1379,26 @@ __global__ void __launch_bounds__(256) k_shade_rec(ShadeParams S, int64_t F, Sha
   out[f] = R;
 }
 
-// k_shade_rec plus the binning counters' clear in one launch (the fused forward's first kernel):
-// blocks [0, ceil(F/256)) pack ShadeRecs, the rest zero `nzero` ints (per-tile counts, view
-// totals, work counters) with coalesced vector stores — replaces a separate memset.
-__global__ void __launch_bounds__(256) k_shade_rec_zero(ShadeParams S, int64_t F, ShadeRec* __restrict__ out,
-                                                        int* __restrict__ zero, int64_t nzero) {
-  const int64_t fb = (F + 255) / 256;
-  if ((int64_t)blockIdx.x < fb) {
-    const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
-    ShadeRec R;
-    make_shade_rec(S, (uint32_t)f, R);
-    out[f] = R;
+MR_DEV void vertex_normal(const float* __restrict__ verts, const int32_t* __restrict__ faces,
+                          const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj, int64_t v,
+                          float* __restrict__ vn, float* __restrict__ vraw);
+
+// The fused forward's first kernel: blocks [0, vb) compute the vertex normals (one thread per
+// vertex, as k_vertex_normals; vb = 0 when the caller passed them), the rest zero `nzero` ints
+// (per-tile counts, view totals, work counters) with coalesced stores — one launch instead of a
+// normals launch + a memset. The ShadeRecs, which need the normals, are packed by extra blocks
+// of the binning fill launch (k_bin_fill_world row N).
+__global__ void __launch_bounds__(256) k_setup_zero(const float* __restrict__ verts, int64_t V,
+                                                    const int32_t* __restrict__ faces, const int32_t* __restrict__ ptr,
+                                                    const int32_t* __restrict__ adj, float* __restrict__ vn,
+                                                    float* __restrict__ vraw, int64_t vb, int* __restrict__ zero,
+                                                    int64_t nzero) {
+  if ((int64_t)blockIdx.x < vb) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (v < V) vertex_normal(verts, faces, ptr, adj, v, vn, vraw);
     return;
   }
-  const int64_t base = ((int64_t)blockIdx.x - fb) * 1024;
+  const int64_t base = ((int64_t)blockIdx.x - vb) * 1024;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int64_t i = base + k * 256 + threadIdx.x;
@@ -1417,25 +1433,31 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   const int64_t HW = (int64_t)P.H * P.W;
   int s0, G, send;
   xcd_slot_range(nslots, wave, s0, G, send);
-  // slot s + G's tile and winners are loaded while slot s is processed
-  int gt_n = 0, f_n = -1;
-  if (s0 < send) {
-    gt_n = P.stile[s0];
-    f_n = P.sface[(int64_t)s0 * 64 + lane];
-  }
+  // Two-deep pipeline: while slot s is processed, the winners' face records of slot s + G and
+  // the tile and winners of slot s + 2G are in flight (unconditional loads of clamped indices;
+  // the tile id as a per-lane copy made uniform at use — see k_bwd_fused).
+  const int lz = lane_zero();
+  const int slast = max(nslots - 1, 0);
+  int sc = min(s0, slast);
+  int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
+  sc = min(s0 + G, slast);
+  int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
+  FaceRec r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
   for (int s = s0; s < send; s += G) {
-    const int gt = gt_n;
-    const int f = f_n;
-    if (s + G < send) {
-      gt_n = P.stile[s + G];
-      f_n = P.sface[(int64_t)(s + G) * 64 + lane];
-    }
+    const int gt = __builtin_amdgcn_readfirstlane(gt_c);
+    const int f = f_c;
+    const FaceRec r = r_c;
+    gt_c = gt_n;
+    f_c = f_n;
+    r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
+    sc = min(s + 2 * G, slast);
+    gt_n = P.stile[sc + lz];
+    f_n = P.sface[(int64_t)sc * 64 + lane];
     if (f < 0) continue;
     const int n = gt / P.T, t = gt - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
     const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
     const int64_t q = n * HW + (int64_t)py * P.W + px;
-    const FaceRec r = P.recs[f];
     const int fo = rec_orig(f, P.NF);  // the original face instance
     PixGeom G;
     if (MODE == 1) load_geom(P.srec, (uint32_t)(fo - n * P.F), G);  // in parallel with the record
@@ -2199,7 +2221,13 @@ __global__ void __launch_bounds__(256) k_vertex_normals(const float* __restrict_
                                                         const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                                                         float* __restrict__ vn, float* __restrict__ vraw) {
   const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
+  if (v < V) vertex_normal(verts, faces, ptr, adj, v, vn, vraw);
+}
+// verts_normals_packed for vertex v: the sum of its faces' (unnormalised) normals in CSR order
+// (the reference's index_add order), then F.normalize.
+MR_DEV void vertex_normal(const float* __restrict__ verts, const int32_t* __restrict__ faces,
+                          const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj, int64_t v,
+                          float* __restrict__ vn, float* __restrict__ vraw) {
   float s[3] = {0.f, 0.f, 0.f};
   for (int e = ptr[v]; e < ptr[v + 1]; ++e) {
     float nf[3];
@@ -2606,7 +2634,7 @@ int32_t mr_debug_set_prof(void* buf) {
 }
 #endif
 
-int32_t mr_version(void) { return 2; }
+int32_t mr_version(void) { return 3; }
 
 int32_t mr_struct_size(int32_t which) {
   switch (which) {
@@ -2920,10 +2948,17 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.rgb = rgb;
   P.p2f32 = p2f32;
   const int64_t nzero = (int64_t)(zero_bytes(N, g) / sizeof(int));
-  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec_zero<<<(unsigned)(ceil_div(m->F, 256) + ceil_div(nzero, 1024)), 256, 0, st>>>(P.S, m->F, w.srec, w.cnt, nzero)));
-  MR_CHECK_LAUNCH("k_shade_rec_zero");
+  // normals computed here (the mesh's vnormals_out) or passed in (vnormals)
+  const int64_t vb = (sp->light_kind == 0 && m->vnormals_out) ? ceil_div(m->V, 256) : 0;
+  if (vb) {
+    if (!m->vraw_out) return set_err(MR_EINVAL, "vnormals_out without vraw_out");
+    P.S.vnormals = m->vnormals_out;
+  }
+  MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.cnt, nzero)));
+  MR_CHECK_LAUNCH("k_setup_zero");
   const int fpt = MR_BIN_FPT;
   dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);
+  dim3 fgrid(sgrid.x, (unsigned)N + 1);  // + the ShadeRec row
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   if (lds)
@@ -2933,9 +2968,9 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   MR_CHECK_LAUNCH("k_bin_count_world");
   if ((rc = launch_scan(w, N, g, nullptr, m->F, st))) return rc;
   if (lds)
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<sgrid, 256, shm, st>>>(SP, m->F, fpt)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<fgrid, 256, shm, st>>>(SP, m->F, fpt, (int)N, P.S, w.srec)));
   else
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<sgrid, 256, 0, st>>>(SP, m->F, fpt)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<fgrid, 256, 0, st>>>(SP, m->F, fpt, (int)N, P.S, w.srec)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
   if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
   return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);

@@ -319,12 +319,14 @@ class RenderViews(torch.autograd.Function):
         N = views.shape[0]
         H, W = cfg.H, cfg.W
         vn = raw = None
-        if cfg.light_kind == 0:
-            vn, raw = _vertex_normals(v, f, vptr, vadj)
+        if cfg.light_kind == 0:  # computed by the forward's first launch (mesh.vnormals_out)
+            vn, raw = torch.empty_like(v), torch.empty_like(v)
         cc = cam_centers.float().contiguous().reshape(-1, 3)
         rs = cfg.raster_struct()
         sp = cfg.shade_struct()
         mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol)
+        if vn is not None:
+            mesh.vnormals_out, mesh.vraw_out = vn.data_ptr(), raw.data_ptr()
         depth = torch.empty((N, H, W), device=dev) if cfg.want_depth else None
         sil = torch.empty((N, H, W), device=dev) if cfg.want_sil else None
         rgb = torch.empty((N, H, W, cfg.rgb_channels), device=dev) if cfg.want_rgb else None

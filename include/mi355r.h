@@ -73,7 +73,11 @@ typedef struct mr_shade_params {
   int32_t rgb_channels;      /* 3 (rgb) or 4 (rgba, alpha = 1 - prod(1 - prob)) */
 } mr_shade_params_t;
 
-enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4 };
+enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
+       /* with MR_OUT_RGB, mr_shade_fragments_* only: upstream hard_rgb_blend (HardPhongShader) —
+        * the nearest fragment's Phong colour or the background, alpha = 1 where a face covers the
+        * pixel; gradients reach the colour of the nearest fragment only */
+       MR_OUT_HARD = 8 };
 
 /* One triangle mesh shared by all N views (Meshes.extend(N)). */
 typedef struct mr_mesh {
@@ -202,6 +206,23 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* mesh, const float* vnormals
                                     void* stream);
 
 /* ---------------- instrumentation ---------------- */
+
+/* camera_pose_optimizer.py:257-276 Model.calc_loss fused: sil_loss =
+ * L1Loss(sil, mask), hloss = HuberLoss(delta)(depth[mask], depth_ref[mask]), color_loss =
+ * MSELoss(rgb, rgb_ref); out[4] = {sil_loss + hloss + w_color * color_loss, sil_loss, hloss,
+ * color_loss} (device). All inputs hold npix = N*H*W pixels; rgb may be an RGBA view
+ * (rgb_stride 4); mask is a bool (uint8) tensor. Deterministic (fixed-order reductions). The
+ * backward writes dL/d{depth, sil, rgb (npix,3)} given the device scalar dL/dtotal and the
+ * forward's workspace. */
+size_t mr_pose_loss_workspace(int64_t npix);
+int32_t mr_pose_loss_forward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
+                             const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
+                             float delta, float w_color, float* out, void* ws, size_t ws_bytes, void* stream);
+int32_t mr_pose_loss_backward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
+                              const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
+                              float delta, float w_color, const float* g_total, const void* fwd_ws,
+                              float* g_depth, float* g_sil, float* g_rgb, void* stream);
+
 /* Work counters left in `workspace` by the last mr_render_forward / mr_rasterize_meshes that used it
  * (same N, total faces, H, W, max_faces_per_bin). Synchronises `stream`; for benchmarks and tools.
  * out[0] = (tile, face) list entries, out[1] = raster work units, out[2] = non-empty 8x8 tiles,

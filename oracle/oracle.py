@@ -379,6 +379,18 @@ def softmax_rgb_blend(colors, p2f, zbuf, dists, sigma, gamma, bg, znear=1.0, zfa
     return torch.cat([rgb, (1.0 - alpha)[..., None]], dim=-1)
 
 
+def hard_rgb_blend(colors, p2f, bg):
+    """upstream blending.py hard_rgb_blend (PyTorch3D >= 0.5; HardPhongShader, myrenderer.py:88):
+    the nearest fragment's colour where a face covers the pixel, the background elsewhere;
+    alpha = ~is_background. Restated from the published source as recalled (no copy here to check
+    against; parity unpinned beyond this restatement)."""
+    is_bg = p2f[..., 0] < 0
+    bgc = torch.as_tensor(bg, dtype=colors.dtype)
+    rgb = torch.where(is_bg[..., None], bgc.expand(colors[..., 0, :].shape), colors[..., 0, :])
+    alpha = (~is_bg).to(colors.dtype)[..., None]
+    return torch.cat([rgb, alpha], dim=-1)
+
+
 def sigmoid_alpha(p2f, dists, sigma):
     mask = p2f >= 0
     prob = torch.sigmoid(-dists / sigma) * mask

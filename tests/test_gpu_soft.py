@@ -15,8 +15,8 @@ from oracle import oracle as O
 from tests.helpers import canonical_views, mesh_arrays, report
 from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
 from torch_renderer_amd.cameras import PerspectiveCameras
-from torch_renderer_amd.mesh_renderer import (BlendParams, Fragments, Materials, PointLights, SoftPhongShader,
-                                              SoftSilhouetteShader)
+from torch_renderer_amd.mesh_renderer import (BlendParams, Fragments, HardPhongShader, Materials, PointLights,
+                                              SoftPhongShader, SoftSilhouetteShader)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -29,7 +29,7 @@ def _leaf(t):
 
 @pytest.mark.parametrize("K", [1, 3, 8, 50])
 @pytest.mark.parametrize("texture", ["vertex", "uv"])
-@pytest.mark.parametrize("shader", ["phong", "silhouette"])
+@pytest.mark.parametrize("shader", ["phong", "silhouette", "hard"])
 def test_hip_shader_on_oracle_fragments(K, texture, shader):
     H, W, N = 40, 48, 2
     name = "teapot" if texture == "vertex" else "cow"
@@ -62,6 +62,9 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
     if shader == "phong":
         colors = O.phong_colors(local, ba, vr, faces, texels, light, mat, cc)
         out_ref = O.softmax_rgb_blend(colors, p2f, zb, di, 1e-4, 1e-4, bg)
+    elif shader == "hard":  # HardPhongShader: hard_rgb_blend of the same Phong colours
+        colors = O.phong_colors(local, ba, vr, faces, texels, light, mat, cc)
+        out_ref = O.hard_rgb_blend(colors, p2f, bg)
     else:
         sil = O.sigmoid_alpha(p2f, di, 1e-4)
         out_ref = torch.cat([torch.ones(sil.shape + (3,)), sil[..., None]], -1)
@@ -80,20 +83,26 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
     cams = PerspectiveCameras(device=DEV, R=torch.eye(3)[None], T=-cc @ torch.eye(3))
     blend = BlendParams(sigma=1e-4, gamma=1e-4, background_color=bg)
     frags = Fragments(p2f.to(DEV), zg, bgp, dg)
-    if shader == "phong":
+    if shader in ("phong", "hard"):
         lights = PointLights(location=[light["location"]], ambient_color=[light["ambient"]],
                              diffuse_color=[light["diffuse"]], specular_color=[light["specular"]])
         mats = Materials(ambient_color=[mat["ambient"]], diffuse_color=[mat["diffuse"]],
                          specular_color=[mat["specular"]], shininess=mat["shininess"])
-        out = SoftPhongShader(device=DEV, cameras=cams, lights=lights, materials=mats, blend_params=blend)(frags, meshes)
+        cls = SoftPhongShader if shader == "phong" else HardPhongShader
+        out = cls(device=DEV, cameras=cams, lights=lights, materials=mats, blend_params=blend)(frags, meshes)
     else:
         out = SoftSilhouetteShader(blend_params=blend)(frags, meshes, cameras=cams)
     tag = f"K={K} {texture} {shader}"
     report(f"{tag} rgba", out, out_ref)
     (out * go.to(DEV)).sum().backward()
-    report(f"{tag} grad dists", dg.grad, di.grad)
-    if shader == "phong":
-        report(f"{tag} grad zbuf", zg.grad, zb.grad)
+    if shader == "hard":  # no depth / distance dependence
+        assert not zg.grad.any() and not dg.grad.any()
+        assert zb.grad is None or not zb.grad.any()
+    else:
+        report(f"{tag} grad dists", dg.grad, di.grad)
+    if shader in ("phong", "hard"):
+        if shader == "phong":
+            report(f"{tag} grad zbuf", zg.grad, zb.grad)
         report(f"{tag} grad bary", bgp.grad, ba.grad)
         report(f"{tag} grad verts", vg.grad, vr.grad)
         if texture == "vertex":

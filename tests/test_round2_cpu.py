@@ -177,3 +177,29 @@ def test_neighbor_rule_in_c_oracle():
     assert ((b[0] >= 0).sum(-1) <= 1).all()  # with it, never
     win = O.raster_fwd(fv, first, count, H, W, K=2, blur=1e-3, persp=True, window=(4, 9, 2, 7))
     assert torch.equal(win[0][:, 4:9, 2:7], a[0][:, 4:9, 2:7]) and (win[0][:, :4] == -1).all()
+
+
+def test_hard_rgb_blend_oracle_known_answer():
+    """upstream hard_rgb_blend (HardPhongShader): nearest fragment's colour or background, alpha =
+    coverage; the oracle restatement on a 1x1x2 image with K = 2."""
+    colors = torch.tensor([[[[[0.1, 0.2, 0.3], [0.9, 0.9, 0.9]], [[0.4, 0.5, 0.6], [0.7, 0.7, 0.7]]]]])
+    p2f = torch.tensor([[[[3, 5], [-1, -1]]]])
+    out = O.hard_rgb_blend(colors, p2f, (1.0, 0.5, 0.25))
+    assert torch.equal(out, torch.tensor([[[[0.1, 0.2, 0.3, 1.0], [1.0, 0.5, 0.25, 0.0]]]]))
+
+
+def test_pose_loss_needs_device_tensors():
+    from torch_renderer_amd.losses import pose_loss
+
+    t = torch.zeros(1, 4, 4)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        pose_loss(t, t, torch.zeros(1, 4, 4, 3), t > 0, t, torch.zeros(1, 4, 4, 3))
+
+
+def test_hard_phong_shader_is_exported_and_routed_to_fragments():
+    import torch_renderer_amd as T
+    from torch_renderer_amd.mesh_renderer import HardPhongShader, _shade_config
+
+    assert T.HardPhongShader is HardPhongShader
+    cfg = _shade_config(HardPhongShader(), None, 8, 8, {})
+    assert cfg.hard and cfg.want_rgb and not cfg.want_sil

@@ -9,4 +9,4 @@ from .transforms import (quaternion_to_matrix, matrix_to_quaternion, look_at_vie
 __version__ = "0.1.0"
 from .mesh_renderer import (RasterizationSettings, MeshRasterizer, MeshRenderer, Fragments, rasterize,  # noqa: F401
                             PointLights, AmbientLights, Materials, BlendParams, SoftPhongShader,
-                            SoftSilhouetteShader)
+                            SoftSilhouetteShader, HardPhongShader)

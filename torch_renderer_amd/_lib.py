@@ -23,6 +23,7 @@ c_i32_p = ctypes.POINTER(ctypes.c_int32)
 MR_OUT_DEPTH = 1
 MR_OUT_SIL = 2
 MR_OUT_RGB = 4
+MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
 
 
 class MrView(ctypes.Structure):
@@ -94,6 +95,11 @@ _SIGS = [
     ("mr_shade_fragments_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _VP, _VP, _VP, _I64, _I32, _I32, _I32,
                                            _VP, _I64, ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _SZ, _VP, _VP,
                                            _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
+    ("mr_pose_loss_workspace", _SZ, [_I64]),
+    ("mr_pose_loss_forward", _I32, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float, _VP,
+                                    _VP, _SZ, _VP]),
+    ("mr_pose_loss_backward", _I32, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float, _VP,
+                                     _VP, _VP, _VP, _VP, _VP]),
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_timing_enable", _I32, [_I32]),
     ("mr_timing_read", _I32, [_VP, _VP, _I32]),

@@ -2407,6 +2407,7 @@ struct FragShadeParams {
   int N, H, W, K;
   int64_t F;   // faces of the shared mesh; p2f holds packed ids n*F + f
   int sil;     // 1: sigmoid_alpha_blend (rgb = 1); 0: Phong + softmax_rgb_blend
+  int hard;    // 1 (with sil = 0): Phong + hard_rgb_blend (HardPhongShader)
   const int64_t* p2f;
   const float* zbuf;
   const float* bary;
@@ -2491,6 +2492,21 @@ __global__ void __launch_bounds__(256) k_frag_shade_fwd(FragShadeParams P) {
   const int64_t HW = (int64_t)P.H * P.W;
   if (pix >= (int64_t)P.N * HW) return;
   const int n = (int)(pix / HW);
+  if (P.hard) {  // hard_rgb_blend: the nearest fragment (k = 0) or the background
+    const int64_t f = P.p2f[pix * P.K];
+    float4 o = make_float4(P.S.bg[0], P.S.bg[1], P.S.bg[2], 0.0f);
+    if (f >= 0) {
+      PixGeom G;
+      load_geom(P.srec, (uint32_t)(f - (int64_t)n * P.F), G);
+      const float* b = P.bary + 3 * (pix * P.K);
+      float col[3];
+      PhongCache C;
+      phong_fwd(P.S, n, G, b[0], b[1], b[2], col, C);
+      o = make_float4(col[0], col[1], col[2], 1.0f);
+    }
+    ((float4*)P.rgba)[pix] = o;
+    return;
+  }
   FragSums R;
   frag_sums(P, pix, n, R, true);
   const float alpha = R.nzero ? 0.0f : R.alpha_nz;
@@ -2521,7 +2537,9 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
   FragSums R;
   float4 g4 = make_float4(0.f, 0.f, 0.f, 0.f);
   float g_num[3] = {0.f, 0.f, 0.f}, g_den = 0.0f, g_zmax = 0.0f, g_alpha = 0.0f;
-  if (act) {
+  if (act && P.hard) {
+    g4 = ((const float4*)P.g_rgba)[pix];  // alpha (coverage) has no gradient
+  } else if (act) {
     frag_sums(P, pix, n, R, true);
     g4 = ((const float4*)P.g_rgba)[pix];
     g_alpha = -g4.w;  // A = 1 - alpha
@@ -2556,7 +2574,44 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
 #pragma unroll
     for (int q = 0; q < ACC; ++q) row[q] = 0.0f;
     int key = -1;
-    if (f >= 0) {
+    if (f >= 0 && P.hard) {
+      // hard_rgb_blend: only the nearest fragment's colour carries a gradient; no depth / dists
+      float gb[3] = {0.f, 0.f, 0.f};
+      if (k == 0) {
+        const int face = (int)(f - (int64_t)n * P.F);
+        PixGeom G;
+        load_geom(P.srec, (uint32_t)face, G);
+        const float* b = P.bary + 3 * base;
+        float col[3];
+        PhongCache C;
+        phong_fwd(S, n, G, b[0], b[1], b[2], col, C);
+        const float gcol[3] = {g4.x, g4.y, g4.z};
+        float gP[3], gNn[3], gtex[3], guv[2];
+        phong_bwd(S, G, C, gcol, gb, gP, gNn, gtex, guv);
+        key = face;
+        for (int c = 0; c < 3; ++c)
+          for (int q = 0; q < 3; ++q) {
+            row[3 * c + q] = b[c] * gP[q];
+            row[9 + 3 * c + q] = b[c] * gNn[q];
+            if (ACC == 27) row[18 + 3 * c + q] = b[c] * gtex[q];
+          }
+        if (S.tex_kind == 2) {
+          if (P.gmap) tex_map_bwd(S, C.tap, gtex, P.gmap);
+          if (P.guv) {
+            const int32_t* fu = S.faces_uvs + 3 * (int64_t)face;
+            for (int c = 0; c < 3; ++c) {
+              if (guv[0] != 0.0f) atomicAdd(&P.guv[2 * (int64_t)fu[c]], b[c] * guv[0]);
+              if (guv[1] != 0.0f) atomicAdd(&P.guv[2 * (int64_t)fu[c] + 1], b[c] * guv[1]);
+            }
+          }
+        }
+      }
+      P.g_zbuf[base + k] = 0.0f;
+      P.g_dists[base + k] = 0.0f;
+      P.g_bary[3 * (base + k)] = gb[0];
+      P.g_bary[3 * (base + k) + 1] = gb[1];
+      P.g_bary[3 * (base + k) + 2] = gb[2];
+    } else if (f >= 0) {
       const float d = P.dists[base + k];
       const float prob = frag_prob(d, isig);
       const float one_m = 1.0f - prob;
@@ -2619,6 +2674,123 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
     if (!P.sil && S.light_kind == 0) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     else if (ACC == 27 && !P.sil) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Fused pose-optimiser loss (camera_pose_optimizer.py:257-276 Model.calc_loss):
+//   sil_loss   = L1Loss()(silhouette, mask)               mean over all pixels
+//   hloss      = HuberLoss(delta)(depth[mask], depth_ref[mask])   mean over the masked pixels
+//   color_loss = MSELoss()(color, rgb_ref)                mean over all pixels x 3
+//   total      = sil_loss + hloss + w_color * color_loss
+// Forward: per-block partial sums (fixed-order wave / block reductions), then one block sums the
+// partials in block order (deterministic). Backward: the elementwise gradients of the three
+// means, scaled by the device scalar dL/dtotal (no host read).
+// ---------------------------------------------------------------------------
+struct PoseLossParams {
+  const float* depth;
+  const float* sil;
+  const float* rgb;
+  int64_t rgb_stride;  // floats between consecutive pixels' colours (3, or 4 for an RGBA view)
+  const uint8_t* mask;
+  const float* depth_ref;
+  const float* rgb_ref;  // (npix, 3)
+  int64_t npix;
+  float delta, w_color;
+};
+#define MR_LOSS_BLOCKS 512
+
+MR_DEV float huber_val(float d, float delta) {
+  const float a = fabsf(d);
+  return a < delta ? 0.5f * d * d : delta * (a - 0.5f * delta);
+}
+MR_DEV float huber_grad(float d, float delta) {
+  return fabsf(d) < delta ? d : (d > 0.0f ? delta : (d < 0.0f ? -delta : 0.0f));
+}
+MR_DEV float block_sum_256(float v, float* sm) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float t = ((sm[0] + sm[1]) + sm[2]) + sm[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ void __launch_bounds__(256) k_pose_loss_partial(PoseLossParams P, float* __restrict__ part,
+                                                           int* __restrict__ pcnt) {
+  __shared__ float sm[4];
+  float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
+  int cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
+    const bool m = P.mask[i] != 0;
+    s_l1 += fabsf(P.sil[i] - (m ? 1.0f : 0.0f));
+    if (m) {
+      s_h += huber_val(P.depth[i] - P.depth_ref[i], P.delta);
+      ++cnt;
+    }
+    const float* c = P.rgb + i * P.rgb_stride;
+    const float* r = P.rgb_ref + 3 * i;
+    const float d0 = c[0] - r[0], d1 = c[1] - r[1], d2 = c[2] - r[2];
+    s_mse += (d0 * d0 + d1 * d1) + d2 * d2;
+  }
+  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), c = block_sum_256(s_mse, sm);
+  const float n = block_sum_256((float)cnt, sm);  // exact: <= 2^24 pixels per block
+  if (threadIdx.x == 0) {
+    part[3 * blockIdx.x] = a;
+    part[3 * blockIdx.x + 1] = b;
+    part[3 * blockIdx.x + 2] = c;
+    pcnt[blockIdx.x] = (int)n;
+  }
+}
+
+// out: {total, sil_loss, hloss, color_loss}; count: the number of masked pixels (backward)
+__global__ void __launch_bounds__(256) k_pose_loss_final(PoseLossParams P, const float* __restrict__ part,
+                                                         const int* __restrict__ pcnt, int nb, float* __restrict__ out,
+                                                         int64_t* __restrict__ count) {
+  __shared__ float sm[4];
+  float a = 0.0f, b = 0.0f, c = 0.0f;
+  long long n = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    a += part[3 * i];
+    b += part[3 * i + 1];
+    c += part[3 * i + 2];
+    n += pcnt[i];
+  }
+  a = block_sum_256(a, sm);
+  b = block_sum_256(b, sm);
+  c = block_sum_256(c, sm);
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  __shared__ long long sn[4];
+  if ((threadIdx.x & 63) == 0) sn[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long tn = ((sn[0] + sn[1]) + sn[2]) + sn[3];
+    const float l1 = a / (float)P.npix;
+    const float hl = b / (float)tn;  // an empty mask gives NaN, as torch's mean of nothing
+    const float ms = c / (float)(3 * P.npix);
+    out[0] = (l1 + hl) + P.w_color * ms;
+    out[1] = l1;
+    out[2] = hl;
+    out[3] = ms;
+    *count = tn;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pose_loss_bwd(PoseLossParams P, const float* __restrict__ g_total,
+                                                       const int64_t* __restrict__ count, float* __restrict__ g_depth,
+                                                       float* __restrict__ g_sil, float* __restrict__ g_rgb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P.npix) return;
+  const float g = *g_total;
+  const bool m = P.mask[i] != 0;
+  const float e = P.sil[i] - (m ? 1.0f : 0.0f);
+  g_sil[i] = g * ((e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f)) / (float)P.npix);
+  g_depth[i] = m ? g * (huber_grad(P.depth[i] - P.depth_ref[i], P.delta) / (float)*count) : 0.0f;
+  const float s = g * P.w_color * (2.0f / (float)(3 * P.npix));
+  const float* c = P.rgb + i * P.rgb_stride;
+  const float* r = P.rgb_ref + 3 * i;
+  g_rgb[3 * i] = s * (c[0] - r[0]);
+  g_rgb[3 * i + 1] = s * (c[1] - r[1]);
+  g_rgb[3 * i + 2] = s * (c[2] - r[2]);
 }
 
 // ---------------------------------------------------------------------------
@@ -2925,6 +3097,7 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   rc = check_mesh(m, sp);
   if (rc) return rc;
   if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
+  if (sp->out_flags & MR_OUT_HARD) return set_err(MR_EUNSUPPORTED, "hard_rgb_blend runs on the fragment-shader path (mr_shade_fragments_*)");
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if ((int64_t)N * m->F >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
   if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
@@ -3019,6 +3192,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   rc = check_mesh(m, sp);
   if (rc) return rc;
   if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
+  if (sp->out_flags & MR_OUT_HARD) return set_err(MR_EUNSUPPORTED, "hard_rgb_blend runs on the fragment-shader path (mr_shade_fragments_*)");
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
   if (!fws || !bws || !gverts || (!gviews && !(gRcv && gtcv))) return set_err(MR_EINVAL, "NULL argument");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
@@ -3108,6 +3282,7 @@ static FragShadeParams make_frag(const mr_mesh_t* m, const mr_shade_params_t* sp
   P.N = (int)N; P.H = H; P.W = W; P.K = K;
   P.F = m->F;
   P.sil = (sp->out_flags & MR_OUT_SIL) ? 1 : 0;
+  P.hard = (!P.sil && (sp->out_flags & MR_OUT_HARD)) ? 1 : 0;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = (const ShadeRec*)ws;
@@ -3263,5 +3438,59 @@ int32_t mr_timing_read(int32_t* launches, double* total_ms, int32_t n) {
 
 const char* mr_timing_kernel_name(int32_t k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : ""; }
 int32_t mr_timing_kernel_count(void) { return KID_COUNT; }
+
+static int pose_loss_params(PoseLossParams& P, const float* depth, const float* sil, const float* rgb,
+                            int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                            int64_t npix, float delta, float w_color) {
+  if (npix <= 0) return set_err(MR_EINVAL, "npix must be > 0");
+  if (!depth || !sil || !rgb || !mask || !depth_ref || !rgb_ref) return set_err(MR_EINVAL, "NULL loss input");
+  if (rgb_stride < 3) return set_err(MR_EINVAL, "rgb_stride must be >= 3");
+  if (!(delta > 0.0f)) return set_err(MR_EINVAL, "huber delta must be > 0");
+  P.depth = depth; P.sil = sil; P.rgb = rgb; P.rgb_stride = rgb_stride; P.mask = mask;
+  P.depth_ref = depth_ref; P.rgb_ref = rgb_ref; P.npix = npix; P.delta = delta; P.w_color = w_color;
+  return MR_OK;
+}
+
+size_t mr_pose_loss_workspace(int64_t npix) {
+  (void)npix;
+  return align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256) + 256;
+}
+
+int32_t mr_pose_loss_forward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
+                             const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
+                             float delta, float w_color, float* out, void* ws, size_t ws_bytes, void* stream) {
+  PoseLossParams P;
+  int rc = pose_loss_params(P, depth, sil, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
+  if (rc) return rc;
+  if (!out || !ws) return set_err(MR_EINVAL, "NULL output / workspace");
+  if (ws_bytes < mr_pose_loss_workspace(npix)) return set_err(MR_EWORKSPACE, "loss workspace too small");
+  char* w = (char*)ws;
+  float* part = (float*)w;
+  int* pcnt = (int*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256));
+  int64_t* count = (int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
+  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
+  hipStream_t st = (hipStream_t)stream;
+  k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
+  MR_CHECK_LAUNCH("k_pose_loss_partial");
+  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, out, count);
+  MR_CHECK_LAUNCH("k_pose_loss_final");
+  return MR_OK;
+}
+
+int32_t mr_pose_loss_backward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
+                              const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
+                              float delta, float w_color, const float* g_total, const void* fwd_ws,
+                              float* g_depth, float* g_sil, float* g_rgb, void* stream) {
+  PoseLossParams P;
+  int rc = pose_loss_params(P, depth, sil, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
+  if (rc) return rc;
+  if (!g_total || !fwd_ws || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL gradient argument");
+  const char* w = (const char*)fwd_ws;
+  const int64_t* count = (const int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) +
+                                          align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
+  k_pose_loss_bwd<<<(unsigned)ceil_div(npix, 256), 256, 0, (hipStream_t)stream>>>(P, g_total, count, g_depth, g_sil, g_rgb);
+  MR_CHECK_LAUNCH("k_pose_loss_bwd");
+  return MR_OK;
+}
 
 }  // extern "C"

@@ -243,6 +243,7 @@ class ShadeConfig:
     want_rgb: bool = True
     rgb_channels: int = 3
     want_p2f: bool = False  # also return the (N,H,W) int32 packed face ids (tests / tools)
+    hard: bool = False  # hard_rgb_blend (HardPhongShader): fragment-shader path only
     z_clip: float | None = None  # near clip plane (view z) of FoVPerspectiveCameras: znear / 2
 
     def raster_struct(self):
@@ -262,7 +263,7 @@ class ShadeConfig:
         sp.zfar = float(self.zfar)
         sp.sigma_sil = float(self.sigma_sil)
         sp.out_flags = ((_lib.MR_OUT_DEPTH if self.want_depth else 0) | (_lib.MR_OUT_SIL if self.want_sil else 0) |
-                        (_lib.MR_OUT_RGB if self.want_rgb else 0))
+                        (_lib.MR_OUT_RGB if self.want_rgb else 0) | (_lib.MR_OUT_HARD if self.hard else 0))
         sp.rgb_channels = int(self.rgb_channels)
         return sp
 
@@ -464,7 +465,7 @@ class ShadeFragments(torch.autograd.Function):
                               _padded_rgba(tex_map))
         mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol)
         sp = cfg.shade_struct()
-        sp.out_flags = _lib.MR_OUT_SIL if sil else _lib.MR_OUT_RGB
+        sp.out_flags = _lib.MR_OUT_SIL if sil else (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0))
         sp.rgb_channels = 4
         if sil:
             sp.light_kind = 1  # the silhouette blend reads no lighting (no vertex normals needed)
@@ -496,7 +497,7 @@ class ShadeFragments(torch.autograd.Function):
         tex = TextureArgs(ctx.tex_kind, e(vuv), e(fuv), e(rgba_map))
         mesh = _mesh_struct(v, f, vptr, vadj, e(vn), tex, e(vcol))
         sp = cfg.shade_struct()
-        sp.out_flags = _lib.MR_OUT_RGB if cfg.want_rgb else _lib.MR_OUT_SIL
+        sp.out_flags = (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0)) if cfg.want_rgb else _lib.MR_OUT_SIL
         sp.rgb_channels = 4
         if not cfg.want_rgb:
             sp.light_kind = 1

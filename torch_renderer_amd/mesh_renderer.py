@@ -235,8 +235,9 @@ def _shade_config(sh, cameras, H, W, kwargs):
         cfg.want_rgb = False
         cfg.want_sil = True
         return cfg
-    if not isinstance(sh, SoftPhongShader):
+    if not isinstance(sh, (SoftPhongShader, HardPhongShader)):
         raise NotImplementedError(f"shader {type(sh).__name__} is not implemented on the MI355X path")
+    cfg.hard = isinstance(sh, HardPhongShader)
     lights = kwargs.get("lights", sh.lights)
     mats = kwargs.get("materials", sh.materials)
     if isinstance(lights, AmbientLights):
@@ -325,6 +326,14 @@ class SoftPhongShader(_SoftShader):
     blur = 0 the fused one-launch render shades instead."""
 
 
+class HardPhongShader(_SoftShader):
+    """upstream mesh/shader.py HardPhongShader (myrenderer.py:88): phong_shading + hard_rgb_blend —
+    the nearest fragment's colour, the background elsewhere, alpha = 1 where a face covers the
+    pixel (PyTorch3D >= 0.5 `alpha = ~is_background`); on stored Fragments (HIP:
+    mr_shade_fragments_* with MR_OUT_HARD). Gradients reach the nearest fragment's colour
+    (bary, vertex positions / normals / colours, texture) only, as upstream's."""
+
+
 class SoftSilhouetteShader(_SoftShader):
     """upstream mesh/shader.py SoftSilhouetteShader: sigmoid_alpha_blend -> (1, 1, 1, alpha)."""
 
@@ -364,7 +373,7 @@ class MeshRenderer(torch.nn.Module):
         rs = kwargs.get("raster_settings", self.rasterizer.raster_settings)
         from .torch_renderer import textures_need_modular
 
-        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0 or (
+        if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0 or isinstance(self.shader, HardPhongShader) or (
                 isinstance(self.shader, SoftPhongShader) and textures_need_modular(meshes)):
             # soft rasterization, or a texture map that needs gradients: the HIP
             # raster, then the shader over the fragments (differentiable w.r.t. the map and uvs)

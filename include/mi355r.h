@@ -99,6 +99,11 @@ typedef struct mr_mesh {
    * launch, instead of reading `vnormals` (saves the separate mr_vertex_normals launch). */
   float* vnormals_out;
   float* vraw_out;
+  /* Optional: the same map as 8-bit texels, (Ht,Wt,4) u8, when every value of tex_rgba is exactly
+   * tex_lut[k] for some k (e.g. a PNG divided by 255): the samplers then read 4-B texels and
+   * convert through the 256-entry table, bitwise the same values at a quarter of the bytes. */
+  const uint8_t* tex_u8;
+  const float* tex_lut;      /* (256) f32, required with tex_u8 */
 } mr_mesh_t;
 
 const char* mr_last_error(void);

@@ -47,7 +47,7 @@ def test_pose_loss_matches_torch(shape, rgba_view):
     tot.backward()
     for name, a, b in (("total", tot, tot_r), ("sil", terms[0], terms_r[0]), ("huber", terms[1], terms_r[1]),
                        ("mse", terms[2], terms_r[2])):
-        a, b = float(a), float(b)
+        a, b = float(a.detach()), float(b.detach())
         print(f"[parity] pose_loss {name}: {a:.9g} vs torch {b:.9g}")
         assert abs(a - b) <= 1e-5 * max(abs(b), 1e-6), name
     report("pose_loss grad depth", dg.grad, dr_.grad, tol=1e-6)

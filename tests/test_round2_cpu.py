@@ -203,3 +203,19 @@ def test_hard_phong_shader_is_exported_and_routed_to_fragments():
     assert T.HardPhongShader is HardPhongShader
     cfg = _shade_config(HardPhongShader(), None, 8, 8, {})
     assert cfg.hard and cfg.want_rgb and not cfg.want_sil
+
+
+def test_u8_texture_copy_only_when_exact():
+    """TexturesUV.u8_map: an 8-bit copy is offered only when every texel is exactly float32(k)/255
+    (then the kernels' table lookup returns the identical floats); otherwise None (f32 texels)."""
+    g = torch.Generator().manual_seed(0)
+    u8 = torch.randint(0, 256, (16, 12, 3), generator=g, dtype=torch.uint8)
+    exact = u8.float() / 255.0
+    t = TexturesUV(maps=[exact], faces_uvs=[torch.zeros(1, 3, dtype=torch.long)], verts_uvs=[torch.zeros(1, 2)])
+    q, lut = t.u8_map(0)
+    assert q.dtype == torch.uint8 and q.shape == (16, 12, 4)
+    assert torch.equal(lut[q.long()][..., :3], exact) and not q[..., 3].any()
+    off = exact.clone()
+    off[3, 4, 1] = 0.5  # not k/255 for any k
+    t2 = TexturesUV(maps=[off], faces_uvs=[torch.zeros(1, 3, dtype=torch.long)], verts_uvs=[torch.zeros(1, 2)])
+    assert t2.u8_map(0) is None

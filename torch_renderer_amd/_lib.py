@@ -56,7 +56,7 @@ class MrMesh(ctypes.Structure):
                 ("vnormals", ctypes.c_void_p), ("tex_kind", ctypes.c_int32), ("vcolors", ctypes.c_void_p),
                 ("verts_uvs", ctypes.c_void_p), ("faces_uvs", ctypes.c_void_p), ("tex_rgba", ctypes.c_void_p),
                 ("tex_h", ctypes.c_int32), ("tex_w", ctypes.c_int32), ("vnormals_out", ctypes.c_void_p),
-                ("vraw_out", ctypes.c_void_p)]
+                ("vraw_out", ctypes.c_void_p), ("tex_u8", ctypes.c_void_p), ("tex_lut", ctypes.c_void_p)]
 
 
 # (name, restype, argtypes) — mirrors include/mi355r.h

@@ -3043,6 +3043,8 @@ static ShadeParams make_shade(const mr_mesh_t* m, const mr_shade_params_t* sp, c
   S.verts_uvs = m->verts_uvs;
   S.faces_uvs = m->faces_uvs;
   S.tex = (const float4*)m->tex_rgba;
+  S.tex8 = (m->tex_u8 && m->tex_lut) ? (const uchar4*)m->tex_u8 : nullptr;
+  S.tex_lut = m->tex_lut;
   S.tex_h = m->tex_h;
   S.tex_w = m->tex_w;
   S.light_kind = sp->light_kind;

@@ -26,6 +26,8 @@ struct ShadeParams {
   const float* verts_uvs;   // (Vt,2)
   const int32_t* faces_uvs; // (F,3)
   const float4* tex;        // (Ht,Wt) RGBA-padded, row 0 = first image row (unflipped)
+  const uchar4* tex8;       // optional 8-bit copy (value = tex_lut[u8]); read instead of tex
+  const float* tex_lut;
   int tex_h, tex_w;
   // lighting / materials
   int light_kind;  // 0 = point light, 1 = ambient only
@@ -82,12 +84,25 @@ MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b,
   const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
   bool ok[4];
   float4 v[4];
+  int64_t idx[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int xc = xs[i & 1], yc = ys[i >> 1];
     ok[i] = (unsigned)xc < (unsigned)S.tex_w && (unsigned)yc < (unsigned)S.tex_h;
     const int x = ok[i] ? xc : 0, y = ok[i] ? yc : S.tex_h - 1;
-    v[i] = S.tex[(int64_t)(S.tex_h - 1 - y) * S.tex_w + x];  // torch.flip(maps, [H])
+    idx[i] = (int64_t)(S.tex_h - 1 - y) * S.tex_w + x;  // torch.flip(maps, [H])
+  }
+  if (S.tex8) {  // 4-B texels, the exact values through the 256-entry table (L1-resident)
+    uchar4 u[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) u[i] = S.tex8[idx[i]];
+    asm volatile("" ::"v"(*(const int*)&u[0]), "v"(*(const int*)&u[1]), "v"(*(const int*)&u[2]),
+                 "v"(*(const int*)&u[3]));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = make_float4(S.tex_lut[u[i].x], S.tex_lut[u[i].y], S.tex_lut[u[i].z], 0.0f);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = S.tex[idx[i]];
   }
   asm volatile("" ::"v"(v[0].x), "v"(v[0].y), "v"(v[0].z), "v"(v[1].x), "v"(v[1].y), "v"(v[1].z), "v"(v[2].x),
                "v"(v[2].y), "v"(v[2].z), "v"(v[3].x), "v"(v[3].y), "v"(v[3].z));

@@ -274,6 +274,8 @@ class TextureArgs:
     verts_uvs: torch.Tensor | None = None
     faces_uvs: torch.Tensor | None = None
     tex_rgba: torch.Tensor | None = None  # (Ht,Wt,4) float32
+    tex_u8: torch.Tensor | None = None    # optional exact 8-bit copy (TexturesUV.u8_map)
+    tex_lut: torch.Tensor | None = None
 
 
 def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol):
@@ -292,6 +294,8 @@ def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol):
     m.tex_rgba = tex.tex_rgba.data_ptr() if tex.tex_rgba is not None else None
     if tex.tex_rgba is not None:
         m.tex_h, m.tex_w = int(tex.tex_rgba.shape[0]), int(tex.tex_rgba.shape[1])
+    if tex.tex_u8 is not None and tex.tex_lut is not None:
+        m.tex_u8, m.tex_lut = tex.tex_u8.data_ptr(), tex.tex_lut.data_ptr()
     return m
 
 

@@ -109,7 +109,23 @@ class TexturesUV:
             rgba = torch.zeros((Ht, Wt, 4), dtype=torch.float32, device=m.device)
             rgba[..., :min(C, 3)] = m[..., :3].float()
             self._rgba_cache = (key, rgba.contiguous())
+            self._u8_cache = None
         return self._rgba_cache[1]
+
+    def u8_map(self, i=0):
+        """(8-bit (Ht, Wt, 4) copy, (256,) f32 table) of rgba_map(i) when every value is exactly
+        table[k] = float32(k) / 255 for some k (a PNG read as uint8 / 255), else None. The samplers
+        then read 4-B texels, bitwise the same values. Checked once per map version (cached)."""
+        rgba = self.rgba_map(i)
+        if getattr(self, "_u8_cache", None) is not None and self._u8_cache[0] is rgba:
+            return self._u8_cache[1]
+        lut_cpu = torch.arange(256, dtype=torch.float32) / 255.0  # IEEE float32 division
+        lut = lut_cpu.to(rgba.device)
+        q = torch.round(rgba * 255.0).clamp(0, 255).to(torch.uint8)
+        exact = bool(torch.equal(lut[q.long()], rgba))
+        res = (q.contiguous(), lut) if exact else None
+        self._u8_cache = (rgba, res)
+        return res
 
 
 class Meshes:

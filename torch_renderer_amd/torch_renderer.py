@@ -31,7 +31,8 @@ def texture_args(meshes: Meshes, need_color: bool):
         raise ValueError("Meshes does not have textures")  # upstream Meshes.sample_textures
     if isinstance(tex, TexturesUV):
         vuv, fuv = tex.kernel_uvs(0)
-        return TextureArgs(2, vuv, fuv, tex.rgba_map(0)), None
+        u8 = tex.u8_map(0)
+        return TextureArgs(2, vuv, fuv, tex.rgba_map(0), *(u8 if u8 is not None else (None, None))), None
     if isinstance(tex, TexturesVertex):
         vc = tex.verts_features_list()[0]
         if vc.shape[-1] != 3:

@@ -13,6 +13,10 @@
 
 #define MR_KEPS_D 1e-8  // geometry_utils.h: `const auto kEpsilon = 1e-8;` (a double)
 #define MR_DEV __device__ __forceinline__
+// FMA contraction allowed inside shading / gradient arithmetic (tolerance-compared, never a raster
+// decision): the library builds with -ffp-contract=off so that every raster expression keeps the
+// CPU oracle's rounding, and these blocks opt back in.
+#define MR_FP_FAST _Pragma("clang fp contract(fast)")
 
 // Fast math for the shading and gradient arithmetic (never for raster decisions, pix_to_face,
 // zbuf, bary or dists, which stay IEEE and bit-exact with the CPU): 1-ulp hardware reciprocal,

@@ -1137,13 +1137,14 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const bool fast_ok = !(blur > 0.0f);
 #endif
   const int H = P.H, W = P.W;
-  // background chunks of this wave: c = gw, gw + G, ... < N * cpv, spread over its units
+  // background chunks of this wave: c = gw, gw + G, ... < N * cpv, written after its units (the
+  // waves that finish their raster work early stream the background while the others still run;
+  // chunks interleaved with the units measured 3 us slower, all chunks before them 20 us slower)
   const int gw = blockIdx.x * 4 + wave, G = gridDim.x * 4;
   const bool vec = (W & 3) == 0;
   const int64_t HW = (int64_t)H * W * (MODE == 0 ? P.K : 1);
   const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
   const int nchunks = P.fill ? P.N * cpv : 0;
-  const int my_chunks = gw < nchunks ? (nchunks - gw + G - 1) / G : 0;
   // XCD-aware unit partition: workgroups are dispatched round-robin over the 8 XCDs, so
   // blockIdx % 8 names this wave's XCD; each XCD's waves take a contiguous eighth of the
   // (view-major) units, which keeps the face records they gather in that XCD's L2.
@@ -1151,8 +1152,6 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const int jw = (blockIdx.x / parts) * 4 + wave, Gp = (gridDim.x / parts) * 4;
   const int Cp = (nunits + parts - 1) / parts;
   const int ub = (blockIdx.x % parts) * Cp, ue = ub + Cp < nunits ? ub + Cp : nunits;
-  const int my_units = ub + jw < ue ? (ue - ub - jw + Gp - 1) / Gp : 0;
-  const int per_unit = my_units > 0 ? (my_chunks + my_units - 1) / my_units : my_chunks;
   const Bg bg = background<MODE>(P);
   int chunk = gw;
   // Software pipeline over the wave's units u, u + Gp, u + 2Gp, ...: while unit u is
@@ -1252,12 +1251,6 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
       }
       // pair numbering
       ACC(acc_load);
-      if (eb == 0) {  // this unit's share of background chunks: they drain during the passes
-#pragma unroll 1
-        for (int j = 0; j < per_unit && chunk < nchunks; ++j, chunk += G)
-          fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
-        ACC(acc_fill);
-      }
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
@@ -2059,7 +2052,11 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
       FragEval e;
       float4 o[MR_BWD_REC];
+#ifdef MR_EXP_NOHALF1
+      if (false) {  // experiment build: no shading backward (half 2 gets zero records)
+#else
       if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
+#endif
         if (r.flags & FR_CLIP) clip_unconvert(P.crec[f], e.b0, e.b1, e.b2, e.b0, e.b1, e.b2);
         ShadeOut so;
         ShadeCache C;
@@ -2109,7 +2106,11 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
 #pragma unroll
     for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
     int key = -1;
+#ifdef MR_EXP_NOHALF2
+    if (false) {  // experiment build: no raster / projection backward
+#else
     if (f >= 0) {
+#endif
       const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
       const float4 a3 = lrec[wave][3][lane];
       const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);

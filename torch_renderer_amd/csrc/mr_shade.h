@@ -52,6 +52,7 @@ struct ShadeOut {
 
 // ---- F.normalize(x, eps=1e-6) forward/backward ----
 MR_DEV void normalize3(const float x[3], float y[3], float& nrm, float& den) {
+  MR_FP_FAST
   nrm = fsqrt(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]);
   den = smax(nrm, 1e-6f);
   const float r = frcp(den);
@@ -60,6 +61,7 @@ MR_DEV void normalize3(const float x[3], float y[3], float& nrm, float& den) {
   y[2] = x[2] * r;
 }
 MR_DEV void normalize3_bwd(const float x[3], float nrm, float den, const float g[3], float gx[3]) {
+  MR_FP_FAST
   const float r = frcp(den);
   const float gd = -((g[0] * x[0] + g[1] * x[1]) + g[2] * x[2]) * (r * r);
   const float gn = (nrm >= 1e-6f && nrm > 0.0f) ? gd * frcp(nrm) : 0.0f;
@@ -67,7 +69,10 @@ MR_DEV void normalize3_bwd(const float x[3], float nrm, float den, const float g
   gx[1] = g[1] * r + gn * x[1];
   gx[2] = g[2] * r + gn * x[2];
 }
-MR_DEV float dot3(const float a[3], const float b[3]) { return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]; }
+MR_DEV float dot3(const float a[3], const float b[3]) {
+  MR_FP_FAST
+  return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
 MR_DEV float sigmoidf_(float x) { return frcp(1.0f + fexp(-x)); }
 
 // ---- texture: grid_sample(bilinear, align_corners=True, border) on flipped map ----
@@ -113,6 +118,7 @@ MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b,
   d = ok[3] ? v[3] : z;
 }
 MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t) {
+  MR_FP_FAST
   const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
   float ix = ((gx + 1.0f) / 2.0f) * (float)(S.tex_w - 1);
   float iy = ((gy + 1.0f) / 2.0f) * (float)(S.tex_h - 1);
@@ -135,6 +141,7 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
 }
 // d(texel)/d(u,v) contracted with g (3 channels) -> (gu, gv)
 MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[3], float& gu, float& gv) {
+  MR_FP_FAST
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   float4 a, b, c, d;
   tex_taps(S, t.x0, t.y0, a, b, c, d);
@@ -225,6 +232,7 @@ MR_DEV void load_geom(const ShadeRec* __restrict__ recs, uint32_t face, PixGeom&
 
 // interpolate_face_attributes: sum_i b_i * attr_i
 MR_DEV float interp3(float b0, float b1, float b2, float a0, float a1, float a2) {
+  MR_FP_FAST
   return (b0 * a0 + b1 * a1) + b2 * a2;
 }
 
@@ -239,6 +247,7 @@ struct ShadeCache {
 // Forward shading of one pixel (hit = face found). b = bary (after clip), z, sd = signed dist.
 MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, float b0, float b1, float b2,
                       float z, float sd, ShadeOut& o, ShadeCache& C) {
+  MR_FP_FAST
   const float m = hit ? 1.0f : 0.0f;
   const float zb = hit ? z : -1.0f;    // zbuf background = -1
   const float dd = hit ? sd : -1.0f;   // dists background = -1
@@ -313,6 +322,7 @@ struct ShadeGrad {
 
 MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1, float b2, float z,
                       const ShadeCache& C, float gD, float gS, const float gRGB[3], float gA, ShadeGrad& R) {
+  MR_FP_FAST
   const float b[3] = {b0, b1, b2};
   R.gz = 0.0f;
   R.gsd = 0.0f;
@@ -602,6 +612,7 @@ MR_DEV void project_point(const ViewRec& V, const float X[3], float& vx, float& 
 // g_ndc (x, y, z=view z) at world point X -> g_view; then g_X = R g_view,
 // g_R += X (x) g_view, g_T += g_view.
 MR_DEV void project_bwd(const ViewRec& V, const float X[3], const float gn[3], float gX[3], float gR[9], float gT[3]) {
+  MR_FP_FAST
   const float vx = ((X[0] * V.R[0] + X[1] * V.R[3]) + X[2] * V.R[6]) + V.T[0];
   const float vy = ((X[0] * V.R[1] + X[1] * V.R[4]) + X[2] * V.R[7]) + V.T[1];
   const float vz = ((X[0] * V.R[2] + X[1] * V.R[5]) + X[2] * V.R[8]) + V.T[2];
@@ -628,6 +639,7 @@ struct PhongCache {
 
 MR_DEV void phong_fwd(const ShadeParams& S, int n, const PixGeom& G, float b0, float b1, float b2, float col[3],
                       PhongCache& C) {
+  MR_FP_FAST
   for (int k = 0; k < 3; ++k) {
     C.P[k] = interp3(b0, b1, b2, G.X[0][k], G.X[1][k], G.X[2][k]);
     C.amb[k] = S.mat_amb[k] * S.light_amb[k];
@@ -671,6 +683,7 @@ MR_DEV void phong_fwd(const ShadeParams& S, int n, const PixGeom& G, float b0, f
 // (gtex) and the interpolated uv (guv; UV textures).
 MR_DEV void phong_bwd(const ShadeParams& S, const PixGeom& G, const PhongCache& C, const float gcol[3], float gb[3],
                       float gP[3], float gNn[3], float gtex[3], float guv[2]) {
+  MR_FP_FAST
   for (int k = 0; k < 3; ++k) {
     gtex[k] = gcol[k] * (C.amb[k] + C.diff[k]);
     gP[k] = gNn[k] = 0.0f;

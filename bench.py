@@ -31,6 +31,15 @@ METRIC = "frames/sec fwd+bwd, 512×512, ~6k-face mesh, batch=64; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 
 
+def view_distance(mesh, verts):
+    """0.5 m for the cow; other meshes at the same distance relative to their extent
+    (the cow's 0.172 m), so the framing matches (dolphin 0.71 m -> 2.1 m)."""
+    if mesh == "cow":
+        return 0.5
+    ext = float((verts.max(0).values - verts.min(0).values).max())
+    return 0.5 * ext / 0.172
+
+
 def canonical_views(verts, n_total, H, W, dist_m=0.5, fov_deg=60.0, seed=0):
     """OpenCV look-at from 0.5 m to the centroid, azimuth 360*i/n,
     elevation ~U[-20, 60] deg (seeded), fx = fy for a 60 deg FoV, centred principal point."""
@@ -48,7 +57,7 @@ def canonical_views(verts, n_total, H, W, dist_m=0.5, fov_deg=60.0, seed=0):
     return R_cv, t_cv, K
 
 
-def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3):
+def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3, mesh="cow"):
     """Reference CPU path restated (oracle: C naive rasterizer + torch-CPU shading/autograd) on a
     bounded sample of the same workload: `n_views` frames, 1 warm-up + `reps` timed fwd+bwd passes
     on all host cores, then one view, one timed pass on 1 core."""
@@ -57,8 +66,10 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3):
     from oracle import oracle as O
     from torch_renderer_amd.transforms import opencv_to_pytorch3d
 
-    img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
-    tex = ("uv", torch.from_numpy(d["verts_uvs"]).float(), torch.from_numpy(d["faces_uvs"]).long(), img)
+    tex = None  # untextured meshes (dolphin, teapot): white, as the GPU path
+    if "texture_u8" in d:
+        img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
+        tex = ("uv", torch.from_numpy(d["verts_uvs"]).float(), torch.from_numpy(d["faces_uvs"]).long(), img)
     s = min(H, W) / 2.0
     intr1 = torch.tensor([[K[0, 0] / s, (W / 2.0 - K[0, 2]) / s, K[1, 1] / s, (H / 2.0 - K[1, 2]) / s]]).float()
     gen = torch.Generator().manual_seed(1)
@@ -96,7 +107,7 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3):
     O.set_threads(threads)
     return {"value": n_views / sec, "unit": "frames/s", "cores": threads, "kind": "port",
             "value_1core": round(1.0 / sec1, 4),
-            "sample": f"{n_views} views of the same workload (cow, {H}x{W}, fwd+bwd), 1 warm-up + {reps} timed "
+            "sample": f"{n_views} views of the same workload ({mesh}, {H}x{W}, fwd+bwd), 1 warm-up + {reps} timed "
                       f"passes, {sec:.2f} s/pass: C naive rasterizer (OpenMP {threads} threads) + torch-CPU "
                       f"shading/autograd ({tt} threads); 1 core: 1 view, 1 timed pass, {sec1:.2f} s"}
 
@@ -185,13 +196,13 @@ def main():
     faces = meshes.shared_faces()
     Fn = faces.shape[0]
     nv = args.views
-    R_all, t_all, K = canonical_views(verts0, nv * world, H, W)
+    R_all, t_all, K = canonical_views(verts0, nv * world, H, W, dist_m=view_distance(args.mesh, verts0))
     R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
     R_cv = R_cv.to(dev).contiguous().requires_grad_(True)
     t_cv = t_cv.to(dev).contiguous().requires_grad_(True)
     verts = meshes.shared_verts().clone().requires_grad_(True)
     tex = meshes.textures
-    if args.texture == "white":
+    if args.texture == "white" or tex is None:  # untextured meshes render white (drop-in default)
         from torch_renderer_amd.structures import TexturesVertex
         tex = TexturesVertex([torch.ones_like(verts).detach()])
     bmesh = Meshes([verts], [faces], tex).extend(nv)
@@ -305,18 +316,21 @@ def main():
                 "frac": round(fwd_bytes / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)} if fwd_us > 0 else None
     kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2),
                    "share": round(v[1] / sum(x[1] for x in kt.values()), 3)} for k, v in kt.items()}
-    pb = path_bytes_per_frame(H, W, Fn, d["texture_u8"].shape[0] * d["texture_u8"].shape[1], nv, wstats["covered"])
+    texels = d["texture_u8"].shape[0] * d["texture_u8"].shape[1] if "texture_u8" in d else 0
+    pb = path_bytes_per_frame(H, W, Fn, texels, nv, wstats["covered"])
     path_roof = {"bytes_per_frame": int(pb), "achieved": round(value * pb / 1e9, 1), "peak": HBM_PEAK_GBS,
                  "unit": "GB/s", "frac": round(value * pb / 1e9 / HBM_PEAK_GBS, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(verts0, faces.cpu(), d, R_all, t_all, K, H, W, n_views=args.cpu_views)
+        cpu = cpu_baseline(verts0, faces.cpu(), d, R_all, t_all, K, H, W, n_views=args.cpu_views, mesh=args.mesh)
     line = {
         "metric": METRIC, "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "launch": "eager" if args.eager else "hipgraph",
-        "data": "synthetic camera poses on the reference's cow mesh + texture (assets/cow.npz from data/cow_mesh)",
+        "data": (f"synthetic camera poses on the reference's {args.mesh} mesh"
+                 + (" + texture (assets/cow.npz from data/cow_mesh)" if "texture_u8" in d and args.texture == "uv"
+                    else " (white: no texture map)")),
         "config": {"workload": f"{args.mesh} (F={Fn}, V={verts0.shape[0]}), {H}x{W}, {nv} views/GPU, fwd+bwd: "
                                "depth+silhouette+Phong RGB from one raster pass, grads to verts and per-view R,t",
                    "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "global_views": nv * world,
@@ -350,7 +364,7 @@ def bench_fragments(args, dev, world, rank):
     faces = meshes.shared_faces()
     Fn = faces.shape[0]
     nv = args.views
-    R_all, t_all, K = canonical_views(verts.cpu(), nv * world, H, W)
+    R_all, t_all, K = canonical_views(verts.cpu(), nv * world, H, W, dist_m=view_distance(args.mesh, verts.cpu()))
     R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
     Rp, Tp = opencv_to_pytorch3d(R_cv.to(dev), t_cv.to(dev))
     cams = PerspectiveCameras(focal_length=((float(K[0, 0]), float(K[1, 1])),),

@@ -49,8 +49,8 @@ def main():
     _lib.check(L.mr_debug_set_prof(None))
     p = buf.cpu().numpy().view(np.uint64).reshape(nw, 8).astype(np.float64)
     p = p[p[:, 7] == 1]
-    print(f"waves {len(p)}; units/wave {st(p[:, 5])}; passes/wave {st(p[:, 4])}")
-    for i, nm in enumerate(["load", "passes", "emit", "fill", "", "", "total"]):
+    print(f"waves {len(p)}; units/wave {st(p[:, 5] % 65536)}; passes/wave {st(p[:, 5] // 65536)}")
+    for i, nm in enumerate(["load", "cheap", "emit", "fill", "exact", "", "total"]):
         if nm:
             print(f"  {nm:8s} cycles/wave {st(p[:, i])}")
 

@@ -1172,7 +1172,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   int id2 = P.list[(ub + jw + Gp < ue && U2v.y >= 0 && lane < U2v.z) ? U2v.y + lane : 0];
   FaceRec r1 = load_rec(P.recs, (ub + jw < ue && U1v.y >= 0 && lane < U1v.z) ? id1 : 0);
 #ifdef MR_PROF
-  unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, npass = 0, nunit = 0;
+  unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, acc_eval = 0, npass = 0, nunit = 0;
   unsigned long long tp0 = __builtin_amdgcn_s_memtime();
   const unsigned long long tstart = tp0;
 #define ACC(v) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); v += _t - tp0; tp0 = _t; } while (0)
@@ -1262,6 +1262,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
       // it needed it, i.e. almost always, for ~20-30% useful lanes.
       int qhead = 0, qtail = 0;  // ring positions (wave-uniform)
       auto eval_queued = [&](int cnt) {
+        ACC(acc_pass);
         wave_lds_sync();
         if (lane < cnt) {
           const int pk = S.queue[(qhead + lane) & 127];
@@ -1272,6 +1273,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
             atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
         }
         qhead += cnt;
+        ACC(acc_eval);
       };
 #pragma unroll 1
       for (int pb = 0; pb < NP; pb += 64) {
@@ -1357,7 +1359,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   if (g_prof && lane == 0) {
     unsigned long long* o = g_prof + (size_t)gw * 8;
     o[0] = acc_load; o[1] = acc_pass; o[2] = acc_emit; o[3] = acc_fill;
-    o[4] = npass; o[5] = nunit; o[6] = __builtin_amdgcn_s_memtime() - tstart; o[7] = 1;
+    o[4] = acc_eval; o[5] = npass * 65536 + nunit; o[6] = __builtin_amdgcn_s_memtime() - tstart; o[7] = 1;
   }
 #endif
 #undef ACC

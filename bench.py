@@ -117,7 +117,7 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3, mesh="
 # covered pixels). Device-side caches may serve part of it; rocprof FETCH/WRITE is reported
 # beside it as roofline.traffic.
 def algorithmic_bytes(kernel, H, W, F, views, st):
-    HW, cov, ent, slots = H * W, st["covered"], st["entries"], st["tiles"]
+    HW, cov, ent, slots, units = H * W, st["covered"], st["entries"], st["tiles"], st.get("units", 0)
     table = {
         # background of every pixel (depth + silhouette + rgb(3)), list ids, each face record once,
         # 64 winners per non-empty tile
@@ -131,6 +131,8 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
         "k_bwd_fused": (256 + 48) * slots + 20 * cov + (64 + 144 + 72) * F,
         "k_bin_count": 64 * F * views + 24 * F,            # face records out, mesh in
         "k_bin_fill": 64 * F * views + 4 * ent,            # face records in, list ids out
+        "k_bin_rect": (64 + 4) * F * views + 24 * F,       # face records + tile rectangles out, mesh in
+        "k_bin_view": 4 * F * views + 4 * ent + 16 * units,  # rectangles in, list ids + work units out
     }
     return table.get(kernel)
 
@@ -138,6 +140,7 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
 # Forward fragment pass (everything from projected geometry to the three images): API-minimum
 # bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
 FORWARD_KERNELS = ("k_setup_zero", "k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill",
+                   "k_bin_rect", "k_bin_view",
                    "k_tile_raster", "k_shade<1>")
 
 
@@ -343,7 +346,8 @@ def main():
         dist.destroy_process_group()
 
 
-FRAG_KERNELS = ("k_project_faces", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster", "k_shade<0>")
+FRAG_KERNELS = ("k_project_faces", "k_bin_count", "k_bin_scan", "k_bin_fill", "k_bin_rect", "k_bin_view", "k_tile_raster",
+                "k_shade<0>")
 
 
 def bench_fragments(args, dev, world, rank):

@@ -61,14 +61,15 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_BIN_RECT, KID_BIN_VIEW, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade(unused)", "k_bwd_geom(unused)", "k_rt_reduce",
                                               "k_vgrad_a", "k_vgrad_b",
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
-                                              "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero"};
+                                              "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero",
+                                              "k_bin_rect", "k_bin_view"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -108,8 +109,14 @@ __device__ unsigned long long* g_prof = nullptr;
   do {                                                                                   \
     if (g_prof && (threadIdx.x & 63) == 0) g_prof[(size_t)(gw) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// workgroup-level stamp (thread 0)
+#define PROF_B(gw, i)                                                                    \
+  do {                                                                                   \
+    if (g_prof && threadIdx.x == 0) g_prof[(size_t)(gw) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
 #else
 #define PROF_T(gw, i) do {} while (0)
+#define PROF_B(gw, i) do {} while (0)
 #endif
 
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
@@ -121,7 +128,8 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // per-view list of covered (pixel, face) pairs.
 // ---------------------------------------------------------------------------
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
-enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_COUNT = 4 };
+// ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_ENTRIES64 = 4, CTR_COUNT = 8 };
 
 struct BinGeom {
   int TX, TY, T;
@@ -147,9 +155,10 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
 
 struct RasterWS {
   FaceRec* recs;
-  int* cnt;    // (N*T) entries per tile; zeroed per call together with vtot and ctr
-  int* vtot;   // (N) list entries per view
-  int* ctr;    // (CTR_COUNT) units / slots emitted by the scan, covered pixels
+  int* ctr;    // (CTR_COUNT) units / slots emitted by the scan, covered pixels, entries (u64)
+  int* cnt;    // (N*T) entries per tile; zeroed per call together with ctr and vtot (count -> scan path)
+  int* vtot;   // (N) list entries per view (count -> scan path)
+  uint32_t* rects;  // (2 * Ftot) per record: tile rectangle (k_bin_view path)
   int* start;  // (N*T) entry offset of each tile inside its view's region
   int* cur;    // (N*T) fill cursors
   int* vbase;  // (N) first list entry of each view (saturating)
@@ -175,10 +184,12 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   // split at the near plane (only written for such faces)
   w.recs = (FaceRec*)(b + off);
   off = align_up(off + sizeof(FaceRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
-  w.cnt = (int*)(b + off);
+  w.ctr = (int*)(b + off);  // 256-B aligned: the u64 entry counter at ctr + CTR_ENTRIES64
+  w.cnt = w.ctr + CTR_COUNT;
   w.vtot = w.cnt + NT;
-  w.ctr = w.vtot + N;
   off = align_up(off + sizeof(int) * (NT + (size_t)N + CTR_COUNT), 256);
+  w.rects = (uint32_t*)(b + off);
+  off = align_up(off + sizeof(uint32_t) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.start = (int*)(b + off);
   off = align_up(off + sizeof(int) * NT, 256);
   w.cur = (int*)(b + off);
@@ -206,8 +217,10 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   w.bytes = off;
   return w;
 }
-static size_t zero_bytes(int64_t N, const BinGeom& g) {
-  return sizeof(int) * ((size_t)N * g.T + (size_t)N + CTR_COUNT);
+// Bytes to clear from w.ctr before a forward: the counters and, on the count -> scan path, the
+// per-tile counts and per-view totals.
+static size_t zero_bytes(int64_t N, const BinGeom& g, bool view_path) {
+  return sizeof(int) * (view_path ? (size_t)CTR_COUNT : (size_t)N * g.T + (size_t)N + CTR_COUNT);
 }
 
 // ---------------------------------------------------------------------------
@@ -228,6 +241,7 @@ struct SetupParams {
   int* list;
   int* vtot;
   const int* vbase;
+  uint32_t* rects;  // k_bin_view path: per-record tile rectangles
 };
 
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
@@ -831,6 +845,270 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
   __syncthreads();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
+}
+
+// ---------------------------------------------------------------------------
+// 1b. per-view binning (the common case: tile grids of <= MR_VIEW_TMAX tiles, <= 256 per side)
+// ---------------------------------------------------------------------------
+// k_bin_rect_* project the faces and write each record's 8x8-tile rectangle (4 bytes); one
+// 1024-thread workgroup per view (k_bin_view) then counts the view's tile lists in an LDS
+// histogram, scans them, emits the view's slots and work units, and fills the lists through LDS
+// cursors: count -> scan -> fill of one view never leaves the workgroup (no global per-tile
+// counters, no per-tile global atomics, one launch instead of two). List, slot and unit space
+// come from one atomic each per view; the raster result does not depend on their order.
+#define MR_VIEW_TMAX 16384              // LDS histogram: 64 KB
+#define MR_VIEW_FMAX 65536              // faces per view (mean) above which the count -> scan path is used
+#define MR_RECT_NONE 0x000000ffu        // tx0 = 255 > tx1 = 0: an empty rectangle
+#define MR_VIEW_RPT 8                   // rectangles per thread per chunk
+#ifndef MR_RECT_FPT
+#define MR_RECT_FPT 1                   // faces per thread of k_bin_rect_world
+#endif
+MR_DEV uint32_t rec_rect(const SetupParams& P, const FaceRec& r) {
+  int tx0, tx1, ty0, ty1;
+  if (!rec_tiles(P, r, tx0, tx1, ty0, ty1)) return MR_RECT_NONE;
+  return (uint32_t)tx0 | ((uint32_t)tx1 << 8) | ((uint32_t)ty0 << 16) | ((uint32_t)ty1 << 24);
+}
+
+MR_DEV void vertex_normal(const float* __restrict__ verts, const int32_t* __restrict__ faces,
+                          const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj, int64_t v,
+                          float* __restrict__ vn, float* __restrict__ vraw);
+// The fused forward's setup, world mode (the first launch of the per-view path): grid rows 1..N
+// project (face, view) pairs, one thread each; row 0, dispatched first (the CSR gathers are its
+// longest dependent chain), computes the vertex normals when the call asks for them (as
+// k_setup_zero does on the count -> scan path) and clears the work counters. The ShadeRecs, which
+// read the normals, are packed by extra workgroups of k_bin_view.
+// CLIP: near-plane clipping on (its sub-triangle code indexes corners dynamically: scratch);
+// the CLIP = false instantiation carries none of it.
+struct NormalsArgs {
+  int64_t V;
+  const int32_t* ptr;
+  const int32_t* adj;
+  float* vn;    // NULL: no normals to compute
+  float* vraw;
+};
+template <bool CLIP>
+__global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const float* __restrict__ verts,
+                                                        const int32_t* __restrict__ faces, int64_t F,
+                                                        const ViewRec* __restrict__ views, NormalsArgs NA,
+                                                        int* __restrict__ ctr) {
+  const int n = (int)blockIdx.y - 1;
+  if (n < 0) {
+    const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
+    if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < MR_RECT_FPT; ++k) {
+    const int64_t f = ((int64_t)blockIdx.x * MR_RECT_FPT + k) * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    float v[3][3];
+    world_face_verts(verts, faces, f, views[n], v);
+    const int64_t rid = (int64_t)n * F + f;
+    FaceRec r2;
+    const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
+    P.recs[rid] = r;
+    P.rects[rid] = rec_rect(P, r);
+    if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
+  }
+}
+
+// face_verts mode (record = packed face id): the workgroup's face_verts staged through LDS
+// with 16-B loads.
+template <bool CLIP>
+__global__ void __launch_bounds__(256) k_bin_rect_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot) {
+  __shared__ __attribute__((aligned(16))) float sfv[9 * 256];
+  const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
+  const int nf = (int)(Ftot - f0 < (int64_t)blockDim.x ? Ftot - f0 : (int64_t)blockDim.x);
+  const float4* src = (const float4*)(fv + 9 * f0);  // f0 % 256 == 0: 16-B aligned if fv is
+  const int n4 = ((uintptr_t)src & 15) == 0 ? 9 * nf / 4 : 0;
+  for (int i = threadIdx.x; i < n4; i += blockDim.x) ((float4*)sfv)[i] = src[i];
+  for (int i = 4 * n4 + threadIdx.x; i < 9 * nf; i += blockDim.x) sfv[i] = fv[9 * f0 + i];
+  __syncthreads();
+  if ((int)threadIdx.x >= nf) return;
+  const int64_t f = f0 + threadIdx.x;
+  float v[3][3];
+  for (int c = 0; c < 3; ++c)
+    for (int q = 0; q < 3; ++q) v[c][q] = sfv[9 * threadIdx.x + 3 * c + q];
+  FaceRec r2;
+  const FaceRec r = CLIP ? build_records(P, f, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
+  P.recs[f] = r;
+  P.rects[f] = rec_rect(P, r);
+  if (CLIP) P.rects[P.NF + f] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
+}
+
+struct ViewBinParams {
+  int T, TX, mfpb, clipz;
+  int nviews;
+  int ranges;  // write cnt / start per tile (read by k_raster_k, K > 1)
+  int64_t list_cap, NF;
+  const uint32_t* rects;
+  const int64_t* first;       // NULL: shared mode (view n's records are n*F + f)
+  const int64_t* view_count;  // NULL: shared mode (F faces per view)
+  int64_t F;
+  int* cnt;
+  int* start;
+  int* vbase;
+  int* tdone;
+  int* vslot;
+  int* stile;
+  int4* units;
+  int* ctr;
+  unsigned long long* tkey;
+  int* list;
+  // workgroups N.. pack the mesh's ShadeRecs (fused path; srec NULL otherwise)
+  ShadeParams S;
+  ShadeRec* srec;
+  int64_t Fs;
+};
+
+template <typename Fn>
+MR_DEV void rect_tiles(uint32_t r, int TX, Fn&& fn) {
+  const int tx0 = r & 255, tx1 = (r >> 8) & 255, ty0 = (r >> 16) & 255, ty1 = r >> 24;
+  for (int ty = ty0; ty <= ty1; ++ty)
+    for (int tx = tx0; tx <= tx1; ++tx) fn(ty * TX + tx);
+}
+
+__global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) {
+  extern __shared__ __attribute__((aligned(16))) int hist[];  // T (+ T/64 pad): counts, then fill cursors
+  __shared__ int part[16];
+  __shared__ long long base[3];
+  __shared__ int nmulti;
+  __shared__ int multi_slot[MR_SCAN_MULTI];
+  const int n = blockIdx.x, t = threadIdx.x;
+  if (n >= (int)P.nviews) {  // ShadeRec workgroups (they run on the CUs the views leave idle)
+    const int64_t f = (int64_t)(n - P.nviews) * 1024 + t;
+    if (f < P.Fs) {
+      ShadeRec R;
+      make_shade_rec(P.S, (uint32_t)f, R);
+      P.srec[f] = R;
+    }
+    return;
+  }
+  // tile tt lives at hist[tt + tt / 64] (the scan's per-thread runs of C tiles spread over the
+  // banks); a view's rectangles are read in chunks of MR_VIEW_RPT per thread, all loads of a
+  // chunk in flight together, and a view of one chunk keeps them in registers for the fill.
+  const int j = t;
+  PROF_B(60000 + n, 0);
+  const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
+  const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
+  for (int i = t; i < P.T + (P.T >> 6); i += 1024) hist[i] = 0;
+  if (t == 0) nmulti = 0;
+  __syncthreads();
+  const int nq = P.clipz ? 2 : 1;
+  uint32_t rr[MR_VIEW_RPT][2];
+  auto load_chunk = [&](int i0) {
+#pragma unroll
+    for (int k = 0; k < MR_VIEW_RPT; ++k)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = i0 + k * 1024 + j;
+        rr[k][q] = (q < nq && i < vcount) ? P.rects[(q ? P.NF : 0) + f0 + i] : MR_RECT_NONE;
+      }
+  };
+  // count
+#pragma unroll 1
+  for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+    load_chunk(i0);
+#pragma unroll
+    for (int k = 0; k < MR_VIEW_RPT; ++k)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
+  }
+  __syncthreads();
+  PROF_B(60000 + n, 1);
+  // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
+  const int C = (P.T + 1023) / 1024;
+  const int t0 = min(t * C, P.T), t1 = min(t0 + C, P.T);
+  int le = 0, my_u = 0, my_s = 0;
+  for (int tt = t0; tt < t1; ++tt) {
+    const int cc = hist[tt + (tt >> 6)];
+    le += cc;
+    const bool mo = P.mfpb > 0 && cc > P.mfpb;  // PyTorch3D's per-bin cap: the whole-view path
+    my_u += cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
+    my_s += cc > 0 ? 1 : 0;
+  }
+  int te, au, as;
+  const int ex0 = block_incl_sum(le, part, te) - le;
+  const int iu = block_incl_sum(my_u, part, au);
+  const int is = block_incl_sum(my_s, part, as);
+  PROF_B(60000 + n, 2);
+  if (t == 0) {
+    base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
+    base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
+    base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
+    P.vslot[n] = (int)base[1];
+    P.vslot[P.nviews + n] = as;
+  }
+  __syncthreads();
+  PROF_B(60000 + n, 3);
+  const long long vb = base[2];
+  if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
+  int u0 = (int)base[0] + iu - my_u, slot = (int)base[1] + is - my_s;
+  for (int tt = t0, ex = ex0; tt < t1; ++tt) {
+    const int cc = hist[tt + (tt >> 6)];
+    const int gt = n * P.T + tt;
+    if (P.ranges) {
+      P.cnt[gt] = cc;
+      P.start[gt] = ex;
+    }
+    const bool mo = P.mfpb > 0 && cc > P.mfpb;
+    const int nu = cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
+    // a list that would overflow the pool: its first unit scans every face of the view, the
+    // others (reserved before the pool base was known) are empty
+    const bool ovf = cc > 0 && (mo || vb + ex + cc > P.list_cap);
+    if (cc > 0) P.stile[slot] = gt;
+    const int multi = nu > 1 ? (int)0x80000000u : 0;
+    for (int k = 0; k < nu; ++k) {
+      int4 U;
+      U.x = gt;
+      U.y = ovf ? -1 : (int)(vb + ex) + k * MR_UE;
+      U.z = ovf ? (k == 0 ? vcount : 0) : min(MR_UE, cc - k * MR_UE);
+      U.w = slot | multi;
+      P.units[u0 + k] = U;
+    }
+    if (nu > 1) {
+      P.tdone[slot] = nu - 1;
+      const int k = atomicAdd(&nmulti, 1);
+      if (k < MR_SCAN_MULTI) multi_slot[k] = slot;
+      else
+        for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
+    }
+    hist[tt + (tt >> 6)] = ovf ? 0x7fffffff : (int)(vb + ex);  // fill cursor (overflowing lists are not filled)
+    u0 += nu;
+    slot += cc > 0 ? 1 : 0;
+    ex += cc;
+  }
+  __syncthreads();
+  const int nm = min(nmulti, MR_SCAN_MULTI);
+  for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
+  PROF_B(60000 + n, 4);
+  // fill
+  const bool one = vcount <= 1024 * MR_VIEW_RPT;  // the rectangles are still in registers
+#pragma unroll 1
+  for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+    if (!one) load_chunk(i0);
+#pragma unroll
+    for (int k = 0; k < MR_VIEW_RPT; ++k)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int rid = (int)((q ? P.NF : 0) + f0 + i0 + k * 1024 + j);
+        rect_tiles(rr[k][q], P.TX, [&](int tt) {
+          int* h = &hist[tt + (tt >> 6)];
+          if (*h != 0x7fffffff) {
+            const int pos = atomicAdd(h, 1);
+            if (pos < P.list_cap) P.list[pos] = rid;
+          }
+        });
+      }
+  }
+#ifdef MR_PROF
+  __syncthreads();
+#endif
+  PROF_B(60000 + n, 5);
+#ifdef MR_PROF
+  if (t == 0 && g_prof) g_prof[(size_t)(60000 + n) * 8 + 7] = 1;
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2856,6 +3134,7 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.list = w.list;
   P.vtot = w.vtot;
   P.vbase = w.vbase;
+  P.rects = w.rects;
   return P;
 }
 
@@ -2868,6 +3147,35 @@ static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, const int
   P.view_count = view_count; P.F = F;
   MR_TIMED(KID_BIN_SCAN, st, (k_bin_scan<<<(unsigned)N, 1024, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_bin_scan");
+  return MR_OK;
+}
+
+// The per-view binning applies to tile grids of <= MR_VIEW_TMAX tiles (<= 256 a side) and
+// meshes of <= MR_VIEW_FMAX faces per view on average; else count -> scan -> fill.
+static bool view_binning(const BinGeom& g, int64_t N, int64_t Ftot) {
+  return g.T <= MR_VIEW_TMAX && g.TX <= 256 && g.TY <= 256 && Ftot <= (int64_t)MR_VIEW_FMAX * N;
+}
+static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGeom& g, int64_t N, const int64_t* first,
+                           const int64_t* view_count, int64_t F, bool ranges, hipStream_t st,
+                           const ShadeParams* S = nullptr) {
+  ViewBinParams V;
+  memset(&V, 0, sizeof(V));
+  V.ranges = ranges ? 1 : 0;
+  V.nviews = (int)N;
+  int64_t sb = 0;
+  if (S) {
+    V.S = *S;
+    V.srec = w.srec;
+    V.Fs = F;
+    sb = ceil_div(F, 1024);
+  }
+  V.T = g.T; V.TX = g.TX; V.mfpb = g.mfpb; V.clipz = SP.clipz;
+  V.list_cap = g.list_cap; V.NF = SP.NF;
+  V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
+  V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
+  V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
+  MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<<<(unsigned)(N + sb), 1024, sizeof(int) * (size_t)(g.T + (g.T >> 6)), st>>>(V)));
+  MR_CHECK_LAUNCH("k_bin_view");
   return MR_OK;
 }
 
@@ -2886,7 +3194,8 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
   RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
-  if (hipMemsetAsync(w.cnt, 0, zero_bytes(N, g), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
+  const bool vpath = view_binning(g, N, Fb);
+  if (hipMemsetAsync(w.ctr, 0, zero_bytes(N, g, vpath), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
   FwdParams P = make_fwd(s, g, w, N, first, 0, Fb);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
@@ -2898,6 +3207,16 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
 #endif
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   SP.NF = Fb;
+  if (vpath) {
+    if (Ftot > 0) {
+      if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<true><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot)));
+      else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot)));
+      MR_CHECK_LAUNCH("k_bin_rect_fv");
+    }
+    if ((rc = launch_bin_view(SP, w, g, N, first, count, 0, s->faces_per_pixel > 1, st))) return rc;
+    if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
+    return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
+  }
   const int fvb = ceil_div(Ftot, 256 * MR_FV_FPT);
   if (Ftot > 0) {
     if (lds) MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_fv<true><<<fvb, 256, shm, st>>>(SP, face_verts, Ftot, first, N)));
@@ -3125,14 +3444,29 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  const int64_t nzero = (int64_t)(zero_bytes(N, g) / sizeof(int));
+  const bool vpath = view_binning(g, N, N * m->F);
+  const int64_t nzero = (int64_t)(zero_bytes(N, g, vpath) / sizeof(int));
   // normals computed here (the mesh's vnormals_out) or passed in (vnormals)
   const int64_t vb = (sp->light_kind == 0 && m->vnormals_out) ? ceil_div(m->V, 256) : 0;
   if (vb) {
     if (!m->vraw_out) return set_err(MR_EINVAL, "vnormals_out without vraw_out");
     P.S.vnormals = m->vnormals_out;
   }
-  MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.cnt, nzero)));
+  if (vpath) {
+    NormalsArgs NA;
+    NA.V = m->V; NA.ptr = m->vadj_ptr; NA.adj = m->vadj;
+    NA.vn = vb ? m->vnormals_out : nullptr;
+    NA.vraw = m->vraw_out;
+    const int64_t bx = std::max<int64_t>(ceil_div(m->F, 256 * MR_RECT_FPT), ceil_div(m->V, 256));
+    dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
+    if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr)));
+    else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr)));
+    MR_CHECK_LAUNCH("k_bin_rect_world");
+    if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S))) return rc;
+    if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
+    return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
+  }
+  MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.ctr, nzero)));
   MR_CHECK_LAUNCH("k_setup_zero");
   const int fpt = MR_BIN_FPT;
   dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);
@@ -3385,23 +3719,27 @@ int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, i
   hipStream_t st = (hipStream_t)stream;
   BinGeom g = bin_geom(H, W, N, Ftot > 0 ? Ftot : 1, mfpb);
   RasterWS w = carve_raster_ws((void*)ws, N, Ftot > 0 ? Ftot : 1, H, W, g);
-  const size_t n = (size_t)N + CTR_COUNT;  // vtot and ctr are contiguous
+  const size_t n = (size_t)N + CTR_COUNT + (size_t)N * g.T;  // ctr, cnt and vtot are contiguous
   if (hipMemsetAsync(w.ctr + CTR_COVERED, 0, sizeof(int), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
   k_count_covered<<<1024, 256, 0, st>>>(w.sface, w.ctr, w.ctr + CTR_COVERED);
   MR_CHECK_LAUNCH("k_count_covered");
   int* h = (int*)malloc(sizeof(int) * n);
   if (!h) return set_err(MR_EINVAL, "out of host memory");
-  if (hipMemcpyAsync(h, w.vtot, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
+  if (hipMemcpyAsync(h, w.ctr, sizeof(int) * n, hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess) {
     free(h);
     return set_err(MR_ELAUNCH, "stats copy failed");
   }
-  int64_t ent = 0;
-  for (int64_t i = 0; i < N; ++i) ent += h[i];
+  // entries: the per-view binning's u64 counter, else the per-view totals of the count pass
+  unsigned long long e64;
+  memcpy(&e64, h + CTR_ENTRIES64, sizeof(e64));
+  int64_t ent = (int64_t)e64;
+  if (!view_binning(g, N, Ftot > 0 ? Ftot : 1))
+    for (int64_t i = 0; i < N; ++i) ent += h[CTR_COUNT + (size_t)N * g.T + i];
   out[0] = ent;
-  out[1] = h[N + CTR_UNITS];
-  out[2] = h[N + CTR_SLOTS];
-  out[3] = h[N + CTR_COVERED];
+  out[1] = h[CTR_UNITS];
+  out[2] = h[CTR_SLOTS];
+  out[3] = h[CTR_COVERED];
   free(h);
   return MR_OK;
 }

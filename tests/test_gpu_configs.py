@@ -396,3 +396,33 @@ def test_determinism_metric_config():
     dv = (ga[0] - gb[0]).abs().max().item()
     print(f"[determinism] vertex grad run-to-run max |diff| = {dv:.3e} (scale {ga[0].abs().max().item():.3e})")
     assert dv <= 1e-5 * max(1.0, ga[0].abs().max().item())
+
+
+def test_large_image_count_scan_fill_path():
+    """Tile grids above the per-view binning's LDS limit (1040x1040 = 130x130 tiles > 16384) take the
+    count -> scan -> fill binning. Fused render fwd+bwd of one cow view against the oracle on a window
+    crossing the silhouette (upstream gradients zero outside it on both sides), fused == modular
+    pix_to_face and exact background on the whole image."""
+    H = W = 1040
+    verts, faces, d = mesh_arrays("cow")
+    img, vuv, fuv = _uv_texture(d)
+    tex = TexturesUV(maps=[img.to(DEV)], faces_uvs=[fuv.to(DEV)], verts_uvs=[vuv.to(DEV)])
+    _, _, _, (R_cv, t_cv, K) = canonical_views(verts, 1, H, W, dist=0.5)
+    out, _ = _gpu_views(verts, faces, tex, R_cv, t_cv, K, H, W, None)
+    p2f = out["pix_to_face32"][0]
+    cov = (p2f >= 0).nonzero()
+    cy, cx = cov[:, 0].float().mean().item(), cov[:, 1].float().min().item()
+    y0, x0 = int(cy) - 48, max(int(cx) - 16, 0)
+    win = (y0, y0 + 96, x0, x0 + 96)
+    grads = _upstream(1, H, W, window=win)
+    out, gg = _gpu_views(verts, faces, tex, R_cv, t_cv, K, H, W, grads)
+    ref, rg = _oracle_views(verts, faces, R_cv, t_cv, K, H, W, ("uv", vuv, fuv, img), grads, window=win)
+    p2f_ref = ref["p2f"][0, y0:y0 + 96, x0:x0 + 96, 0]
+    assert (p2f_ref >= 0).any() and (p2f_ref < 0).any(), "window must cross the silhouette"
+    assert torch.equal(out["pix_to_face32"][0, y0:y0 + 96, x0:x0 + 96].cpu().long(), p2f_ref)
+    for k, r in (("depth", ref["depth"]), ("sil", ref["sil"]), ("rgb", ref["rgba"][..., :3])):
+        report(f"1040 {k} (window)", out[k][0, y0:y0 + 96, x0:x0 + 96], r[0, y0:y0 + 96, x0:x0 + 96])
+    for nm, a, b in zip(("verts", "R_cv", "t_cv"), gg, rg):
+        report(f"1040 grad {nm}", a, b)
+    assert torch.equal(out["pix_to_face32"].long(), _modular_p2f(verts, faces, R_cv, t_cv, K, H, W))
+    _check_background(out, out["pix_to_face32"], (1.0, 1.0, 1.0))

@@ -164,6 +164,26 @@ int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t
                           int64_t num_cam_centers, const mr_raster_settings_t* rs, const mr_shade_params_t* sp,
                           float* depth, float* silhouette, float* rgb, int32_t* pix_to_face32, void* workspace,
                           size_t workspace_bytes, void* stream);
+/* OpenCV camera poses as DifferentiableRenderer takes them (torch_renderer.py:73-80): R_cv (N,3,3),
+ * t_cv (N,3), intrinsics rows {ax, bx, ay, by} (N,4); *_stride = floats between consecutive views
+ * (0 broadcasts one row). */
+typedef struct mr_opencv_poses {
+  const float* R;
+  int64_t R_stride;
+  const float* t;
+  int64_t t_stride;
+  const float* intr;
+  int64_t intr_stride;
+} mr_opencv_poses_t;
+/* mr_render_forward for OpenCV poses: the pose conversion (mr_views_from_opencv) happens inside the
+ * forward's first launch, which also writes the converted records to views_out (N) for the backward
+ * (mr_render_backward_opencv). Replaces DifferentiableRenderer._camera_pose_from_opencv_to_pytorch +
+ * the render call (torch_renderer.py:73-80, :110-121, :155-159). */
+int32_t mr_render_forward_opencv(const mr_mesh_t* mesh, const mr_opencv_poses_t* poses, mr_view_t* views_out,
+                                 int64_t N, const float* cam_centers, int64_t num_cam_centers,
+                                 const mr_raster_settings_t* rs, const mr_shade_params_t* sp, float* depth,
+                                 float* silhouette, float* rgb, int32_t* pix_to_face32, void* workspace,
+                                 size_t workspace_bytes, void* stream);
 /* Backward from upstream grads (each may be NULL when not requested in out_flags).
  * Writes grad_verts (V,3), grad_views (N,12), grad_vcolors (V,3; tex_kind 1 only, may be NULL).
  * `fwd_workspace` must be the one passed to the matching mr_render_forward: its face records and

@@ -50,6 +50,11 @@ class MrShadeParams(ctypes.Structure):
                 ("rgb_channels", ctypes.c_int32)]
 
 
+class MrOpencvPoses(ctypes.Structure):
+    _fields_ = [("R", ctypes.c_void_p), ("R_stride", ctypes.c_int64), ("t", ctypes.c_void_p),
+                ("t_stride", ctypes.c_int64), ("intr", ctypes.c_void_p), ("intr_stride", ctypes.c_int64)]
+
+
 class MrMesh(ctypes.Structure):
     _fields_ = [("verts", ctypes.c_void_p), ("V", ctypes.c_int64), ("faces", ctypes.c_void_p),
                 ("F", ctypes.c_int64), ("vadj_ptr", ctypes.c_void_p), ("vadj", ctypes.c_void_p),
@@ -81,6 +86,9 @@ _SIGS = [
     ("mr_render_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
     ("mr_render_forward", _I32, [ctypes.POINTER(MrMesh), _VP, _I64, _VP, _I64, ctypes.POINTER(MrRasterSettings),
                                  ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
+    ("mr_render_forward_opencv", _I32, [ctypes.POINTER(MrMesh), ctypes.POINTER(MrOpencvPoses), _VP, _I64, _VP, _I64,
+                                        ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP,
+                                        _VP, _VP, _VP, _SZ, _VP]),
     ("mr_render_backward_workspace", _SZ, [_I64, _I64, _I64, _I32, _I32]),
     ("mr_render_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _I64, _VP, _I64,
                                   ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP, _VP,

@@ -886,12 +886,38 @@ struct NormalsArgs {
   float* vn;    // NULL: no normals to compute
   float* vraw;
 };
+// OpenCV poses converted on the fly (mr_render_forward_opencv): element k of view n's record,
+// as k_views_from_opencv writes it (torch_renderer.py:73-80; bitwise the torch conversion).
+struct CvPoses {
+  const float* R;  // NULL: the view records are given
+  int64_t sR;
+  const float* t;
+  int64_t sT;
+  const float* intr;
+  int64_t sI;
+  float* out;  // (N,16) view records written for the later launches
+};
+MR_DEV float cv_view_elem(const CvPoses& C, int64_t n, int k) {
+  float v;
+  if (k < 9) {  // R_p3d[a][b] = R_cv[b][a] * s[b], s = (-1, -1, 1)
+    const int a = k / 3, b = k - 3 * a;
+    v = C.R[n * C.sR + 3 * b + a];
+    if (b < 2) v = -v;
+  } else if (k < 12) {
+    v = C.t[n * C.sT + (k - 9)];
+    if (k < 11) v = -v;
+  } else {
+    v = C.intr[n * C.sI + (k - 12)];
+  }
+  return v;
+}
 template <bool CLIP>
 __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const float* __restrict__ verts,
                                                         const int32_t* __restrict__ faces, int64_t F,
                                                         const ViewRec* __restrict__ views, NormalsArgs NA,
-                                                        int* __restrict__ ctr) {
+                                                        int* __restrict__ ctr, CvPoses C) {
   const int n = (int)blockIdx.y - 1;
+  if (n >= 0 && C.R && blockIdx.x == 0 && threadIdx.x < 16) C.out[(int64_t)n * 16 + threadIdx.x] = cv_view_elem(C, n, threadIdx.x);
   if (n < 0) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
@@ -903,7 +929,15 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     const int64_t f = ((int64_t)blockIdx.x * MR_RECT_FPT + k) * blockDim.x + threadIdx.x;
     if (f >= F) return;
     float v[3][3];
-    world_face_verts(verts, faces, f, views[n], v);
+    ViewRec V;
+    if (C.R) {
+      float* e = (float*)&V;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) e[k] = cv_view_elem(C, n, k);
+    } else {
+      V = views[n];
+    }
+    world_face_verts(verts, faces, f, V, v);
     const int64_t rid = (int64_t)n * F + f;
     FaceRec r2;
     const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
@@ -3413,9 +3447,30 @@ size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t m
   return carve_raster_ws(nullptr, N, N * F, H, W, g, F).bytes;
 }
 
+static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
+                              const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
+                              float* rgb, int32_t* p2f32, void* ws, size_t ws_bytes, void* stream, const CvPoses& C);
 int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
                           const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
                           float* rgb, int32_t* p2f32, void* ws, size_t ws_bytes, void* stream) {
+  CvPoses C;
+  memset(&C, 0, sizeof(C));
+  return render_forward(m, views, N, cc, ncc, s, sp, depth, sil, rgb, p2f32, ws, ws_bytes, stream, C);
+}
+int32_t mr_render_forward_opencv(const mr_mesh_t* m, const mr_opencv_poses_t* poses, mr_view_t* views_out, int64_t N,
+                                 const float* cc, int64_t ncc, const mr_raster_settings_t* s,
+                                 const mr_shade_params_t* sp, float* depth, float* sil, float* rgb, int32_t* p2f32,
+                                 void* ws, size_t ws_bytes, void* stream) {
+  if (!poses || !poses->R || !poses->t || !poses->intr || !views_out) return set_err(MR_EINVAL, "NULL pose argument");
+  if (poses->R_stride < 0 || poses->t_stride < 0 || poses->intr_stride < 0) return set_err(MR_EINVAL, "negative stride");
+  CvPoses C;
+  C.R = poses->R; C.sR = poses->R_stride; C.t = poses->t; C.sT = poses->t_stride;
+  C.intr = poses->intr; C.sI = poses->intr_stride; C.out = (float*)views_out;
+  return render_forward(m, views_out, N, cc, ncc, s, sp, depth, sil, rgb, p2f32, ws, ws_bytes, stream, C);
+}
+static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
+                              const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
+                              float* rgb, int32_t* p2f32, void* ws, size_t ws_bytes, void* stream, const CvPoses& C) {
   int rc = check_settings(s);
   if (rc) return rc;
   rc = check_mesh(m, sp);
@@ -3459,12 +3514,16 @@ int32_t mr_render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
     NA.vraw = m->vraw_out;
     const int64_t bx = std::max<int64_t>(ceil_div(m->F, 256 * MR_RECT_FPT), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
-    if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr)));
-    else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr)));
+    if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
+    else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
     MR_CHECK_LAUNCH("k_bin_rect_world");
     if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S))) return rc;
     if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
     return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
+  }
+  if (C.R) {  // count -> scan path: the view records first
+    k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C.R, C.sR, C.t, C.sT, C.intr, C.sI, N, C.out);
+    MR_CHECK_LAUNCH("k_views_from_opencv");
   }
   MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.ctr, nzero)));
   MR_CHECK_LAUNCH("k_setup_zero");

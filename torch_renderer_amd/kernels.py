@@ -317,8 +317,14 @@ class RenderViews(torch.autograd.Function):
         v = verts.detach().float().contiguous()
         f, vptr, vadj = mesh_topology(faces, v.shape[0])
         vcol = vcolors.detach().float().contiguous() if vcolors is not None else None
-        if pose_cv:  # R, T are OpenCV poses (DifferentiableRenderer callers)
-            views = views_from_opencv(R, T, intr, max(R.shape[0], T.shape[0], intr.shape[0]))
+        poses = None
+        if pose_cv:  # R, T are OpenCV poses (DifferentiableRenderer callers): converted inside the forward
+            Rc, sR = _batch_stride(R.detach().reshape(-1, 3, 3))
+            tc, sT = _batch_stride(T.detach().reshape(-1, 3))
+            ic, sI = _batch_stride(intr.reshape(-1, 4))
+            sp_ = _lib.strided_ptr
+            poses = _lib.MrOpencvPoses(sp_(Rc), sR, sp_(tc), sT, sp_(ic), sI)
+            views = torch.empty((max(R.shape[0], T.shape[0], intr.shape[0]), 16), device=dev)
         else:
             views = make_views(R.detach(), T.detach(), intr)
         N = views.shape[0]
@@ -340,9 +346,14 @@ class RenderViews(torch.autograd.Function):
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
         global _LAST_RENDER
         _LAST_RENDER = (weakref.ref(ws), (N, N * f.shape[0], H, W, rs.max_faces_per_bin))
-        check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
-                                  ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
-                                  _lib.stream_handle(dev)))
+        if poses is not None:
+            check(L.mr_render_forward_opencv(ctypes.byref(mesh), ctypes.byref(poses), ptr(views), N, ptr(cc),
+                                             cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(depth), ptr(sil),
+                                             ptr(rgb), ptr(p2f), ptr(ws), wsb, _lib.stream_handle(dev)))
+        else:
+            check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
+                                      ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
+                                      _lib.stream_handle(dev)))
         ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
                               vn if vn is not None else torch.empty(0, device=dev),
                               raw if raw is not None else torch.empty(0, device=dev), vptr, vadj)

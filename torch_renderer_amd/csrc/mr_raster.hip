@@ -1215,8 +1215,20 @@ MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, cons
                       float pad, float blur, bool persp, bool clipb, int& cid, float& pz);
 // The pixels of one lane's tile rectangle for a split face's triangle (k_tile_raster, rare path;
 // out of line so that its registers do not weigh on the pixel-pair loop).
+MR_DEV void stage_rec_put(float (*rec)[64], int lane, const FaceRec& r) {
+  const float* f = (const float*)&r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) rec[i][lane] = f[i];
+}
+MR_DEV FaceRec stage_rec_get(const float (*rec)[64], int m) {
+  FaceRec r;
+  float* f = (float*)&r;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) f[i] = rec[i][m];
+  return r;
+}
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
-                                                           const FaceRec* srec, const int* sid, const float* xs,
+                                                           const float (*srec)[64], const int* sid, const float* xs,
                                                            const float* ys, unsigned long long* key, int lane,
                                                            int prect, float pad, float blur, bool persp, bool clipb);
 MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, const FaceRec& r, float x, float y,
@@ -1292,8 +1304,12 @@ struct FwdParams {
 };
 
 // One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).
+// Face records of the unit's entries, structure-of-arrays: field i of entry m at rec[i][m]. The
+// pair passes read the records of up to 64 different entries at once; an array of 64-B records
+// put entries 4 apart on the same LDS bank (bank conflicts on every record read), the field
+// arrays put distinct entries on distinct banks.
 struct WaveStage {
-  FaceRec rec[64];
+  float rec[16][64];
   int id[64];
   int meta[64];  // first pair index | (rect width - 1) << 13 | tile col << 16 | tile row << 19
   int mark[64];  // pass-local: pair slot -> entry lane that starts there
@@ -1415,10 +1431,10 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
 
 
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
-                                                           const FaceRec* srec, const int* sid, const float* xs,
+                                                           const float (*srec)[64], const int* sid, const float* xs,
                                                            const float* ys, unsigned long long* key, int lane,
                                                            int prect, float pad, float blur, bool persp, bool clipb) {
-  const FaceRec r = srec[lane];
+  const FaceRec r = stage_rec_get(srec, lane);
   const int id = sid[lane];
   for (int yy = (prect >> 6) & 7; yy <= ((prect >> 9) & 7); ++yy)
     for (int xx = prect & 7; xx <= ((prect >> 3) & 7); ++xx) {
@@ -1550,7 +1566,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
             meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
           }
         }
-        S.rec[lane] = r;
+        stage_rec_put(S.rec, lane, r);
         S.id[lane] = id;
       }
       if (eb == 0) {  // advance the pipeline (after this unit's records are consumed)
@@ -1579,7 +1595,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
         if (lane < cnt) {
           const int pk = S.queue[(qhead + lane) & 127];
           const int m = pk >> 6, sy = (pk >> 3) & 7, sx = pk & 7;
-          const FaceRec r = S.rec[m];
+          const FaceRec r = stage_rec_get(S.rec, m);
           float pz;
           if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
             atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
@@ -1618,7 +1634,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
 #endif
           const int lx = loc - ly * w;
           const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
-          const FaceRec r = S.rec[m];
+          const FaceRec r = stage_rec_get(S.rec, m);
           cand = frag_cand(r, S.xs[sx], S.ys[sy], pad, fast_ok && (r.flags & FR_FAST));
           pk = (m << 6) | (sy << 3) | sx;
         }
@@ -2308,7 +2324,9 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
   return P.gRGB[pix * P.rgb_ch + 3];
 }
 
-template <int ACC>
+// CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
+// instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
+template <int ACC, bool CLIP>
 __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
@@ -2371,7 +2389,7 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
 #else
       if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
 #endif
-        if (r.flags & FR_CLIP) clip_unconvert(P.crec[f], e.b0, e.b1, e.b2, e.b0, e.b1, e.b2);
+        if (CLIP && (r.flags & FR_CLIP)) clip_unconvert(P.crec[f], e.b0, e.b1, e.b2, e.b0, e.b1, e.b2);
         ShadeOut so;
         ShadeCache C;
         BACC(1);
@@ -2436,7 +2454,7 @@ __global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
       const float gt3[3] = {a3.z, a3.w, a4.x};
       float gfv[3][3];
       BACC(4);
-      const bool clipped = (r.flags & FR_CLIP) != 0;
+      const bool clipped = CLIP && (r.flags & FR_CLIP) != 0;
       const float pxf = col_ndc(px, P.H, P.W), pyf = row_ndc(py, P.H, P.W);
       float gbr[3] = {gb[0], gb[1], gb[2]};
       if (clipped) clip_gb_sub(P.crec[f], gb, gbr);  // near-plane sub-triangle: C g_orig
@@ -3638,11 +3656,18 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
   };
-  static int f18 = 0, f27 = 0;
-  if (!f18) f18 = resident_grid(k_bwd_fused<18>, 256, 3);
-  if (!f27) f27 = resident_grid(k_bwd_fused<27>, 256, 2);
-  if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27><<<cap(f27), 256, 0, st>>>(P)));
-  else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18><<<cap(f18), 256, 0, st>>>(P)));
+  static int f18 = 0, f27 = 0, f18c = 0, f27c = 0;
+  if (!f18) f18 = resident_grid(k_bwd_fused<18, false>, 256, 3);
+  if (!f27) f27 = resident_grid(k_bwd_fused<27, false>, 256, 2);
+  if (!f18c) f18c = resident_grid(k_bwd_fused<18, true>, 256, 3);
+  if (!f27c) f27c = resident_grid(k_bwd_fused<27, true>, 256, 2);
+  if (s->clip_z) {
+    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, true><<<cap(f27c), 256, 0, st>>>(P)));
+    else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, true><<<cap(f18c), 256, 0, st>>>(P)));
+  } else {
+    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false><<<cap(f27), 256, 0, st>>>(P)));
+    else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false><<<cap(f18), 256, 0, st>>>(P)));
+  }
   MR_CHECK_LAUNCH("k_bwd_fused");
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V * MR_VL, 256);

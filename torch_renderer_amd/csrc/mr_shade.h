@@ -543,13 +543,23 @@ MR_DEV void pt_tri_bwd(float px, float py, const FaceRec& r, float g, float gv[3
   const float e01 = FAST ? pt_line_dist_fast(px, py, r.x0, r.y0, r.x1, r.y1) : pt_line_dist(px, py, r.x0, r.y0, r.x1, r.y1);
   const float e02 = FAST ? pt_line_dist_fast(px, py, r.x0, r.y0, r.x2, r.y2) : pt_line_dist(px, py, r.x0, r.y0, r.x2, r.y2);
   const float e12 = FAST ? pt_line_dist_fast(px, py, r.x1, r.y1, r.x2, r.y2) : pt_line_dist(px, py, r.x1, r.y1, r.x2, r.y2);
-  for (int c = 0; c < 3; ++c) gv[c][0] = gv[c][1] = 0.0f;
-  if (e01 <= e02 && e01 <= e12)
-    pt_line_bwd<FAST>(px, py, r.x0, r.y0, r.x1, r.y1, g, gv[0][0], gv[0][1], gv[1][0], gv[1][1]);
-  else if (e02 <= e01 && e02 <= e12)
-    pt_line_bwd<FAST>(px, py, r.x0, r.y0, r.x2, r.y2, g, gv[0][0], gv[0][1], gv[2][0], gv[2][1]);
-  else if (e12 <= e01 && e12 <= e02)
-    pt_line_bwd<FAST>(px, py, r.x1, r.y1, r.x2, r.y2, g, gv[1][0], gv[1][1], gv[2][0], gv[2][1]);
+  // the closest edge (ties: e01, then e02, then e12; none when a distance is NaN), then ONE
+  // pt_line_bwd on its endpoints (branch-free: per-lane selects instead of three divergent calls)
+  const bool s01 = e01 <= e02 && e01 <= e12;
+  const bool s02 = !s01 && e02 <= e01 && e02 <= e12;
+  const bool s12 = !s01 && !s02 && e12 <= e01 && e12 <= e02;
+  const int ia = s12 ? 1 : 0, ib = s01 ? 1 : 2;  // endpoint corners
+  const float ax = ia ? r.x1 : r.x0, ay = ia ? r.y1 : r.y0;
+  const float bx = ib == 1 ? r.x1 : r.x2, by = ib == 1 ? r.y1 : r.y2;
+  float gax, gay, gbx, gby;
+  pt_line_bwd<FAST>(px, py, ax, ay, bx, by, (s01 || s02 || s12) ? g : 0.0f, gax, gay, gbx, gby);
+  const bool any = s01 || s02 || s12;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const bool isa = any && c == ia, isb = any && c == ib;
+    gv[c][0] = isa ? gax : (isb ? gbx : 0.0f);
+    gv[c][1] = isa ? gay : (isb ? gby : 0.0f);
+  }
 }
 
 // RasterizeMeshesBackward for one (pixel, face): grads of (zbuf, bary, dists)

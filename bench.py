@@ -116,12 +116,14 @@ def cpu_baseline(verts, faces, d, R_cv, t_cv, K, H, W, n_views=2, reps=3, mesh="
 # launch's batch, from the forward's own work counters (kernels.render_stats: list entries,
 # covered pixels). Device-side caches may serve part of it; rocprof FETCH/WRITE is reported
 # beside it as roofline.traffic.
-def algorithmic_bytes(kernel, H, W, F, views, st):
+def algorithmic_bytes(kernel, H, W, F, views, st, bgpix=0):
+    """bgpix: pixels whose background k_bin_view's spare workgroups write (mr_binning_background_pixels);
+    k_tile_raster writes the background of the others."""
     HW, cov, ent, slots, units = H * W, st["covered"], st["entries"], st["tiles"], st.get("units", 0)
     table = {
-        # background of every pixel (depth + silhouette + rgb(3)), list ids, each face record once,
-        # 64 winners per non-empty tile
-        "k_tile_raster": 20 * HW * views + 4 * ent + 64 * F * views + 256 * slots,
+        # background (depth + silhouette + rgb(3)) of the pixels k_bin_view did not take, list ids,
+        # each face record once, 64 winners per non-empty tile
+        "k_tile_raster": 20 * (HW * views - bgpix) + 4 * ent + 64 * F * views + 256 * slots,
         "k_shade<1>": 256 * slots + 20 * cov,              # winners in, 20 B of outputs per covered pixel
         "k_bwd_shade": 256 * slots + (20 + 80) * cov,      # winners + upstream grads, 80-B gradient record out
         "k_bwd_geom": 256 * slots + 80 * cov + 72 * F,     # winners + gradient record in, per-face rows out
@@ -132,7 +134,8 @@ def algorithmic_bytes(kernel, H, W, F, views, st):
         "k_bin_count": 64 * F * views + 24 * F,            # face records out, mesh in
         "k_bin_fill": 64 * F * views + 4 * ent,            # face records in, list ids out
         "k_bin_rect": (64 + 4) * F * views + 24 * F,       # face records + tile rectangles out, mesh in
-        "k_bin_view": 4 * F * views + 4 * ent + 16 * units,  # rectangles in, list ids + work units out
+        # rectangles in, list ids + work units out, the background of bgpix pixels
+        "k_bin_view": 4 * F * views + 4 * ent + 16 * units + 20 * bgpix,
     }
     return table.get(kernel)
 
@@ -303,7 +306,8 @@ def main():
     if dom is not None:
         name, (launches, total_ms) = dom
         avg_s = total_ms / launches / 1e3
-        b = algorithmic_bytes(name, H, W, Fn, nv, wstats)
+        bgpix = int(_lib.load().mr_binning_background_pixels(nv, Fn, H, W, 1))
+        b = algorithmic_bytes(name, H, W, Fn, nv, wstats, bgpix)
         ent = pmc.get(name)
         traffic = ent.get("hbm_bytes_per_launch") if ent and ent.get("config") == f"{args.mesh}-{H}x{W}-{nv}" else None
         if b is not None:
@@ -353,12 +357,13 @@ FRAG_KERNELS = ("k_project_faces", "k_bin_count", "k_bin_scan", "k_bin_fill", "k
 def bench_fragments(args, dev, world, rank):
     """The fragment pass alone: MeshRasterizer(meshes_world, R, T) -> Fragments(pix_to_face int64, zbuf,
     bary_coords, dists), K=1 (camera_pose_optimizer.py:244-246, batch_rendering_test.py:274): projection
-    (mr_project_faces) + binning + raster + fragment writes (mr_rasterize_meshes). API-minimum bytes per
-    frame: 28 B/px of fragments + 36 B/face of face_verts."""
+    + binning + raster + fragment writes in one native call (mr_rasterize_meshes_world, what
+    MeshRasterizer.forward runs for an extended mesh). API-minimum bytes per frame:
+    28 B/px of fragments + 36 B/face of face_verts."""
     from torch_renderer_amd import _lib
     from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset
-    from torch_renderer_amd.kernels import ProjectFaces, RasterizeFaceVerts, mesh_topology
+    from torch_renderer_amd.kernels import RasterizeMeshesWorld, mesh_topology
     from torch_renderer_amd.cameras import PerspectiveCameras, view_batch
     from torch_renderer_amd.transforms import opencv_to_pytorch3d
 
@@ -377,12 +382,9 @@ def bench_fragments(args, dev, world, rank):
     Rb, Tb, intr = view_batch(cams, (H, W), Rp, Tp, n_views=nv)
     intr = intr.contiguous()
     mesh_topology(faces, verts.shape[0])
-    first = (torch.arange(nv, device=dev) * Fn).contiguous()
-    count = torch.full((nv,), Fn, device=dev, dtype=torch.int64)
 
-    def step():
-        fv = ProjectFaces.apply(verts, Rb, Tb, faces, intr)
-        return RasterizeFaceVerts.apply(fv, first, count, H, W, 1, 0.0, True, False, False, None)
+    def step():  # MeshRasterizer.forward's native call for one mesh shared by the views
+        return RasterizeMeshesWorld.apply(verts, Rb, Tb, faces, intr, nv, H, W, 1, 0.0, True, False, False, None)
 
     with torch.no_grad():
         for _ in range(args.warmup):

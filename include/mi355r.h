@@ -123,6 +123,36 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* mesh_to_face
                             const mr_raster_settings_t* settings, int64_t* pix_to_face, float* zbuf,
                             float* bary, float* dists, void* workspace, size_t workspace_bytes, void* stream);
 
+/* Camera poses in the PyTorch3D convention (row-vector R (N,3,3), T (N,3); X_view = X_world R + T) with
+ * the intrinsics rows {ax, bx, ay, by} (N,4) of mr_view_t; *_stride = floats between consecutive views
+ * (0 broadcasts one row). Same layout as mr_opencv_poses_t. */
+typedef struct mr_poses {
+  const float* R;
+  int64_t R_stride;
+  const float* T;
+  int64_t T_stride;
+  const float* intr;
+  int64_t intr_stride;
+} mr_poses_t;
+
+/* MeshRasterizer.forward for ONE mesh shared by N views (Meshes.extend; upstream
+ * mesh/rasterizer.py transform + rasterize_meshes): verts (V,3) f32, faces (F,3) i32. Writes the
+ * fragments (as mr_rasterize_meshes, packed face ids n*F + f), face_verts (N*F,3,3) — what
+ * _RasterizeFaceVerts saves for mr_rasterize_meshes_backward, bitwise mr_project_faces' output — and
+ * the view records views_out (N) for mr_project_faces_backward. The projection runs inside the
+ * binning's first launch (no separate projection launch, no counter memset). */
+size_t mr_rasterize_meshes_world_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
+int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                  const mr_poses_t* poses, int64_t N, const mr_raster_settings_t* settings,
+                                  mr_view_t* views_out, float* face_verts, int64_t* pix_to_face, float* zbuf,
+                                  float* bary, float* dists, void* workspace, size_t workspace_bytes, void* stream);
+
+/* Measurement helper (bench.py's per-kernel algorithmic bytes): output pixels whose background the
+ * per-view binning launch (k_bin_view) writes on the CUs its view workgroups leave idle, for a
+ * K = 1 forward of N views of F faces (mode 0: mr_rasterize_meshes[_world] fragments, 1: the
+ * fused render); k_tile_raster writes the rest. */
+int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W, int32_t mode);
+
 /* grad_face_verts (F,3,3) is overwritten (zeroed then accumulated). */
 int32_t mr_rasterize_meshes_backward(const float* face_verts, const int64_t* pix_to_face,
                                      const float* grad_zbuf, const float* grad_bary, const float* grad_dists,

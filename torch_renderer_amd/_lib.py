@@ -55,6 +55,11 @@ class MrOpencvPoses(ctypes.Structure):
                 ("t_stride", ctypes.c_int64), ("intr", ctypes.c_void_p), ("intr_stride", ctypes.c_int64)]
 
 
+class MrPoses(ctypes.Structure):
+    _fields_ = [("R", ctypes.c_void_p), ("R_stride", ctypes.c_int64), ("T", ctypes.c_void_p),
+                ("T_stride", ctypes.c_int64), ("intr", ctypes.c_void_p), ("intr_stride", ctypes.c_int64)]
+
+
 class MrMesh(ctypes.Structure):
     _fields_ = [("verts", ctypes.c_void_p), ("V", ctypes.c_int64), ("faces", ctypes.c_void_p),
                 ("F", ctypes.c_int64), ("vadj_ptr", ctypes.c_void_p), ("vadj", ctypes.c_void_p),
@@ -78,6 +83,11 @@ _SIGS = [
                                    _VP, _VP, _SZ, _VP]),
     ("mr_rasterize_meshes_backward", _I32, [_VP, _VP, _VP, _VP, _VP, _I64, _I64, ctypes.POINTER(MrRasterSettings),
                                             _VP, _VP]),
+    ("mr_rasterize_meshes_world_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
+    ("mr_rasterize_meshes_world", _I32, [_VP, _I64, _VP, _I64, ctypes.POINTER(MrPoses), _I64,
+                                         ctypes.POINTER(MrRasterSettings), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ,
+                                         _VP]),
+    ("mr_binning_background_pixels", _I64, [_I64, _I64, _I32, _I32, _I32]),
     ("mr_project_faces", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_views_from_opencv", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _VP]),
     ("mr_view_grads_to_opencv", _I32, [_VP, _I64, _VP, _VP, _VP]),
@@ -134,7 +144,11 @@ def load(path: str | None = None) -> ctypes.CDLL:
                 "(python -m torch_renderer_amd._build). There is no CPU fallback.")
         lib = ctypes.CDLL(p)
         for name, res, args in _SIGS:
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None and path is None and not os.environ.get("MI355R_LIB"):
+                raise RuntimeError(f"mi355r: {p} does not export {name} (stale build?)")
+            if fn is None:  # an experiment build older than the current ABI
+                continue
             fn.restype = res
             fn.argtypes = args
         if path is None:

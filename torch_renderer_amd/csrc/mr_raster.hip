@@ -242,6 +242,7 @@ struct SetupParams {
   int* vtot;
   const int* vbase;
   uint32_t* rects;  // k_bin_view path: per-record tile rectangles
+  float* fv_out;    // k_bin_rect_world: face_verts (N*F,3,3) written beside the records (NULL: none)
 };
 
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
@@ -896,10 +897,13 @@ struct CvPoses {
   const float* intr;
   int64_t sI;
   float* out;  // (N,16) view records written for the later launches
+  int opencv;  // 1: OpenCV R_cv / t_cv (converted); 0: PyTorch3D R / T as given
 };
 MR_DEV float cv_view_elem(const CvPoses& C, int64_t n, int k) {
   float v;
-  if (k < 9) {  // R_p3d[a][b] = R_cv[b][a] * s[b], s = (-1, -1, 1)
+  if (!C.opencv) {
+    v = k < 9 ? C.R[n * C.sR + k] : k < 12 ? C.t[n * C.sT + (k - 9)] : C.intr[n * C.sI + (k - 12)];
+  } else if (k < 9) {  // R_p3d[a][b] = R_cv[b][a] * s[b], s = (-1, -1, 1)
     const int a = k / 3, b = k - 3 * a;
     v = C.R[n * C.sR + 3 * b + a];
     if (b < 2) v = -v;
@@ -939,6 +943,13 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     }
     world_face_verts(verts, faces, f, V, v);
     const int64_t rid = (int64_t)n * F + f;
+    if (P.fv_out) {
+      float* o = P.fv_out + rid * 9;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) o[3 * c + q] = v[c][q];
+    }
     FaceRec r2;
     const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
     P.recs[rid] = r;
@@ -950,9 +961,11 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
 // face_verts mode (record = packed face id): the workgroup's face_verts staged through LDS
 // with 16-B loads.
 template <bool CLIP>
-__global__ void __launch_bounds__(256) k_bin_rect_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot) {
+__global__ void __launch_bounds__(256) k_bin_rect_fv(SetupParams P, const float* __restrict__ fv, int64_t Ftot,
+                                                     int* __restrict__ ctr) {
   __shared__ __attribute__((aligned(16))) float sfv[9 * 256];
   const int64_t f0 = (int64_t)blockIdx.x * blockDim.x;
+  if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;  // the work counters (k_bin_view)
   const int nf = (int)(Ftot - f0 < (int64_t)blockDim.x ? Ftot - f0 : (int64_t)blockDim.x);
   const float4* src = (const float4*)(fv + 9 * f0);  // f0 % 256 == 0: 16-B aligned if fv is
   const int n4 = ((uintptr_t)src & 15) == 0 ? 9 * nf / 4 : 0;
@@ -994,6 +1007,7 @@ struct ViewBinParams {
   ShadeParams S;
   ShadeRec* srec;
   int64_t Fs;
+  int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
 };
 
 template <typename Fn>
@@ -1003,7 +1017,7 @@ MR_DEV void rect_tiles(uint32_t r, int TX, Fn&& fn) {
     for (int tx = tx0; tx <= tx1; ++tx) fn(ty * TX + tx);
 }
 
-__global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) {
+MR_DEV void bin_view_body(const ViewBinParams& P) {
   extern __shared__ __attribute__((aligned(16))) int hist[];  // T (+ T/64 pad): counts, then fill cursors
   __shared__ int part[16];
   __shared__ long long base[3];
@@ -1144,6 +1158,7 @@ __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) {
   if (t == 0 && g_prof) g_prof[(size_t)(60000 + n) * 8 + 7] = 1;
 #endif
 }
+__global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) { bin_view_body(P); }
 
 // ---------------------------------------------------------------------------
 // 2. raster: per-tile depth keys (k_tile_raster), then a streaming resolve (k_resolve)
@@ -1283,6 +1298,7 @@ struct FwdParams {
   int64_t list_cap;
   int mfpb;
   int fill;  // k_tile_raster also writes the background
+  int fill_first;  // ... from this chunk on: the chunks before it were written by k_bin_view<MODE, CH>
   int* ctr;
   unsigned long long* tkey;
   int* tdone;
@@ -1430,6 +1446,27 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
 }
 
 
+// The per-view binning with background workgroups: one 1024-thread workgroup per view leaves
+// most CUs idle, so workgroups past the views (and the ShadeRec ones) stream the background of
+// the first F.fill_first chunks (view-major) while the views bin; k_tile_raster writes the rest.
+// The background does not depend on the raster (k_shade overwrites the covered pixels later).
+template <int MODE, int CH>
+__global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P, FwdParams F) {
+  const int b = (int)blockIdx.x - P.nviews - P.nsrec_wg;
+  if (b < 0) {
+    bin_view_body(P);
+    return;
+  }
+  const int nbw = ((int)gridDim.x - P.nviews - P.nsrec_wg) * 16;  // background waves
+  const bool vec = (F.W & 3) == 0;
+  const int64_t HW = (int64_t)F.H * F.W * (MODE == 0 ? F.K : 1);
+  const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
+  const Bg bg = background<MODE>(F);
+#pragma unroll 1
+  for (int c = b * 16 + (int)(threadIdx.x >> 6); c < F.fill_first; c += nbw)
+    fill_chunk<MODE, CH>(F, bg, c / cpv, c - (c / cpv) * cpv, vec);
+}
+
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
                                                            const float (*srec)[64], const int* sid, const float* xs,
                                                            const float* ys, unsigned long long* key, int lane,
@@ -1481,7 +1518,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const int Cp = (nunits + parts - 1) / parts;
   const int ub = (blockIdx.x % parts) * Cp, ue = ub + Cp < nunits ? ub + Cp : nunits;
   const Bg bg = background<MODE>(P);
-  int chunk = gw;
+  int chunk = P.fill_first + gw;
   // Software pipeline over the wave's units u, u + Gp, u + 2Gp, ...: while unit u is
   // rasterised, the face records of u + Gp, the list entries of u + 2Gp and the unit record of
   // u + 3Gp are in flight (unit records are wave-uniform scalar loads). Each link of the
@@ -1881,8 +1918,9 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
     const int64_t vb = P.vbase[n];
     // the scan's overflow rule: scan the whole view
     const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
-    const int64_t vfirst = P.view_first[n];
-    const int count = ovf ? (int)(P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : cc;
+    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
+    const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
+    const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
     int nq = 0;
 #pragma unroll 1
     for (int eb = 0; eb < count; eb += 64) {
@@ -3187,6 +3225,7 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.vtot = w.vtot;
   P.vbase = w.vbase;
   P.rects = w.rects;
+  P.fv_out = nullptr;
   return P;
 }
 
@@ -3207,9 +3246,40 @@ static int launch_scan(const RasterWS& w, int64_t N, const BinGeom& g, const int
 static bool view_binning(const BinGeom& g, int64_t N, int64_t Ftot) {
   return g.T <= MR_VIEW_TMAX && g.TX <= 256 && g.TY <= 256 && Ftot <= (int64_t)MR_VIEW_FMAX * N;
 }
+extern "C++" {
+// Background chunks per wave of k_bin_view's background workgroups (measured on the bench
+// workloads, profiles/r2e_bg_ab.txt): beyond these the stores slow the view workgroups' binning
+// more than they shorten the raster.
+#ifndef MR_BG_CPW_RENDER
+#define MR_BG_CPW_RENDER 8  // 5 KB chunks (depth, silhouette, RGB)
+#endif
+#ifndef MR_BG_CPW_FRAG
+#define MR_BG_CPW_FRAG 4    // 7 KB chunks (PyTorch3D fragments)
+#endif
+static int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+// Background chunks the k_bin_view launch takes over (chunks of 64 lanes x 4 pixels when W % 4 == 0,
+// else 64 pixels); 0 when the views leave no CU idle.
+static int64_t bg_chunks(int64_t N, int64_t sb, int H, int W, int mode) {
+  const int64_t nbg = (int64_t)num_cus() - N - sb;
+  if (nbg <= 0) return 0;
+  const int64_t HW = (int64_t)H * W;
+  const int64_t nchunks = N * ((W & 3) == 0 ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
+  return std::min<int64_t>(nchunks, nbg * 16 * (mode == 0 ? MR_BG_CPW_FRAG : MR_BG_CPW_RENDER));
+}
+// MODE >= 0 with Pf: the fused K = 1 raster follows, and the CUs the views leave idle stream the
+// first chunks of its background (Pf->fill_first).
+template <int MODE = -1, int CH = 3>
 static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGeom& g, int64_t N, const int64_t* first,
                            const int64_t* view_count, int64_t F, bool ranges, hipStream_t st,
-                           const ShadeParams* S = nullptr) {
+                           const ShadeParams* S = nullptr, FwdParams* Pf = nullptr) {
   ViewBinParams V;
   memset(&V, 0, sizeof(V));
   V.ranges = ranges ? 1 : 0;
@@ -3221,14 +3291,35 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.Fs = F;
     sb = ceil_div(F, 1024);
   }
+  V.nsrec_wg = (int)sb;
   V.T = g.T; V.TX = g.TX; V.mfpb = g.mfpb; V.clipz = SP.clipz;
   V.list_cap = g.list_cap; V.NF = SP.NF;
   V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
   V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
   V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
-  MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<<<(unsigned)(N + sb), 1024, sizeof(int) * (size_t)(g.T + (g.T >> 6)), st>>>(V)));
+  const size_t shm = sizeof(int) * (size_t)(g.T + (g.T >> 6));
+  if constexpr (MODE >= 0) {
+    const int64_t nbg = (int64_t)num_cus() - N - sb;
+    if (Pf && nbg > 0 && (MODE != 0 || Pf->K == 1)) {
+      Pf->fill_first = (int)bg_chunks(N, sb, Pf->H, Pf->W, MODE);
+      MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<MODE, CH><<<(unsigned)(N + sb + nbg), 1024, shm, st>>>(V, *Pf)));
+      MR_CHECK_LAUNCH("k_bin_view");
+      return MR_OK;
+    }
+  }
+  MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<<<(unsigned)(N + sb), 1024, shm, st>>>(V)));
   MR_CHECK_LAUNCH("k_bin_view");
   return MR_OK;
+}
+}  // extern "C++"
+
+int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W, int32_t mode) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  BinGeom g = bin_geom(H, W, N, N * (F > 0 ? F : 1), 0);
+  if (!view_binning(g, N, N * (F > 0 ? F : 1))) return 0;
+  const int64_t sb = mode == 1 ? ceil_div(F, 1024) : 0;
+  const int64_t px = bg_chunks(N, sb, H, W, mode) * ((W & 3) == 0 ? 256 : 64);
+  return std::min<int64_t>(px, N * (int64_t)H * W);
 }
 
 int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const int64_t* count, int64_t N,
@@ -3247,7 +3338,9 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   const bool vpath = view_binning(g, N, Fb);
-  if (hipMemsetAsync(w.ctr, 0, zero_bytes(N, g, vpath), st) != hipSuccess) return set_err(MR_ELAUNCH, "memset failed");
+  // per-view path: k_bin_rect_fv clears the counters
+  if ((!vpath || Ftot == 0) && hipMemsetAsync(w.ctr, 0, zero_bytes(N, g, vpath), st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
   SetupParams SP = make_setup(s, g, w);
   FwdParams P = make_fwd(s, g, w, N, first, 0, Fb);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
@@ -3261,12 +3354,15 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   SP.NF = Fb;
   if (vpath) {
     if (Ftot > 0) {
-      if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<true><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot)));
-      else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot)));
+      if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<true><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, w.ctr)));
+      else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_fv<false><<<ceil_div(Ftot, 256), 256, 0, st>>>(SP, face_verts, Ftot, w.ctr)));
       MR_CHECK_LAUNCH("k_bin_rect_fv");
     }
-    if ((rc = launch_bin_view(SP, w, g, N, first, count, 0, s->faces_per_pixel > 1, st))) return rc;
-    if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
+    if (s->faces_per_pixel > 1) {
+      if ((rc = launch_bin_view(SP, w, g, N, first, count, 0, true, st))) return rc;
+      return launch_raster_k(P, g, N, st);
+    }
+    if ((rc = launch_bin_view<0, 3>(SP, w, g, N, first, count, 0, false, st, nullptr, &P))) return rc;
     return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
   }
   const int fvb = ceil_div(Ftot, 256 * MR_FV_FPT);
@@ -3282,6 +3378,77 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
     MR_CHECK_LAUNCH("k_bin_fill_fv");
   }
   if (s->faces_per_pixel > 1) return launch_raster_k(P, g, N, st);
+  return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
+}
+
+// View records from PyTorch3D poses, and the shared-mesh face ranges (first[n] = n F, count F)
+// the count -> scan fallback of mr_rasterize_meshes_world reads.
+__global__ void __launch_bounds__(256) k_views_from_poses(CvPoses C, int64_t N, int64_t F, int64_t* __restrict__ first,
+                                                          int64_t* __restrict__ count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N * 16) C.out[i] = cv_view_elem(C, i >> 4, (int)(i & 15));
+  if (i < N) {
+    first[i] = i * F;
+    count[i] = F;
+  }
+}
+
+size_t mr_rasterize_meshes_world_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin) {
+  return align_up(mr_rasterize_meshes_workspace(N, N * F, H, W, max_faces_per_bin), 256) +
+         align_up(sizeof(int64_t) * 2 * (size_t)(N > 0 ? N : 1), 256);
+}
+
+// MeshRasterizer.forward of one mesh shared by N views: transform + rasterize. On the per-view
+// binning path the projection happens in k_bin_rect_world (record, tile rectangle and face_verts
+// row of each (view, face) from one thread; the counters cleared by its row 0), so the step is
+// k_bin_rect_world -> k_bin_view -> k_tile_raster -> k_shade<0> with no projection launch, memset
+// or host-side view packing. Else: view records, mr_project_faces, mr_rasterize_meshes.
+int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                  const mr_poses_t* poses, int64_t N, const mr_raster_settings_t* s,
+                                  mr_view_t* views_out, float* face_verts, int64_t* p2f, float* zbuf, float* bary,
+                                  float* dists, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_settings(s);
+  if (rc) return rc;
+  if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N must be in [1, 65535] (got %lld)", (long long)N);
+  if (F < 0 || V < 0 || N * F >= (1ll << 30)) return set_err(MR_EINVAL, "F / V out of range");
+  if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
+  if (!poses || !poses->R || !poses->T || !poses->intr || !views_out || !p2f || !zbuf || !bary || !dists ||
+      (F > 0 && (!verts || !faces || !face_verts)))
+    return set_err(MR_EINVAL, "NULL argument");
+  if (poses->R_stride < 0 || poses->T_stride < 0 || poses->intr_stride < 0) return set_err(MR_EINVAL, "negative stride");
+  const size_t need = mr_rasterize_meshes_world_workspace(N, F, s->H, s->W, s->max_faces_per_bin);
+  if (ws_bytes < need) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
+  hipStream_t st = (hipStream_t)stream;
+  CvPoses C;
+  C.R = poses->R; C.sR = poses->R_stride; C.t = poses->T; C.sT = poses->T_stride;
+  C.intr = poses->intr; C.sI = poses->intr_stride; C.out = (float*)views_out; C.opencv = 0;
+  const int64_t Fb = N * F > 0 ? N * F : 1;
+  BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
+  if (F == 0 || !view_binning(g, N, Fb)) {
+    const size_t rws = align_up(mr_rasterize_meshes_workspace(N, N * F, s->H, s->W, s->max_faces_per_bin), 256);
+    int64_t* first = (int64_t*)((char*)ws + rws);
+    k_views_from_poses<<<ceil_div(N * 16, 256), 256, 0, st>>>(C, N, F, first, first + N);
+    MR_CHECK_LAUNCH("k_views_from_poses");
+    if ((rc = mr_project_faces(verts, V, faces, F, views_out, N, face_verts, stream))) return rc;
+    return mr_rasterize_meshes(face_verts, first, first + N, N, N * F, s, p2f, zbuf, bary, dists, ws, rws, stream);
+  }
+  RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g);
+  SetupParams SP = make_setup(s, g, w);
+  SP.NF = Fb;
+  SP.fv_out = face_verts;
+  FwdParams P = make_fwd(s, g, w, N, nullptr, F, Fb);
+  P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
+  NormalsArgs NA;
+  memset(&NA, 0, sizeof(NA));
+  dim3 rgrid((unsigned)ceil_div(F, 256 * MR_RECT_FPT), (unsigned)N + 1);  // row 0: counter clear
+  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  MR_CHECK_LAUNCH("k_bin_rect_world");
+  if (s->faces_per_pixel > 1) {
+    if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, F, true, st))) return rc;
+    return launch_raster_k(P, g, N, st);
+  }
+  if ((rc = launch_bin_view<0, 3>(SP, w, g, N, nullptr, nullptr, F, false, st, nullptr, &P))) return rc;
   return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
 }
 
@@ -3484,6 +3651,7 @@ int32_t mr_render_forward_opencv(const mr_mesh_t* m, const mr_opencv_poses_t* po
   CvPoses C;
   C.R = poses->R; C.sR = poses->R_stride; C.t = poses->t; C.sT = poses->t_stride;
   C.intr = poses->intr; C.sI = poses->intr_stride; C.out = (float*)views_out;
+  C.opencv = 1;
   return render_forward(m, views_out, N, cc, ncc, s, sp, depth, sil, rgb, p2f32, ws, ws_bytes, stream, C);
 }
 static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
@@ -3535,8 +3703,11 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
     else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
     MR_CHECK_LAUNCH("k_bin_rect_world");
-    if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S))) return rc;
-    if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
+    if (sp->rgb_channels == 4) {
+      if ((rc = launch_bin_view<1, 4>(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S, &P))) return rc;
+      return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
+    }
+    if ((rc = launch_bin_view<1, 3>(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S, &P))) return rc;
     return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
   }
   if (C.R) {  // count -> scan path: the view records first

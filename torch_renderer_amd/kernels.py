@@ -195,6 +195,67 @@ class ProjectFaces(torch.autograd.Function):
         return gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], None, None
 
 
+def _poses_struct(R, T, intr):
+    """mr_poses_t over (N,3,3) R, (N,3) T, (N,4) intr (a batch stride of 0 broadcasts one row);
+    returns the struct and the tensors it points into (keep them alive for the call)."""
+    R, sR = _batch_stride(R.detach().reshape(-1, 3, 3))
+    T, sT = _batch_stride(T.detach().reshape(-1, 3))
+    it, sI = _batch_stride(intr.reshape(-1, 4))
+    sp = _lib.strided_ptr
+    return _lib.MrPoses(sp(R).value, sR, sp(T).value, sT, sp(it).value, sI), (R, T, it)
+
+
+class RasterizeMeshesWorld(torch.autograd.Function):
+    """MeshRasterizer.transform + _RasterizeFaceVerts for one mesh shared by N views, in one
+    native call (mr_rasterize_meshes_world): the projection runs inside the binning's first launch,
+    which also writes face_verts (saved for the backward) and the view records. Results are bitwise
+    those of ProjectFaces.apply followed by RasterizeFaceVerts.apply; the backward is
+    mr_rasterize_meshes_backward followed by mr_project_faces_backward."""
+
+    @staticmethod
+    def forward(ctx, verts, R, T, faces, intr, N, H, W, K, blur, persp, clip, cull, mfpb, z_clip=None):
+        _require_cuda(verts, R, T, faces, intr)
+        L = _lib.load()
+        v = verts.detach().float().contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
+        N, Fn, dev = int(N), f.shape[0], v.device
+        ps, keep = _poses_struct(R, T, intr)
+        s = raster_settings_struct(H, W, K, blur, persp, clip, cull, mfpb, z_clip)
+        views = torch.empty((N, 16), device=dev)
+        fv = torch.empty((N * Fn, 3, 3), device=dev)
+        p2f = torch.empty((N, H, W, K), dtype=torch.int64, device=dev)
+        zbuf = torch.empty((N, H, W, K), dtype=torch.float32, device=dev)
+        bary = torch.empty((N, H, W, K, 3), dtype=torch.float32, device=dev)
+        dists = torch.empty((N, H, W, K), dtype=torch.float32, device=dev)
+        wsb = L.mr_rasterize_meshes_world_workspace(N, Fn, H, W, s.max_faces_per_bin)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        check(L.mr_rasterize_meshes_world(ptr(v), v.shape[0], ptr(f), Fn, ctypes.byref(ps), N, ctypes.byref(s),
+                                          ptr(views), ptr(fv), ptr(p2f), ptr(zbuf), ptr(bary), ptr(dists), ptr(ws),
+                                          wsb, _lib.stream_handle(dev)))
+        del keep
+        ctx.save_for_backward(v, f, views, vptr, vadj, fv, p2f)
+        ctx.cfg = (H, W, K, persp, clip, blur, cull, z_clip)
+        ctx.mark_non_differentiable(p2f)
+        return p2f, zbuf, bary, dists
+
+    @staticmethod
+    def backward(ctx, _gp, gz, gb, gd):
+        v, f, views, vptr, vadj, fv, p2f = ctx.saved_tensors
+        H, W, K, persp, clip, blur, cull, z_clip = ctx.cfg
+        gz = torch.zeros_like(p2f, dtype=torch.float32) if gz is None else gz
+        gb = torch.zeros(p2f.shape + (3,), device=p2f.device) if gb is None else gb
+        gd = torch.zeros_like(p2f, dtype=torch.float32) if gd is None else gd
+        gfv = rasterize_meshes_bwd(fv, p2f, gz, gb, gd, H, W, K, persp, clip, blur, cull, z_clip)
+        L = _lib.load()
+        N = views.shape[0]
+        gv = torch.empty_like(v)
+        gviews = torch.empty((N, 12), device=v.device)
+        check(L.mr_project_faces_backward(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(vptr), ptr(vadj), ptr(views),
+                                          N, ptr(gfv.contiguous()), ptr(gv), ptr(gviews),
+                                          _lib.stream_handle(v.device)))
+        return (gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12]) + (None,) * 12
+
+
 def vertex_normals(verts, faces):
     """(normals, raw sums) — Meshes.verts_normals_packed on the GPU (no autograd)."""
     _require_cuda(verts, faces)

@@ -8,7 +8,8 @@ The reference reaches the render path through PyTorch3D's classes
 argument meaning and outputs:
 
 * ``MeshRasterizer(meshes)`` runs the modular path — ``mr_project_faces`` then
-  ``mr_rasterize_meshes`` (the ``pytorch3d._C.rasterize_meshes`` boundary) — and returns
+  ``mr_rasterize_meshes`` (the ``pytorch3d._C.rasterize_meshes`` boundary), or for one mesh shared
+  by every view both in one call (``mr_rasterize_meshes_world``, bitwise the same) — and returns
   ``Fragments`` in PyTorch3D layout (int64 packed ``pix_to_face`` (N,H,W,K), zbuf, bary_coords,
   dists), differentiable w.r.t. vertex positions and R, T.
 * ``MeshRenderer(meshes)`` with a Soft* shader runs ONE fused launch (project + bin +
@@ -32,7 +33,7 @@ from dataclasses import dataclass
 import torch
 
 from .cameras import CamerasBase, view_batch
-from .kernels import ProjectFaces, RasterizeFaceVerts, ShadeConfig
+from .kernels import ProjectFaces, RasterizeFaceVerts, RasterizeMeshesWorld, ShadeConfig
 from .structures import Meshes
 
 
@@ -199,10 +200,19 @@ class MeshRasterizer(torch.nn.Module):
         cameras = kwargs.get("cameras", self.cameras)
         rs = kwargs.get("raster_settings", self.raster_settings)
         H, W = rs.hw()
-        fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
         _check_cull_to_frustum(rs.cull_to_frustum)
         persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
         clip = rs.blur_radius > 0.0 if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
+        if cameras is not None and meshes.is_shared():
+            # one mesh for every view (Meshes.extend): transform + rasterize in one native call,
+            # bitwise the two-step result below
+            R, T, intr = _views(meshes, cameras, (H, W), kwargs)
+            p2f, zbuf, bary, dists = RasterizeMeshesWorld.apply(
+                meshes.shared_verts(), R, T, meshes.shared_faces(), intr, R.shape[0], H, W,
+                int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
+                rs.max_faces_per_bin, _z_clip_value(cameras, rs))
+            return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+        fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
         first = meshes.mesh_to_faces_packed_first_idx().to(fv.device)
         count = meshes.num_faces_per_mesh().to(fv.device)
         # near-plane clipping (z_clip_value = znear / 2 for FoV cameras) happens inside the HIP

@@ -380,7 +380,9 @@ def bench_fragments(args, dev, world, rank):
                               principal_point=((float(K[0, 2]), float(K[1, 2])),), in_ndc=False,
                               image_size=torch.tensor([[H, W]]), device=dev)
     Rb, Tb, intr = view_batch(cams, (H, W), Rp, Tp, n_views=nv)
-    intr = intr.contiguous()
+    # the poses as a caller holds them (row-major (N,3,3) / (N,3)): opencv_to_pytorch3d returns a
+    # transposed view, whose per-call contiguous copy is input preparation, not the fragment pass
+    Rb, Tb, intr = Rb.contiguous(), Tb.contiguous(), intr.contiguous()
     mesh_topology(faces, verts.shape[0])
 
     def step():  # MeshRasterizer.forward's native call for one mesh shared by the views

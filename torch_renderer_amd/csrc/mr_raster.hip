@@ -147,7 +147,7 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   // max_faces_per_bin (if given) scales the reservation and caps each tile's list (PyTorch3D's per-bin cap).
   int64_t cap = 6 * Ftot + 2 * N * (int64_t)g.T + 65536;
   if (mfpb > 0) cap = (int64_t)mfpb * N * 16 + 65536;
-  g.list_cap = cap;
+  g.list_cap = cap < 0x40000000ll ? cap : 0x40000000ll;  // <= MR_CURSOR_OFF (k_bin_view); tiles past it take the exact path
   g.unit_cap = N * (int64_t)g.T + cap / MR_UE + 1;
   g.mfpb = mfpb > 0 ? mfpb : 0;
   return g;
@@ -860,6 +860,7 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
 #define MR_VIEW_TMAX 16384              // LDS histogram: 64 KB
 #define MR_VIEW_FMAX 65536              // faces per view (mean) above which the count -> scan path is used
 #define MR_RECT_NONE 0x000000ffu        // tx0 = 255 > tx1 = 0: an empty rectangle
+#define MR_CURSOR_OFF 0x40000000        // fill cursor of a tile whose list is not filled (list_cap <= it)
 #define MR_VIEW_RPT 8                   // rectangles per thread per chunk
 #ifndef MR_RECT_FPT
 #define MR_RECT_FPT 1                   // faces per thread of k_bin_rect_world
@@ -928,6 +929,57 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
     return;
   }
+static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
+#if MR_RECT_FPT == 1 && !defined(MR_RECT_NOSTAGE)
+  // One face per thread; the workgroup's records (and face_verts rows) are contiguous in HBM, so
+  // they are staged through LDS and stored as whole lines (each store instruction writes 1 KB of
+  // consecutive bytes instead of 64 lanes' 16-B pieces 64 B apart).
+  __shared__ float4 s4[4 * 256];
+  __shared__ float s9[9 * 256];
+  {
+    const int t = threadIdx.x;
+    const int64_t fb = (int64_t)blockIdx.x * 256;
+    const int64_t f = fb + t;
+    const int nf = (int)(F - fb < 256 ? F - fb : 256);
+    const int64_t rid0 = (int64_t)n * F + fb;
+    if (f < F) {
+      float v[3][3];
+      ViewRec V;
+      if (C.R) {
+        float* e = (float*)&V;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) e[k] = cv_view_elem(C, n, k);
+      } else {
+        V = views[n];
+      }
+      world_face_verts(verts, faces, f, V, v);
+      const int64_t rid = rid0 + t;
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) s9[9 * t + 3 * c + q] = v[c][q];
+      FaceRec r2;
+      const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
+      float4 q4[4];
+      __builtin_memcpy(q4, &r, sizeof(q4));
+#pragma unroll
+      for (int q = 0; q < 4; ++q) s4[4 * t + q] = q4[q];
+      P.rects[rid] = rec_rect(P, r);
+      if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
+    }
+    __syncthreads();
+    float4* d4 = (float4*)(P.recs + rid0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j * 256 + t < 4 * nf) d4[j * 256 + t] = s4[j * 256 + t];
+    if (P.fv_out) {
+      float* d9 = P.fv_out + rid0 * 9;
+#pragma unroll
+      for (int j = 0; j < 9; ++j)
+        if (j * 256 + t < 9 * nf) d9[j * 256 + t] = s9[j * 256 + t];
+    }
+  }
+#else
 #pragma unroll
   for (int k = 0; k < MR_RECT_FPT; ++k) {
     const int64_t f = ((int64_t)blockIdx.x * MR_RECT_FPT + k) * blockDim.x + threadIdx.x;
@@ -956,6 +1008,7 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     P.rects[rid] = rec_rect(P, r);
     if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
   }
+#endif
 }
 
 // face_verts mode (record = packed face id): the workgroup's face_verts staged through LDS
@@ -1081,12 +1134,16 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int iu = block_incl_sum(my_u, part, au);
   const int is = block_incl_sum(my_s, part, as);
   PROF_B(60000 + n, 2);
+  // the three allocations from three waves: their round trips overlap instead of queueing
   if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
-    base[1] = atomicAdd(&P.ctr[CTR_SLOTS], as);
-    base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
-    P.vslot[n] = (int)base[1];
+  } else if (t == 64) {
+    const int b1 = atomicAdd(&P.ctr[CTR_SLOTS], as);
+    base[1] = b1;
+    P.vslot[n] = b1;
     P.vslot[P.nviews + n] = as;
+  } else if (t == 128) {
+    base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
   }
   __syncthreads();
   PROF_B(60000 + n, 3);
@@ -1122,7 +1179,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       else
         for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
     }
-    hist[tt + (tt >> 6)] = ovf ? 0x7fffffff : (int)(vb + ex);  // fill cursor (overflowing lists are not filled)
+    hist[tt + (tt >> 6)] = ovf ? MR_CURSOR_OFF : (int)(vb + ex);  // fill cursor (overflowing lists are not filled)
     u0 += nu;
     slot += cc > 0 ? 1 : 0;
     ex += cc;
@@ -1142,11 +1199,10 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       for (int q = 0; q < 2; ++q) {
         const int rid = (int)((q ? P.NF : 0) + f0 + i0 + k * 1024 + j);
         rect_tiles(rr[k][q], P.TX, [&](int tt) {
-          int* h = &hist[tt + (tt >> 6)];
-          if (*h != 0x7fffffff) {
-            const int pos = atomicAdd(h, 1);
-            if (pos < P.list_cap) P.list[pos] = rid;
-          }
+          // an overflowing tile's cursor starts at MR_CURSOR_OFF >= list_cap: no store, and no
+          // read of the cursor before the atomic
+          const int pos = atomicAdd(&hist[tt + (tt >> 6)], 1);
+          if (pos < P.list_cap) P.list[pos] = rid;
         });
       }
   }

@@ -304,17 +304,24 @@ MR_DEV void wave_lds_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS (and scalar) operations,
+// not for its global stores (a __syncthreads waits vmcnt(0) too, i.e. a full memory round trip
+// of every store in flight — expensive while other workgroups saturate HBM).
+MR_DEV void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // Inclusive scan over a 1024-thread workgroup (16 waves): DPP inside each wave, then the
 // 16 wave totals scanned by every wave from LDS. `tot` = workgroup total. Uniform call only.
+// LDSB: LDS-only barriers (the caller's global stores may stay in flight).
+template <bool LDSB = false>
 MR_DEV int block_incl_sum(int v, int* part16, int& tot) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int w = wave_incl_sum(v);
   if (lane == 63) part16[wave] = w;
-  __syncthreads();
+  if (LDSB) lds_barrier(); else __syncthreads();
   const int ws = wave_incl_sum(lane < 16 ? part16[lane] : 0);
   tot = __builtin_amdgcn_readlane(ws, 15);
   const int before = __shfl(ws, wave > 0 ? wave - 1 : 0, 64);
-  __syncthreads();  // part16 is reused by the next call
+  if (LDSB) lds_barrier(); else __syncthreads();  // part16 is reused by the next call
   return w + (wave > 0 ? before : 0);
 }
 
@@ -1061,6 +1068,7 @@ struct ViewBinParams {
   ShadeRec* srec;
   int64_t Fs;
   int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
+  int stage_cap;  // list entries of a view staged in LDS (after the histogram)
 };
 
 template <typename Fn>
@@ -1095,7 +1103,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   for (int i = t; i < P.T + (P.T >> 6); i += 1024) hist[i] = 0;
   if (t == 0) nmulti = 0;
-  __syncthreads();
+  lds_barrier();
   const int nq = P.clipz ? 2 : 1;
   uint32_t rr[MR_VIEW_RPT][2];
   auto load_chunk = [&](int i0) {
@@ -1116,7 +1124,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
   }
-  __syncthreads();
+  lds_barrier();
   PROF_B(60000 + n, 1);
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
   const int C = (P.T + 1023) / 1024;
@@ -1130,9 +1138,9 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     my_s += cc > 0 ? 1 : 0;
   }
   int te, au, as;
-  const int ex0 = block_incl_sum(le, part, te) - le;
-  const int iu = block_incl_sum(my_u, part, au);
-  const int is = block_incl_sum(my_s, part, as);
+  const int ex0 = block_incl_sum<true>(le, part, te) - le;
+  const int iu = block_incl_sum<true>(my_u, part, au);
+  const int is = block_incl_sum<true>(my_s, part, as);
   PROF_B(60000 + n, 2);
   // the three allocations from three waves: their round trips overlap instead of queueing
   if (t == 0) {
@@ -1145,7 +1153,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   } else if (t == 128) {
     base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
   }
-  __syncthreads();
+  lds_barrier();
   PROF_B(60000 + n, 3);
   const long long vb = base[2];
   if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
@@ -1184,11 +1192,15 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     slot += cc > 0 ? 1 : 0;
     ex += cc;
   }
-  __syncthreads();
+  lds_barrier();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
   PROF_B(60000 + n, 4);
-  // fill
+  // fill: the view's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
+  // staged in LDS and stored as consecutive lines afterwards (scattered 4-B stores issue one
+  // lane per cycle), the rest (a view larger than the stage) go straight to the pool
+  int* stage = hist + ((P.T + (P.T >> 6) + 3) & ~3);
+  const int lst = min(te, P.stage_cap);
   const bool one = vcount <= 1024 * MR_VIEW_RPT;  // the rectangles are still in registers
 #pragma unroll 1
   for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
@@ -1202,10 +1214,17 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
           // an overflowing tile's cursor starts at MR_CURSOR_OFF >= list_cap: no store, and no
           // read of the cursor before the atomic
           const int pos = atomicAdd(&hist[tt + (tt >> 6)], 1);
-          if (pos < P.list_cap) P.list[pos] = rid;
+          if (pos < P.list_cap) {
+            const int rel = (int)(pos - vb);
+            if (rel < lst) stage[rel] = rid;
+            else P.list[pos] = rid;
+          }
         });
       }
   }
+  lds_barrier();
+  for (int i = t; i < lst; i += 1024)
+    if (vb + i < P.list_cap) P.list[vb + i] = stage[i];
 #ifdef MR_PROF
   __syncthreads();
 #endif
@@ -3312,6 +3331,19 @@ extern "C++" {
 #ifndef MR_BG_CPW_FRAG
 #define MR_BG_CPW_FRAG 4    // 7 KB chunks (PyTorch3D fragments)
 #endif
+#ifndef MR_VIEW_LDS
+#define MR_VIEW_LDS 98304  // k_bin_view's LDS: the tile histogram + the list stage
+#endif
+static size_t view_lds_bytes() {
+  static size_t b = 0;
+  if (!b) {
+    int dev = 0, mx = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&mx, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || mx <= 0) mx = 65536;
+    b = std::min<size_t>((size_t)mx, MR_VIEW_LDS);
+  }
+  return b;
+}
 static int num_cus() {
   static int cus = 0;
   if (!cus) {
@@ -3353,7 +3385,9 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
   V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
   V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
   V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
-  const size_t shm = sizeof(int) * (size_t)(g.T + (g.T >> 6));
+  const size_t hist_b = sizeof(int) * (size_t)((g.T + (g.T >> 6) + 3) & ~3);
+  const size_t shm = std::max(hist_b, view_lds_bytes());
+  V.stage_cap = (int)((shm - hist_b) / sizeof(int));
   if constexpr (MODE >= 0) {
     const int64_t nbg = (int64_t)num_cus() - N - sb;
     if (Pf && nbg > 0 && (MODE != 0 || Pf->K == 1)) {

@@ -40,7 +40,11 @@ def main():
     cfg = Kn.ShadeConfig(H=H, W=W)
     nw = 1 << 16
     buf = torch.zeros(nw * 8, dtype=torch.int64, device=dev)
-    run = lambda: Kn.render_views(v, R, T, f, intr, torch.zeros(1, 3, device=dev), cfg, tex)  # noqa: E731
+    if len(sys.argv) > 1 and sys.argv[1] == "frag":  # the fragment pass (mr_rasterize_meshes_world)
+        run = lambda: Kn.RasterizeMeshesWorld.apply(v, R.contiguous(), T.contiguous(), f, intr, N, H, W, 1, 0.0,  # noqa: E731
+                                                    True, False, False, None)
+    else:
+        run = lambda: Kn.render_views(v, R, T, f, intr, torch.zeros(1, 3, device=dev), cfg, tex)  # noqa: E731
     run()
     torch.cuda.synchronize()
     _lib.check(L.mr_debug_set_prof(buf.data_ptr()))

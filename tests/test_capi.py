@@ -74,3 +74,25 @@ def test_struct_layouts_match_header():
 def test_missing_library_raises(tmp_path):
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_world_rasterizer_validation_and_workspace(lib):
+    """mr_rasterize_meshes_world (MeshRasterizer.forward for an extended mesh): host-side checks
+    fail with a status and a message before any device work; its workspace covers the modular
+    rasterizer's plus the shared-mesh face ranges."""
+    s = _lib.MrRasterSettings()
+    s.H, s.W, s.faces_per_pixel, s.blur_radius = 64, 64, 1, 0.0
+    ps = _lib.MrPoses(None, 0, None, 0, None, 0)
+    rc = lib.mr_rasterize_meshes_world(None, 10, None, 10, ctypes.byref(ps), 2, ctypes.byref(s), None, None,
+                                       None, None, None, None, None, 0, None)
+    assert rc == 1 and b"NULL" in lib.mr_last_error()
+    rc = lib.mr_rasterize_meshes_world(None, 10, None, 10, ctypes.byref(ps), 0, ctypes.byref(s), None, None,
+                                       None, None, None, None, None, 0, None)
+    assert rc == 1 and b"N must be" in lib.mr_last_error()
+    s.faces_per_pixel = 0
+    rc = lib.mr_rasterize_meshes_world(None, 10, None, 10, ctypes.byref(ps), 2, ctypes.byref(s), None, None,
+                                       None, None, None, None, None, 0, None)
+    assert rc == 3
+    w = lib.mr_rasterize_meshes_world_workspace(64, 5856, 512, 512, 0)
+    assert w >= lib.mr_rasterize_meshes_workspace(64, 64 * 5856, 512, 512, 0) + 16 * 64
+    assert ctypes.sizeof(_lib.MrPoses) == ctypes.sizeof(_lib.MrOpencvPoses) == 48

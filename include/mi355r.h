@@ -77,7 +77,12 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
        /* with MR_OUT_RGB, mr_shade_fragments_* only: upstream hard_rgb_blend (HardPhongShader) —
         * the nearest fragment's Phong colour or the background, alpha = 1 where a face covers the
         * pixel; gradients reach the colour of the nearest fragment only */
-       MR_OUT_HARD = 8 };
+       MR_OUT_HARD = 8,
+       /* mr_render_backward[_opencv] only: the forward workspace's face-gradient rows are as the
+        * forward left them (cleared), i.e. this is the first backward over that forward; the
+        * backward then skips clearing them. Leave it unset for any later backward over the same
+        * forward workspace (e.g. autograd retain_graph). */
+       MR_GRAD_ROWS_CLEARED = 16 };
 
 /* One triangle mesh shared by all N views (Meshes.extend(N)). */
 typedef struct mr_mesh {

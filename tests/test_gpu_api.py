@@ -340,3 +340,27 @@ def test_soft_raster_distinct_meshes_batch_equals_single_renders():
         (one * go[i:i + 1]).sum().backward()
         _close(img[i:i + 1], one, tol=1e-6)
         _close(vb[i].grad, vs.grad, tol=1e-5)
+
+
+def test_second_backward_over_one_forward_accumulates_exactly():
+    """The fused backward accumulates its per-face gradient rows in the forward's workspace, which
+    the forward clears (MR_GRAD_ROWS_CLEARED on the first backward). A second backward over the same
+    forward (retain_graph) must clear them again: it yields the same gradients as the first."""
+    verts, faces, _ = mesh_arrays("cow")
+    H = W = 96
+    N = 3
+    R_cv, t_cv, K = canonical_views(verts, N, H, W)[3]
+    vg = verts.to(DEV).requires_grad_(True)
+    m = Meshes([vg], [faces.to(DEV)], TexturesVertex([torch.ones_like(vg).detach()])).extend(N)
+    Rg = R_cv.float().to(DEV).requires_grad_(True)
+    tg = t_cv.float().to(DEV).requires_grad_(True)
+    d, s, c = DepthColorRender(K.to(DEV), (H, W), device=DEV).render(m, Rg, tg)
+    g = torch.Generator(device=DEV).manual_seed(3)
+    gd, gs, gc = (torch.rand(x.shape, generator=g, device=DEV) - 0.5 for x in (d, s, c))
+    torch.autograd.backward([d, s, c], [gd, gs, gc], retain_graph=True)
+    first = [x.grad.clone() for x in (vg, Rg, tg)]
+    for x in (vg, Rg, tg):
+        x.grad = None
+    torch.autograd.backward([d, s, c], [gd, gs, gc])
+    for a, b, nm in zip((vg.grad, Rg.grad, tg.grad), first, ("verts", "R", "t")):
+        report(f"second backward {nm}", a.cpu(), b.cpu())

@@ -24,6 +24,7 @@ MR_OUT_DEPTH = 1
 MR_OUT_SIL = 2
 MR_OUT_RGB = 4
 MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
+MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
 
 
 class MrView(ctypes.Structure):

@@ -170,6 +170,7 @@ struct RasterWS {
   unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
   int* sface;  // (N*T*64) per slot, per tile pixel (row-major 8x8): winning face record or -1
   ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
+  float* grows;    // (F, 27) the fused backward's per-face gradient rows, cleared by the forward
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
   size_t bytes;
 };
@@ -212,6 +213,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * 64 * NT, 256);
   w.srec = (ShadeRec*)(b + off);
   off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
+  w.grows = (float*)(b + off);
+  off = align_up(off + sizeof(float) * 27 * (size_t)Fshade, 256);
   w.crec = (ClipRec*)(b + off);
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.bytes = off;
@@ -894,6 +897,8 @@ struct NormalsArgs {
   const int32_t* adj;
   float* vn;    // NULL: no normals to compute
   float* vraw;
+  float4* zero4;   // the fused backward's face-gradient rows, cleared here (nzero4 float4s; NULL: none)
+  int64_t nzero4;
 };
 // OpenCV poses converted on the fly (mr_render_forward_opencv): element k of view n's record,
 // as k_views_from_opencv writes it (torch_renderer.py:73-80; bitwise the torch conversion).
@@ -933,6 +938,7 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
   if (n < 0) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
+    for (int64_t i = v; i < NA.nzero4; i += (int64_t)gridDim.x * blockDim.x) NA.zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
     return;
   }
@@ -3788,6 +3794,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     NA.V = m->V; NA.ptr = m->vadj_ptr; NA.adj = m->vadj;
     NA.vn = vb ? m->vnormals_out : nullptr;
     NA.vraw = m->vraw_out;
+    NA.zero4 = (float4*)w.grows;
+    NA.nzero4 = (27 * m->F + 3) / 4;
     const int64_t bx = std::max<int64_t>(ceil_div(m->F, 256 * MR_RECT_FPT), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
     if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
@@ -3800,6 +3808,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     if ((rc = launch_bin_view<1, 3>(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S, &P))) return rc;
     return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
   }
+  if (hipMemsetAsync(w.grows, 0, sizeof(float) * 27 * (size_t)m->F, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
   if (C.R) {  // count -> scan path: the view records first
     k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C.R, C.sR, C.t, C.sT, C.intr, C.sI, N, C.out);
     MR_CHECK_LAUNCH("k_views_from_opencv");
@@ -3828,8 +3838,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
   const int64_t NT = N * (int64_t)ceil_div(W, MR_TS) * ceil_div(H, MR_TS);
-  size_t off = align_up(sizeof(float) * 27 * (size_t)F, 256);                 // gface
-  off = align_up(off + sizeof(float) * 3 * (size_t)V, 256);                    // gnu
+  (void)F;  // the face-gradient rows are in the forward's workspace
+  size_t off = align_up(sizeof(float) * 3 * (size_t)V, 256);                   // gnu
   off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);                  // rt_part
   return off;
 }
@@ -3883,12 +3893,14 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   const int64_t NT = N * (int64_t)g.T;
   char* b = (char*)bws;
   size_t off = 0;
-  float* gface = (float*)(b + off);
-  off = align_up(sizeof(float) * 27 * (size_t)m->F, 256);
   float* gnu = (float*)(b + off);
   off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
   float* rt_part = (float*)(b + off);
-  if (hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
+  // the per-face gradient rows live in the forward's workspace, which the forward cleared; a
+  // second backward over the same forward (MR_GRAD_ROWS_CLEARED not set) clears them again
+  float* gface = w.grows;
+  if (!(sp->out_flags & MR_GRAD_ROWS_CLEARED) &&
+      hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
   memset(&P, 0, sizeof(P));

@@ -450,6 +450,9 @@ class RenderViews(torch.autograd.Function):
         mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None)
         rs = cfg2.raster_struct()
         sp = cfg2.shade_struct()
+        if not getattr(ctx, "rows_used", False):  # the forward cleared the face-gradient rows in ws
+            sp.out_flags |= _lib.MR_GRAD_ROWS_CLEARED
+            ctx.rows_used = True
         gverts = torch.empty_like(v)
         gviews = torch.empty((N, 12), device=dev)
         gcol = torch.empty_like(v) if ctx.has_vcol else None

@@ -59,6 +59,9 @@ def allreduce_grads(params, group=None):
     grads = [p.grad for p in params if p is not None and p.grad is not None]
     if w == 1 or not grads:
         return
+    if len(grads) == 1 and grads[0].is_contiguous():  # one bucket already: reduce in place (no copies)
+        dist.all_reduce(grads[0], op=dist.ReduceOp.SUM, group=group)
+        return
     flat = torch.cat([g.reshape(-1) for g in grads])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     off = 0

@@ -34,10 +34,14 @@ def _worker(rank, world, port, n_total, q):
         c = torch.zeros(5, requires_grad=True)
         ((v * (rank + 1)).sum() + (c * (rank + 2)).sum()).backward()
         D.allreduce_grads([v, c, None])
+        # a single contiguous gradient takes the in-place path
+        u = torch.zeros(4, 3, requires_grad=True)
+        (u * (rank + 4)).sum().backward()
+        D.allreduce_grads([u])
         got = D.gather_to_root(local, n_total)
         # numpy arrays pickle by value: torch tensors would travel as shared-memory fds that
         # the parent may fail to receive once this worker has exited
-        res = {"v": v.grad.numpy().copy(), "c": c.grad.numpy().copy(), "range": (s, e),
+        res = {"v": v.grad.numpy().copy(), "c": c.grad.numpy().copy(), "u": u.grad.numpy().copy(), "range": (s, e),
                "gather": None if got is None else got.numpy().copy()}
         q.put((rank, res))
     finally:
@@ -65,6 +69,7 @@ def test_gloo_world2_shard_allreduce_gather(n_total):
     for r in range(world):
         assert torch.equal(torch.from_numpy(res[r]["v"]), torch.full((7, 3), 3.0))
         assert torch.equal(torch.from_numpy(res[r]["c"]), torch.full((5,), 5.0))
+        assert torch.equal(torch.from_numpy(res[r]["u"]), torch.full((4, 3), 9.0))
     assert torch.equal(torch.from_numpy(res[0]["gather"]), full * 2.0)
     assert res[1]["gather"] is None
 

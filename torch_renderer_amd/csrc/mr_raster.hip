@@ -2627,11 +2627,22 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
   __shared__ float sm[12][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int s0 = vslot[n], ns = vslot[N + n];
+  // each thread sums whole 48-B partial rows (three 16-B loads in flight together instead of 12
+  // dependent passes over the rows); per component the order is the same as a per-component loop
+  float acc[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
+  for (int t = threadIdx.x; t < ns; t += 256) {
+    const float4* q = (const float4*)(part + ((int64_t)s0 + t) * 12);
+    const float4 a = q[0], b = q[1], c = q[2];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+  }
+#pragma unroll
   for (int i = 0; i < 12; ++i) {
-    float v = 0.0f;
-    for (int t = threadIdx.x; t < ns; t += 256) v += part[((int64_t)s0 + t) * 12 + i];
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    if (lane == 0) sm[i][wave] = v;
+    for (int o = 32; o > 0; o >>= 1) acc[i] += __shfl_xor(acc[i], o, 64);
+    if (lane == 0) sm[i][wave] = acc[i];
   }
   __syncthreads();
   const int i = threadIdx.x;

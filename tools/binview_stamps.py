@@ -34,7 +34,11 @@ def main():
     tex, _ = texture_args(m, True) if m.textures is not None else (None, None)
     cfg = Kn.ShadeConfig(H=H, W=W)
     buf = torch.zeros(65536 * 8, dtype=torch.int64, device=dev)
-    run = lambda: Kn.render_views(v, R, T, f, intr, torch.zeros(1, 3, device=dev), cfg, tex)  # noqa: E731
+    if len(sys.argv) > 3 and sys.argv[3] == "frag":  # the fragment pass (mr_rasterize_meshes_world)
+        run = lambda: Kn.RasterizeMeshesWorld.apply(v, R.contiguous(), T.contiguous(), f, intr, N, H, W, 1, 0.0,  # noqa: E731
+                                                    True, False, False, None)
+    else:
+        run = lambda: Kn.render_views(v, R, T, f, intr, torch.zeros(1, 3, device=dev), cfg, tex)  # noqa: E731
     run()
     torch.cuda.synchronize()
     _lib.check(L.mr_debug_set_prof(buf.data_ptr()))

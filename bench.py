@@ -181,11 +181,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    # one GPU per rank; MR_BENCH_REHEARSE=1 (tests only) lets several ranks share the visible GPUs
+    # over gloo to rehearse the N-rank path on a 1-GPU box; the measured runs use RCCL
+    rehearse = os.environ.get("MR_BENCH_REHEARSE") == "1"
+    local = local % torch.cuda.device_count() if rehearse else local
     torch.cuda.set_device(local)  # before the process group: RCCL binds its communicator to this device
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo" if rehearse else "nccl")
 
     if args.mode == "fragments":
         return bench_fragments(args, dev, world, rank)

@@ -171,7 +171,7 @@ def main():
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
     ap.add_argument("--texture", choices=("uv", "white"), default="uv",
                     help="experiments only: 'white' drops the UV texture (not the benchmark workload)")
-    ap.add_argument("--mode", choices=("render", "fragments"), default="render",
+    ap.add_argument("--mode", choices=("render", "fragments", "soft"), default="render",
                     help="render: the headline fwd+bwd step; fragments: the rasterizer alone "
                          "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline)")
     args = ap.parse_args()
@@ -193,6 +193,8 @@ def main():
 
     if args.mode == "fragments":
         return bench_fragments(args, dev, world, rank)
+    if args.mode == "soft":
+        return bench_soft(args, dev, world, rank)
     from torch_renderer_amd import _lib
     from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset, load_asset_arrays
@@ -443,6 +445,95 @@ def bench_fragments(args, dev, world, rank):
                               "step_frac": round(value * per_frame / 1e9 / HBM_PEAK_GBS, 4),
                               "dominant_kernel": dom[0]},
         "work": {"covered": covered}, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_soft(args, dev, world, rank):
+    """Soft rasterization: the silhouette renderer of deform_mesh_with_color.py:
+    153-165 — MeshRenderer(MeshRasterizer(faces_per_pixel=50, blur_radius=ln(1/1e-4 - 1)·1e-4,
+    perspective_correct=False), SoftSilhouetteShader) on the normalised cow (:106-111), PerspectiveCameras
+    (focal 1, NDC) at look_at_view_transform(2.7, elev, azim) (:118-127), 128x128 (--size), fwd + bwd of a
+    silhouette loss to the vertex positions. Not the headline metric: a measured point for the K-deep path."""
+    from torch_renderer_amd import _lib
+    from torch_renderer_amd import distributed as D
+    from torch_renderer_amd.assets import load_asset
+    from torch_renderer_amd.cameras import PerspectiveCameras
+    from torch_renderer_amd.mesh_renderer import (BlendParams, MeshRasterizer, MeshRenderer, RasterizationSettings,
+                                                  SoftSilhouetteShader)
+    from torch_renderer_amd.structures import Meshes
+    from torch_renderer_amd.transforms import look_at_view_transform
+
+    H = W = args.size
+    K = 50
+    m = load_asset(args.mesh, device=dev, textures=False)
+    v0 = m.shared_verts().detach()
+    c = v0.mean(0)
+    sc = (v0 - c).abs().max()
+    verts = ((v0 - c) / sc).clone().requires_grad_(True)
+    faces = m.shared_faces()
+    nv = args.views
+    n_total = nv * world
+    elev = torch.linspace(0, 360, n_total)[rank * nv:(rank + 1) * nv]
+    azim = torch.linspace(-180, 180, n_total)[rank * nv:(rank + 1) * nv]
+    R, T = look_at_view_transform(dist=2.7, elev=elev, azim=azim)
+    R, T = R.to(dev).contiguous(), T.to(dev).contiguous()
+    cams = PerspectiveCameras(device=dev, R=R, T=T)
+    sigma = 1e-4
+    rs = RasterizationSettings(image_size=H, blur_radius=math.log(1.0 / 1e-4 - 1.0) * sigma, faces_per_pixel=K,
+                               perspective_correct=False)
+    renderer = MeshRenderer(rasterizer=MeshRasterizer(cameras=cams, raster_settings=rs),
+                            shader=SoftSilhouetteShader(blend_params=BlendParams(sigma=sigma)))
+    gen = torch.Generator().manual_seed(1 + rank)
+    target = (torch.rand(nv, H, W, generator=gen) > 0.5).float().to(dev)
+
+    def step():
+        verts.grad = None
+        img = renderer(Meshes([verts], [faces]).extend(nv), cameras=cams, R=R, T=T)
+        ((img[..., 3] - target) ** 2).mean().backward()
+        if world > 1:
+            D.allreduce_grads([verts])
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    _lib.timing_enable(True)
+    for _ in range(min(args.steps, 10)):
+        step()
+    torch.cuda.synchronize()
+    kt = _lib.timing_read()
+    _lib.timing_enable(False)
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    value = nv * world * args.steps / elapsed
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    line = {
+        "metric": f"frames/sec fwd+bwd, soft silhouette K={K}, {H}x{W} (deform_mesh_with_color.py)",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "launch": "eager", "data": "synthetic views of the reference mesh",
+        "config": {"workload": f"{args.mesh} (F={faces.shape[0]}) normalised, {H}x{W}, {nv} views/GPU, K={K}, "
+                               "blur=ln(1/1e-4-1)*1e-4, perspective_correct=False, SoftSilhouetteShader, "
+                               "L2 silhouette loss -> vertex grads",
+                   "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "K": K, "parallelism": f"view-sharded x{world}"},
+        "kernels": kernels,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -2068,12 +2068,141 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
   }
 }
 
+// K <= 64: the same per-tile raster with each lane's K nearest keys in REGISTERS (KP >= K slots,
+// ascending), merged by a compare-exchange network instead of a per-lane LDS insertion loop. The
+// LDS version runs one dependent LDS read / write per shifted entry, every lane waiting for the
+// longest shift of the wave, at one or two waves per SIMD (K * 512 B of LDS per wave); the network
+// is KP unconditional min / max steps of straight VALU, run only when some lane's candidate beats
+// its current KP-th key, and the keys need no LDS (only the staged face records). The KP smallest
+// keys contain the K smallest, so the output (the first K, ascending) is the same.
+template <int KP>
+__global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
+  __shared__ FaceRec srs[4][64];
+  __shared__ int sids[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  FaceRec* rs = srs[wave];
+  int* ids = sids[wave];
+  const int K = P.K;
+  const int nslots = P.ctr[CTR_SLOTS];
+  const float pad = P.bbox_pad, blur = P.blur;
+  const bool persp = P.persp != 0, clipb = P.clipb != 0;
+  const bool fast_ok = !(blur > 0.0f);
+  const int H = P.H, W = P.W;
+  const int64_t HW = (int64_t)H * W;
+#pragma unroll 1
+  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
+    const int gt = P.stile[s];
+    const int n = gt / P.T, t = gt - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
+    const bool in_img = px < W && py < H;
+    const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
+    const int cc = P.cnt[gt], ex = P.start[gt];
+    const int64_t vb = P.vbase[n];
+    const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
+    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
+    const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
+    const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
+    unsigned long long q[KP];
+#pragma unroll
+    for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
+#pragma unroll 1
+    for (int eb = 0; eb < count; eb += 64) {
+      const int e = eb + lane;
+      if (e < count) {
+        const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
+        rs[lane] = P.recs[id];
+        ids[lane] = id;
+      }
+      wave_lds_sync();
+      const int m = count - eb < 64 ? count - eb : 64;
+      auto cand = [&](int jj) -> unsigned long long {  // the key of staged face jj at this lane's pixel
+        const FaceRec r = rs[jj];
+        const int id = ids[jj];
+        float pz;
+        int cid = id;
+        bool keep = false;
+        if (in_img && (r.flags & FR_PAIR)) {  // as k_raster_k
+          keep = pair_keep(P.recs, P.NF, id, r, xf, yf, pad, blur, persp, clipb, cid, pz) &&
+                 (cid == id || (ovf && id < P.NF));
+        } else if (in_img && (r.flags & FR_VALID)) {
+          keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
+        }
+        return keep ? frag_key(pz, (int)rec_code(cid, P.NF)) : MR_KEY_EMPTY;
+      };
+      auto insert = [&](unsigned long long key) {
+        if (__ballot(key < q[KP - 1]) != 0ull) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k) {
+            const unsigned long long a = q[k];
+            const bool lt = key < a;
+            q[k] = lt ? key : a;
+            key = lt ? a : key;
+          }
+        }
+      };
+#pragma unroll 1
+      for (int j = 0; j < m; ++j) insert(cand(j));
+      wave_lds_sync();
+    }
+    if (!in_img) continue;
+    const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
+    // the keys leave in ascending order through q[0], the array shifting down one slot per step:
+    // only constant indices into q[] (a dynamic index would demote the array to scratch), and the
+    // output body (eval_face) is not unrolled KP times
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+      const unsigned long long key = q[0];
+#pragma unroll
+      for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
+      q[KP - 1] = MR_KEY_EMPTY;
+      int64_t f = -1;
+      float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
+      if (key < MR_KEY_EMPTY) {
+        const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
+        const FaceRec r = P.recs[id];
+        FragEval ev;
+        eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
+        if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+        f = rec_orig(id, P.NF); z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
+      }
+      P.p2f[pix + k] = f;
+      P.zbuf[pix + k] = z;
+      P.dists[pix + k] = d;
+      P.bary[3 * (pix + k) + 0] = b0;
+      P.bary[3 * (pix + k) + 1] = b1;
+      P.bary[3 * (pix + k) + 2] = b2;
+    }
+  }
+}
+
+template <int KP>
+static void launch_raster_kr(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
+  const int64_t want = (slots_cap + 3) / 4;
+  const int grid = (int)(want < 8192 ? want : 8192);
+  MR_TIMED(KID_RASTER_K, st, (k_raster_kr<KP><<<grid, 256, 0, st>>>(P)));
+}
+
 static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
   static int fgrid = 0;
   if (!fgrid) fgrid = resident_grid(k_fill<0, 3>, 256, 8);
   MR_TIMED(KID_FILL_FRAG, st, (k_fill<0, 3><<<fgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_fill");
   const int K = P.K;
+#ifndef MR_RASTER_K_LDS
+  if (K <= 64) {  // keys in registers (k_raster_kr)
+    const int64_t sc = N * (int64_t)g.T;
+    if (K <= 4) launch_raster_kr<4>(P, sc, st);
+    else if (K <= 8) launch_raster_kr<8>(P, sc, st);
+    else if (K <= 16) launch_raster_kr<16>(P, sc, st);
+    else if (K <= 32) launch_raster_kr<32>(P, sc, st);
+    else if (K <= 50) launch_raster_kr<50>(P, sc, st);
+    else launch_raster_kr<64>(P, sc, st);
+    MR_CHECK_LAUNCH("k_raster_kr");
+    return MR_OK;
+  }
+#endif
   const size_t wb = (size_t)K * 64 * 8 + 64 * sizeof(FaceRec) + 64 * sizeof(int);
   const int wpg = wb * 4 <= 65536 ? 4 : wb * 2 <= 65536 ? 2 : 1;
   const int64_t slots_cap = N * (int64_t)g.T;

@@ -2301,6 +2301,77 @@ struct RasterBwdParams {
   float* gfv;
 };
 
+// One stored fragment (pixel px, py; slot pix; packed face f) of the modular raster backward:
+// the 9 face_verts gradients of face f in g.
+MR_DEV void raster_bwd_fragment(const RasterBwdParams& P, int px, int py, int64_t pix, int64_t f, float (&g)[3][3]) {
+  FaceRec r;
+  const float* v = P.fv + 9 * f;
+  r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
+  r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
+  r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
+  r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
+  const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
+  const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
+  int ci = 0;
+  const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};
+  const int nb = P.clipz ? clip_class(vv, P.zc, ci) : 0;
+  if (nb == 1 || nb == 2) {
+    // the face was split at the near plane: rebuild its sub-triangle(s) exactly as the forward
+    // binning did, pick the one that produced this fragment (the forward's pair rule), and chain
+    for (int c = 0; c < 3; ++c)
+      for (int q = 0; q < 3; ++q) g[c][q] = 0.0f;
+    float sv[3][3];
+    ClipRec cr0, cr1;
+    clip_sub(vv, nb, ci, 0, P.zc, P.persp != 0, sv, cr0);
+    FaceRec r0 = make_rec_core(P.cull, P.persp, 0u, sv);
+    int use = 0;
+    FaceRec r1;
+    if (nb == 1) {
+      clip_sub(vv, nb, ci, 1, P.zc, P.persp != 0, sv, cr1);
+      r1 = make_rec_core(P.cull, P.persp, 0u, sv);
+      FragEval e0, e1;
+      const bool k0 = (r0.flags & FR_VALID) && eval_face(r0, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e0);
+      const bool k1 = (r1.flags & FR_VALID) && eval_face(r1, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e1);
+      use = (k0 && k1) ? (fabsf(e1.sdist) < fabsf(e0.sdist) ? 1 : 0) : (k1 ? 1 : 0);
+    }
+    const FaceRec& rs = use ? r1 : r0;
+    const ClipRec& cr = use ? cr1 : cr0;
+    FragEval es;
+    eval_face(rs, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, es);
+    const float bs[3] = {es.b0, es.b1, es.b2};
+    float gs[3], gsub[3][3];
+    clip_gb_sub(cr, gb, gs);
+    raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
+    clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
+  } else {
+    raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+  }
+}
+
+// One thread per stored fragment slot (n, y, x, k) in memory order: the loads of pix_to_face and
+// of the upstream gradients are coalesced (one lane per pixel walking its K slots strided them by
+// K elements), and a block whose 256 slots hold no fragment (most of them when K is large: the
+// K-nearest lists are short) returns before touching its LDS accumulator.
+__global__ void __launch_bounds__(256) k_raster_bwd_slots(RasterBwdParams P, int64_t nslots) {
+  __shared__ LdsAcc<9> L;
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t f = pix < nslots ? P.p2f[pix] : -1;
+  if (!__syncthreads_or(f >= 0)) return;
+  acc_init(L);
+  __syncthreads();
+  if (f >= 0) {
+    const int64_t p = pix / P.K;
+    const int64_t hw = (int64_t)P.H * P.W;
+    const int rem = (int)(p % hw);
+    const int py = rem / P.W, px = rem - py * P.W;
+    float g[3][3];
+    raster_bwd_fragment(P, px, py, pix, f, g);
+    acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
+  }
+  __syncthreads();
+  acc_flush(L, P.gfv);
+}
+
 __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
   __shared__ LdsAcc<9> L;
   acc_init(L);
@@ -2316,49 +2387,8 @@ __global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
       const int64_t pix = pix0 + kk;
       const int64_t f = P.p2f[pix];
       if (f < 0) continue;
-      FaceRec r;
-      const float* v = P.fv + 9 * f;
-      r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
-      r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
-      r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
-      r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
-      const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
-      const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
       float g[3][3];
-      int ci = 0;
-      const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};
-      const int nb = P.clipz ? clip_class(vv, P.zc, ci) : 0;
-      if (nb == 1 || nb == 2) {
-        // the face was split at the near plane: rebuild its sub-triangle(s) exactly as the forward
-        // binning did, pick the one that produced this fragment (the forward's pair rule), and chain
-        for (int c = 0; c < 3; ++c)
-          for (int q = 0; q < 3; ++q) g[c][q] = 0.0f;
-        float sv[3][3];
-        ClipRec cr0, cr1;
-        clip_sub(vv, nb, ci, 0, P.zc, P.persp != 0, sv, cr0);
-        FaceRec r0 = make_rec_core(P.cull, P.persp, 0u, sv);
-        int use = 0;
-        FaceRec r1;
-        if (nb == 1) {
-          clip_sub(vv, nb, ci, 1, P.zc, P.persp != 0, sv, cr1);
-          r1 = make_rec_core(P.cull, P.persp, 0u, sv);
-          FragEval e0, e1;
-          const bool k0 = (r0.flags & FR_VALID) && eval_face(r0, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e0);
-          const bool k1 = (r1.flags & FR_VALID) && eval_face(r1, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e1);
-          use = (k0 && k1) ? (fabsf(e1.sdist) < fabsf(e0.sdist) ? 1 : 0) : (k1 ? 1 : 0);
-        }
-        const FaceRec& rs = use ? r1 : r0;
-        const ClipRec& cr = use ? cr1 : cr0;
-        FragEval es;
-        eval_face(rs, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, es);
-        const float bs[3] = {es.b0, es.b1, es.b2};
-        float gs[3], gsub[3][3];
-        clip_gb_sub(cr, gb, gs);
-        raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
-        clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
-      } else {
-        raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
-      }
+      raster_bwd_fragment(P, px, py, pix, f, g);
       acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
     }
   }
@@ -3705,8 +3735,13 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
   P.cull = s->cull_backfaces; P.clipz = s->clip_z != 0; P.zc = s->z_clip_value;
   P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.fv = fv; P.p2f = p2f; P.gz = gz; P.gb = gb; P.gd = gd; P.gfv = gfv;
+#ifndef MR_RASTER_BWD_TILES
+  const int64_t nslots = N * (int64_t)s->H * s->W * s->faces_per_pixel;
+  MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd_slots<<<(unsigned)((nslots + 255) / 256), 256, 0, st>>>(P, nslots)));
+#else
   dim3 grid(P.NBX * ceil_div(s->H, MR_BT), (unsigned)N);
   MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd<<<grid, 256, 0, st>>>(P)));
+#endif
   MR_CHECK_LAUNCH("k_raster_bwd");
   return MR_OK;
 }

@@ -120,6 +120,7 @@ class RasterizeFaceVerts(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, face_verts, first, count, H, W, K, blur, persp, clip, cull, mfpb, z_clip=None):
+        ctx.set_materialize_grads(False)  # no zero-filled int64 grad for pix_to_face, none for unused outputs
         p2f, zbuf, bary, dists = rasterize_meshes_fwd(face_verts, first, count, H, W, K, blur, persp, clip, cull,
                                                       mfpb, z_clip)
         ctx.save_for_backward(face_verts, p2f)
@@ -215,6 +216,7 @@ class RasterizeMeshesWorld(torch.autograd.Function):
     @staticmethod
     def forward(ctx, verts, R, T, faces, intr, N, H, W, K, blur, persp, clip, cull, mfpb, z_clip=None):
         _require_cuda(verts, R, T, faces, intr)
+        ctx.set_materialize_grads(False)  # no zero-filled int64 grad for pix_to_face, none for unused outputs
         L = _lib.load()
         v = verts.detach().float().contiguous()
         f, vptr, vadj = mesh_topology(faces, v.shape[0])

@@ -292,11 +292,13 @@ def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_
             tmap, fuv, vuv = tex_i.maps_list()[0], tex_i.faces_uvs_list()[0], tex_i.verts_uvs_list()[0]
         elif cfg.want_rgb:
             raise NotImplementedError(f"textures of type {type(tex_i).__name__}")
-        q = p2f[i0:i1]
+        whole = i0 == 0 and i1 == N  # the whole batch: no slices (a slice's backward would zero-fill
+        sl = (lambda t: t) if whole else (lambda t: t[i0:i1])  # noqa: E731  and copy each fragment grad)
+        q = sl(p2f)
         if first:
             q = torch.where(q >= 0, q - first, q)
         c = cc[i0:i1] if cc.shape[0] > 1 else cc
-        return ShadeFragments.apply(fragments.zbuf[i0:i1], fragments.bary_coords[i0:i1], fragments.dists[i0:i1],
+        return ShadeFragments.apply(sl(fragments.zbuf), sl(fragments.bary_coords), sl(fragments.dists),
                                     verts, vc, tmap, vuv, q.contiguous(), faces, fuv, c, cfg)
 
     if meshes.is_shared():

@@ -3286,13 +3286,9 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
       P.g_bary[3 * (base + k)] = gb[0];
       P.g_bary[3 * (base + k) + 1] = gb[1];
       P.g_bary[3 * (base + k) + 2] = gb[2];
-    } else if (act) {
-      P.g_zbuf[base + k] = 0.0f;
-      P.g_dists[base + k] = 0.0f;
-      P.g_bary[3 * (base + k)] = 0.0f;
-      P.g_bary[3 * (base + k) + 1] = 0.0f;
-      P.g_bary[3 * (base + k) + 2] = 0.0f;
     }
+    // (empty slots: their zero gradients were written by coalesced fills before the launch; written
+    // here one lane per pixel they were K-strided 4-B stores, most of this kernel's time at large K)
     if (!P.sil && S.light_kind == 0) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     else if (ACC == 27 && !P.sil) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
   }
@@ -4217,6 +4213,13 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   P.gmap = m->tex_kind == 2 ? g_tex_rgba : nullptr;
   P.guv = m->tex_kind == 2 ? g_verts_uvs : nullptr;
   const int grid = ceil_div(N * (int64_t)H * W, 256);
+  {  // the fragment gradients of empty slots are zero: cleared here with coalesced fills
+    const size_t slots = (size_t)N * H * W * K;
+    if (hipMemsetAsync(g_zbuf, 0, sizeof(float) * slots, st) != hipSuccess ||
+        hipMemsetAsync(g_dists, 0, sizeof(float) * slots, st) != hipSuccess ||
+        hipMemsetAsync(g_bary, 0, sizeof(float) * 3 * slots, st) != hipSuccess)
+      return set_err(MR_ELAUNCH, "memset failed");
+  }
   if (vcol) MR_TIMED(KID_FRAG_SHADE_BWD, st, (k_frag_shade_bwd<27><<<grid, 256, 0, st>>>(P)));
   else MR_TIMED(KID_FRAG_SHADE_BWD, st, (k_frag_shade_bwd<18><<<grid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_frag_shade_bwd");

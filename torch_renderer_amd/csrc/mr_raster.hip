@@ -2151,15 +2151,20 @@ __global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
     // the keys leave in ascending order through q[0], the array shifting down one slot per step:
     // only constant indices into q[] (a dynamic index would demote the array to scratch), and the
     // output body (eval_face) is not unrolled KP times
+    // only the filled slots: k_fill wrote the background (-1) of every slot, and the K nearest
+    // lists are short at large K (3.7 of 50 slots per pixel on the deform workload); the loop ends
+    // when no lane of the wave has a key left
 #pragma unroll 1
     for (int k = 0; k < K; ++k) {
+      if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
       const unsigned long long key = q[0];
 #pragma unroll
       for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
       q[KP - 1] = MR_KEY_EMPTY;
+      if (!(key < MR_KEY_EMPTY)) continue;
       int64_t f = -1;
       float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
-      if (key < MR_KEY_EMPTY) {
+      {
         const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
         const FaceRec r = P.recs[id];
         FragEval ev;

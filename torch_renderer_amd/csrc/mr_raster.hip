@@ -2133,6 +2133,19 @@ __global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
       };
       auto insert = [&](unsigned long long key) {
         if (__ballot(key < q[KP - 1]) != 0ull) {
+#ifndef MR_KR_CHAIN
+          // shift-insert with every step independent: q is ascending, so key < q[k] holds from the
+          // insertion point on; walking down, slot k takes q[k-1] (if key < q[k-1] too) or key. The
+          // compare-exchange chain instead carried key through all KP steps (a KP-long dependency).
+          bool ltk = key < q[KP - 1];
+#pragma unroll
+          for (int k = KP - 1; k > 0; --k) {
+            const bool ltp = key < q[k - 1];
+            q[k] = ltk ? (ltp ? q[k - 1] : key) : q[k];
+            ltk = ltp;
+          }
+          q[0] = ltk ? key : q[0];
+#else
 #pragma unroll
           for (int k = 0; k < KP; ++k) {
             const unsigned long long a = q[k];
@@ -2140,6 +2153,7 @@ __global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
             q[k] = lt ? key : a;
             key = lt ? a : key;
           }
+#endif
         }
       };
 #pragma unroll 1

@@ -2201,10 +2201,13 @@ __global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
 // hand-off). With one wave per tile the kernel lasted as long as the longest list (1,896 entries
 // against a mean of 451 on the deform workload); split four ways the long lists finish sooner and
 // the short ones share the CUs.
+#ifndef MR_KR_WPT
+#define MR_KR_WPT 2  // waves per tile in k_raster_kr4 (2: 2.18 ms, 4: 2.37, 8: 3.58 on the deform workload)
+#endif
 template <int KP>
-__global__ void __launch_bounds__(256) k_raster_kr4(FwdParams P) {
-  __shared__ FaceRec srs[4][64];
-  __shared__ int sids[4][64];
+__global__ void __launch_bounds__(64 * MR_KR_WPT) k_raster_kr4(FwdParams P) {
+  __shared__ FaceRec srs[MR_KR_WPT][64];
+  __shared__ int sids[MR_KR_WPT][64];
   __shared__ unsigned long long mbuf[KP * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2231,8 +2234,8 @@ __global__ void __launch_bounds__(256) k_raster_kr4(FwdParams P) {
     const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
     const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
     const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
-    // this wave's quarter of the list, in whole 64-entry batches
-    const int chunk = (((count + 3) >> 2) + 63) & ~63;
+    // this wave's share of the list, in whole 64-entry batches
+    const int chunk = (((count + MR_KR_WPT - 1) / MR_KR_WPT) + 63) & ~63;
     const int e0 = min(wave * chunk, count), e1 = min(e0 + chunk, count);
     unsigned long long q[KP];
 #pragma unroll
@@ -2278,7 +2281,7 @@ __global__ void __launch_bounds__(256) k_raster_kr4(FwdParams P) {
     }
     // waves 1..3 hand their lists to wave 0 through LDS, one at a time
 #pragma unroll 1
-    for (int w2 = 1; w2 < 4; ++w2) {
+    for (int w2 = 1; w2 < MR_KR_WPT; ++w2) {
       __syncthreads();
       if (wave == w2) {
 #pragma unroll
@@ -2326,7 +2329,7 @@ template <int KP>
 static void launch_raster_kr(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
 #ifndef MR_RASTER_KR_WAVE
   const int grid = (int)(slots_cap < 16384 ? slots_cap : 16384);  // one workgroup per tile
-  MR_TIMED(KID_RASTER_K, st, (k_raster_kr4<KP><<<grid, 256, 0, st>>>(P)));
+  MR_TIMED(KID_RASTER_K, st, (k_raster_kr4<KP><<<grid, 64 * MR_KR_WPT, 0, st>>>(P)));
 #else
   const int64_t want = (slots_cap + 3) / 4;
   const int grid = (int)(want < 8192 ? want : 8192);

@@ -108,6 +108,13 @@ def test_empty_views_and_background():
     # soft rasterization as deform_mesh_with_color.py:153-159 configures it (blur > 0 => clip)
     ("sphere", 64, 64, 1, 6, 2e-3, True, None),
     ("cow", 64, 64, 2, 4, 0.0, False, 5),  # overflowing tile lists: whole-view scan
+    # every register-list width of k_raster_kr4 (KP = 16 / 32 / 50 / 64, K below KP too) and the
+    # LDS-list kernel beyond 64, with a blur wide enough to fill deep lists
+    ("cow", 48, 48, 1, 13, 2e-3, True, None),
+    ("cow", 48, 48, 1, 20, 2e-3, True, None),
+    ("cow", 48, 48, 1, 50, 2e-3, True, None),
+    ("cow", 48, 48, 1, 64, 2e-3, True, None),
+    ("cow", 48, 48, 1, 100, 2e-3, True, None),
 ])
 def test_raster_k_nearest_matches_oracle(name, H, W, N, K, blur, clip, cap):
     """faces_per_pixel > 1: the K nearest faces per pixel in ascending

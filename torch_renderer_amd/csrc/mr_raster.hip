@@ -2560,15 +2560,17 @@ MR_DEV float dppf(float v) {
 // Segmented inclusive sum over lanes: d = distance from the lane to the first lane of its run.
 // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry a run across rows
 // (the structure of wave_incl_sum, each step gated on the run reaching that far back).
+// Each step is written as select(gate, x + shifted, x) so the DPP move folds into the add
+// (v_add_f32 with a DPP operand + v_cndmask: two VALU ops per step instead of three).
 MR_DEV float seg_incl_sum(float x, int d, int lane) {
   const int r = lane & 15;
-  float y;
-  y = dppf<0x111, 0xf>(x); x += (d >= 1) ? y : 0.0f;
-  y = dppf<0x112, 0xf>(x); x += (d >= 2) ? y : 0.0f;
-  y = dppf<0x114, 0xf>(x); x += (d >= 4) ? y : 0.0f;
-  y = dppf<0x118, 0xf>(x); x += (d >= 8) ? y : 0.0f;
-  y = dppf<0x142, 0xa>(x); x += (d > r) ? y : 0.0f;            // rows 1, 3 <- lanes 15, 47
-  y = dppf<0x143, 0xc>(x); x += (d > lane - 32) ? y : 0.0f;    // rows 2, 3 <- lane 31
+  float s;
+  s = x + dppf<0x111, 0xf>(x); x = (d >= 1) ? s : x;
+  s = x + dppf<0x112, 0xf>(x); x = (d >= 2) ? s : x;
+  s = x + dppf<0x114, 0xf>(x); x = (d >= 4) ? s : x;
+  s = x + dppf<0x118, 0xf>(x); x = (d >= 8) ? s : x;
+  s = x + dppf<0x142, 0xa>(x); x = (d > r) ? s : x;            // rows 1, 3 <- lanes 15, 47
+  s = x + dppf<0x143, 0xc>(x); x = (d > lane - 32) ? s : x;    // rows 2, 3 <- lane 31
   return x;
 }
 // Full-wave sum, result in lane 63.

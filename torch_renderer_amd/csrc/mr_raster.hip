@@ -2759,8 +2759,13 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 
 // CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
 // instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
+#ifdef MR_BWD_WAVES  // experiment builds: force an occupancy target
+#define MR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(MR_BWD_WAVES)))
+#else
+#define MR_BWD_ATTR
+#endif
 template <int ACC, bool CLIP>
-__global__ void __launch_bounds__(256) k_bwd_fused(RenderBwdParams P) {
+__global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P) {
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
   __shared__ float4 lrec[4][MR_BWD_REC][64];

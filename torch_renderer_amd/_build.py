@@ -26,6 +26,11 @@ HIPCC_FLAGS = [
     # adjacent registers, which cost more than they save. k_bwd_fused: 239 -> 194 VGPRs, 505 -> 247
     # v_mov, 88.5 -> 82.6 us (profiles/r2k_noslp_ab.txt).
     "-fno-slp-vectorize",
+    # Machine scheduler biased to ILP over occupancy: each wave of the latency-bound kernels hides
+    # more of its own latency. k_bwd_fused 82.9 -> 79.8 us, k_tile_raster 85.8 -> 83.8 us
+    # (max-memory-clause: no change; profiles/r2l_sched_ab.txt).
+    "-mllvm",
+    "-amdgpu-sched-strategy=max-ilp",
 ]
 
 

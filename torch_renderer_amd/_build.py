@@ -50,6 +50,7 @@ def needs_build(out: str = OUT) -> bool:
         return True
     t = os.path.getmtime(out)
     deps = sources() + glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(_HERE, "..", "include", "mi355r.h")]
+    deps.append(os.path.abspath(__file__))  # compiler flags live here
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 

@@ -555,9 +555,26 @@ def _spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    # poll every rank: if one dies (e.g. a failed RCCL init) the others would wait in a collective
+    # forever, so the rest are terminated and the parent exits with the failure
     rc = 0
-    for p in procs:
-        rc = max(rc, p.wait())
+    while procs:
+        time.sleep(0.2)
+        for p in list(procs):
+            r = p.poll()
+            if r is None:
+                continue
+            procs.remove(p)
+            if r != 0:
+                rc = r
+                for q in procs:
+                    q.terminate()
+                for q in procs:
+                    try:
+                        q.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                return rc
     return rc
 
 

@@ -156,6 +156,127 @@ def project_faces_torch(verts, faces, R, T, intr):
     return fv.reshape(-1, 3, 3)
 
 
+# ---------------------------------------------------------------- upstream-order projection
+# PyTorch3D's MeshRasterizer.transform does not compute ax * (x / z) + bx: it composes 4x4
+# Transform3d matrices (row-vector convention) and applies one homogeneous product + divide:
+#   v0.5/0.6 ("v06", cameras.transform_points_ndc):  [X, 1] @ (((R4 @ T4) @ K4) @ (FIX4 @ S2N4)) / w
+#   v0.7+    ("v07", projection_transform.compose(to_ndc) on verts_view):  [Xv, 1] @ (K4 @ (FIX4 @ S2N4)) / w
+# with R4 = Rotate(R), T4 = Translate(T) (get_world_to_view_transform), K4 = K^T of the camera's
+# calibration matrix (_get_sfm_calibration_matrix / FoV compute_projection_matrix), FIX4 the
+# principal-point fix and S2N4 = inverse(ndc -> screen) of get_ndc_camera_transform (in_ndc=False
+# only; identity otherwise); then verts_ndc[..., 2] = verts_view[..., 2]. Restated from the published
+# PyTorch3D sources as recalled (the package is absent here: parity unpinned); every 4x4 product is
+# evaluated as torch's small-bmm CPU kernel does, sum over k = 0..3 in order, float32, no FMA. The
+# float32 tan of the FoV camera and LAPACK's 4x4 inverse are taken as correctly rounded (exact for
+# the power-of-two image sizes of every BASELINE config).
+def _mm4(A, B):
+    """(..., 4, 4) float32 matrix product, k summed in order 0..3, one rounding per operation."""
+    A = np.asarray(A, np.float32)
+    B = np.asarray(B, np.float32)
+    shp = np.broadcast_shapes(A.shape, B.shape)
+    C = np.zeros(shp, np.float32)
+    for i in range(4):
+        for j in range(4):
+            acc = A[..., i, 0] * B[..., 0, j]
+            for k in range(1, 4):
+                acc = (acc + A[..., i, k] * B[..., k, j]).astype(np.float32)
+            C[..., i, j] = acc
+    return C
+
+
+def _apply4(P, M):
+    """[P, 1] @ M then divide by w (Transform3d.transform_points, eps=None). P (..., 3), M (..., 4, 4)."""
+    P = np.asarray(P, np.float32)
+    out = []
+    for j in range(4):
+        acc = P[..., 0] * M[..., 0, j]
+        acc = (acc + P[..., 1] * M[..., 1, j]).astype(np.float32)
+        acc = (acc + P[..., 2] * M[..., 2, j]).astype(np.float32)
+        acc = (acc + np.float32(1.0) * M[..., 3, j]).astype(np.float32)
+        out.append(acc)
+    w = out[3]
+    return np.stack([(out[0] / w).astype(np.float32), (out[1] / w).astype(np.float32),
+                     (out[2] / w).astype(np.float32)], -1)
+
+
+def upstream_camera_mats(cam, N):
+    """(K4, NDC4) (N,4,4) float32 row-vector matrices of a camera spec:
+    {"kind": "perspective", "fx", "fy", "px", "py", "in_ndc", "image_size": (H, W)} or
+    {"kind": "fov", "znear", "zfar", "fov", "aspect_ratio", "degrees"}."""
+    f32 = np.float32
+    Kc = np.zeros((N, 4, 4), np.float32)  # column-vector K, transposed at the end
+    ndc = np.tile(np.eye(4, dtype=np.float32), (N, 1, 1))
+    if cam["kind"] == "fov":
+        zn, zf = f32(cam.get("znear", 1.0)), f32(cam.get("zfar", 100.0))
+        ar = f32(cam.get("aspect_ratio", 1.0))
+        fov = f32(cam.get("fov", 60.0))
+        if cam.get("degrees", True):
+            fov = f32(f32(np.pi / 180) * fov)
+        tanh = f32(np.tan(fov / f32(2.0)))
+        max_y = f32(tanh * zn)
+        min_y = f32(-max_y)
+        max_x = f32(max_y * ar)
+        min_x = f32(-max_x)
+        Kc[:, 0, 0] = f32(f32(f32(2.0) * zn) / f32(max_x - min_x))
+        Kc[:, 1, 1] = f32(f32(f32(2.0) * zn) / f32(max_y - min_y))
+        Kc[:, 0, 2] = f32(f32(max_x + min_x) / f32(max_x - min_x))
+        Kc[:, 1, 2] = f32(f32(max_y + min_y) / f32(max_y - min_y))
+        Kc[:, 3, 2] = 1.0
+        Kc[:, 2, 2] = f32(zf / f32(zf - zn))
+        Kc[:, 2, 3] = f32(-f32(zf * zn) / f32(zf - zn))
+    else:
+        fx, fy = f32(cam["fx"]), f32(cam["fy"])
+        px, py = f32(cam["px"]), f32(cam["py"])
+        Kc[:, 0, 0], Kc[:, 1, 1], Kc[:, 0, 2], Kc[:, 1, 2] = fx, fy, px, py
+        Kc[:, 3, 2] = 1.0
+        Kc[:, 2, 3] = 1.0
+        if not cam.get("in_ndc", True):
+            H, W = cam["image_size"]
+            s = f32(f32(min(H, W)) / f32(2.0))
+            fix = np.tile(np.eye(4, dtype=np.float32), (N, 1, 1))
+            fix[:, 3, 0] = f32(-2.0) * px  # pr_point_fix[:, :2, 3] = -2 * pp, transposed
+            fix[:, 3, 1] = f32(-2.0) * py
+            inv_s = f32(f32(1.0) / s)
+            s2n = np.tile(np.eye(4, dtype=np.float32), (N, 1, 1))
+            s2n[:, 0, 0] = inv_s
+            s2n[:, 1, 1] = inv_s
+            s2n[:, 3, 0] = f32(f32(f32(W) / f32(2.0)) * inv_s)  # inverse of the -W/2 translation
+            s2n[:, 3, 1] = f32(f32(f32(H) / f32(2.0)) * inv_s)
+            ndc = _mm4(fix, s2n)
+    return np.ascontiguousarray(np.transpose(Kc, (0, 2, 1))), ndc
+
+
+def project_faces_upstream(verts, faces, R, T, cam, version="v06"):
+    """face_verts (N*F, 3, 3) as upstream MeshRasterizer.transform computes them (see above): NDC
+    x, y from the composed homogeneous product and divide, view z kept. R (N,3,3) row-vector
+    convention, T (N,3). Returns a float32 torch tensor (no autograd)."""
+    v = verts.detach().float().cpu().numpy()
+    f = faces.detach().long().cpu().numpy()
+    Rn = R.detach().float().cpu().numpy().reshape(-1, 3, 3)
+    Tn = T.detach().float().cpu().numpy().reshape(-1, 3)
+    N = max(Rn.shape[0], Tn.shape[0])
+    Rn = np.broadcast_to(Rn, (N, 3, 3))
+    Tn = np.broadcast_to(Tn, (N, 3))
+    R4 = np.tile(np.eye(4, dtype=np.float32), (N, 1, 1))
+    R4[:, :3, :3] = Rn
+    T4 = np.tile(np.eye(4, dtype=np.float32), (N, 1, 1))
+    T4[:, 3, :3] = Tn
+    K4, ndc = upstream_camera_mats(cam, N)
+    W2V = _mm4(R4, T4)
+    X = v[f]  # (F,3,3)
+    view = _apply4(X[None], W2V[:, None, None])  # (N,F,3,3) verts_view
+    if version == "v06":
+        M = _mm4(_mm4(W2V, K4), ndc)
+        out = _apply4(X[None], M[:, None, None])
+    elif version == "v07":
+        P = _mm4(K4, ndc)
+        out = _apply4(view, P[:, None, None])
+    else:
+        raise ValueError(version)
+    out[..., 2] = view[..., 2]
+    return torch.from_numpy(np.ascontiguousarray(out.reshape(-1, 3, 3)))
+
+
 # ---------------------------------------------------------------- near-plane clipping
 def _clip_point(a, b, w, c, persp):
     """Point on edge a->b (rows (x_ndc, y_ndc, z_view)) at view z = c, w = (c - za) / (zb - za).
@@ -406,41 +527,200 @@ DEFAULT_MAT = {"ambient": (1.0, 1.0, 1.0), "diffuse": (1.0, 1.0, 1.0), "specular
 
 def render_ref(verts, faces, R, T, intr, H, W, *, texture=None, light=DEFAULT_LIGHT, mat=DEFAULT_MAT,
                cam_center=(0.0, 0.0, 0.0), sigma=1e-4, gamma=1e-4, bg=(1.0, 1.0, 1.0), sigma_sil=1e-4,
-               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0, clip=False, z_clip=None, window=None):
+               znear=1.0, zfar=100.0, persp=True, K=1, blur=0.0, clip=False, z_clip=None, window=None,
+               precision="f32"):
     """The reference CPU render path for one mesh shared by N views:
     depth = relu(zbuf[...,0]); sil = sigmoid_alpha_blend alpha; rgba = softmax_rgb_blend(phong).
     texture: None (white), ("vertex", vcolors (V,3)), ("uv", verts_uvs, faces_uvs, map (Ht,Wt,C)).
+    precision="f64": the float64 shadow (same decisions, every value and gradient in float64; see
+    frag_eval_t), which measures the f32 oracle's own rounding error.
     Returns dict with depth, sil, rgba, fragments."""
     N = R.shape[0]
     Fn = faces.shape[0]
-    fv = project_faces_torch(verts, faces, R, T, intr)
-    first = torch.arange(N, dtype=torch.int64) * Fn
-    count = torch.full((N,), Fn, dtype=torch.int64)
-    if z_clip is None:
-        p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, clip, False, None, window)
-    else:  # MeshRasterizer with a znear camera: clip_faces -> raster -> convert back (upstream clip.py)
-        cf = clip_faces_ref(fv, first, count, z_clip, persp)
-        p2f_c, zbuf, bary_c, dists = RasterizeRef.apply(cf["face_verts"], cf["first"], cf["count"], H, W, K, blur,
-                                                        persp, clip, False, cf["neighbor"], window)
-        p2f, bary = unclip_fragments(p2f_c, bary_c, cf)
-    faces_packed = faces.long().repeat(N, 1)
-    verts_packed_faces = faces_packed  # faces index the shared verts
+    if precision == "f64":
+        p2f, zbuf, bary, dists, fv = _shadow_fragments(verts, faces, R, T, intr, H, W, K, blur, persp, clip, z_clip,
+                                                       window)
+        verts = verts.double()
+        if texture is not None:
+            texture = tuple(t.double() if torch.is_tensor(t) and t.is_floating_point() else t for t in texture)
+        cam_center = torch.as_tensor(cam_center).double()
+    else:
+        fv = project_faces_torch(verts, faces, R, T, intr)
+        first = torch.arange(N, dtype=torch.int64) * Fn
+        count = torch.full((N,), Fn, dtype=torch.int64)
+        if z_clip is None:
+            p2f, zbuf, bary, dists = RasterizeRef.apply(fv, first, count, H, W, K, blur, persp, clip, False, None,
+                                                        window)
+        else:  # MeshRasterizer with a znear camera: clip_faces -> raster -> convert back (upstream clip.py)
+            cf = clip_faces_ref(fv, first, count, z_clip, persp)
+            p2f_c, zbuf, bary_c, dists = RasterizeRef.apply(cf["face_verts"], cf["first"], cf["count"], H, W, K,
+                                                            blur, persp, clip, False, cf["neighbor"], window)
+            p2f, bary = unclip_fragments(p2f_c, bary_c, cf)
+        zbuf, bary, dists = _jitter(zbuf), _jitter(bary), _jitter(dists)  # conditioning probe (if active)
     local = p2f.clone()
     local[p2f >= 0] = p2f[p2f >= 0] % Fn
     if texture is None:
-        texels = torch.ones(N, H, W, K, 3)
+        texels = torch.ones(N, H, W, K, 3, dtype=zbuf.dtype)
     elif texture[0] == "vertex":
         texels = sample_textures_vertex(local, bary, texture[1], faces)
     else:
         texels = sample_textures_uv(local, bary, texture[1], texture[2], texture[3])
-    cc = torch.as_tensor(cam_center, dtype=torch.float32).view(-1, 3)
+    cc = torch.as_tensor(cam_center, dtype=zbuf.dtype).view(-1, 3)
     colors = phong_colors(local, bary, verts, faces, texels, light, mat, cc)
     rgba = softmax_rgb_blend(colors, p2f, zbuf, dists, sigma, gamma, bg, znear, zfar)
     sil = sigmoid_alpha(p2f, dists, sigma_sil)
     depth = torch.relu(zbuf[..., 0])
-    del verts_packed_faces
+    depth, sil, rgba = _jitter(depth, False), _jitter(sil, False), _jitter(rgba, False)
     return {"depth": depth, "sil": sil, "rgba": rgba, "p2f": p2f, "zbuf": zbuf, "bary": bary, "dists": dists,
             "face_verts": fv}
+
+
+# ---------------------------------------------------------------- conditioning probe
+# Under `with perturbed(seed):` render_ref (f32) scales the values of its fragments (zbuf, bary,
+# dists) by 1 + eps_val * n and every gradient entering its fragments and its outputs (depth,
+# silhouette, rgba) by 1 + eps_grad * n, n ~ N(0, 1) per entry (1e-7 ~ 1 ulp, 1e-6 ~ 8 ulp). How far
+# a result moves under that is how far float32 rounding can move it: the per-entry conditioning that
+# tests.helpers.report allows for (a gradient that is a difference of much larger per-pixel terms,
+# a saturated sigmoid's 1 - p, a sliver face's 1 / area^2).
+_PERTURB = None
+
+
+class perturbed:
+    def __init__(self, seed, eps_val=1e-7, eps_grad=1e-6):
+        self.gen = torch.Generator().manual_seed(1000 + int(seed))
+        self.eps_val, self.eps_grad = eps_val, eps_grad
+
+    def __enter__(self):
+        global _PERTURB
+        _PERTURB = self
+        return self
+
+    def __exit__(self, *exc):
+        global _PERTURB
+        _PERTURB = None
+        return False
+
+
+class _Jitter(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, nv, ng, eps_val, eps_grad):
+        ctx.save_for_backward(ng)
+        ctx.eps_grad = eps_grad
+        return x * (1 + eps_val * nv)
+
+    @staticmethod
+    def backward(ctx, g):
+        (ng,) = ctx.saved_tensors
+        return g * (1 + ctx.eps_grad * ng), None, None, None, None
+
+
+def _jitter(x, value=True):
+    P = _PERTURB
+    if P is None or not torch.is_tensor(x) or not x.is_floating_point():
+        return x
+    nv = torch.randn(x.shape, generator=P.gen, dtype=x.dtype) if value else torch.zeros_like(x)
+    ng = torch.randn(x.shape, generator=P.gen, dtype=x.dtype)
+    return _Jitter.apply(x, nv, ng, P.eps_val if value else 0.0, P.eps_grad)
+
+
+# ---------------------------------------------------------------- float64 shadow
+# The f32 oracle is itself only as accurate as float32 allows: a vertex gradient that is a
+# difference of large per-pixel terms (the 1/sigma = 1e4 factor of the soft blends, 1/area^2 of
+# slivers), or sigmoid(x)(1 - sigmoid(x)) near saturation, carries the oracle's own rounding error.
+# The shadow evaluates the same formulas in float64 at the same decisions (the f32 run's
+# pix_to_face and near-plane split structure), differentiable end to end by torch autograd:
+# |oracle_f32 - shadow_f64| is the f32 oracle's own error, entry by entry (tests.helpers.report).
+def _pix_ndc_t(i, S1, S2, dtype):
+    rng = 2.0 * S1 / S2 if S1 > S2 else 2.0
+    off = rng / 2.0
+    return -off + (rng * i.to(dtype) + off) / S1
+
+
+def _edge_t(px, py, ax, ay, bx, by):
+    return (px - ax) * (by - ay) - (py - ay) * (bx - ax)
+
+
+def _seg_dist2_t(px, py, ax, ay, bx, by):
+    dx, dy = bx - ax, by - ay
+    l2 = dx * dx + dy * dy
+    degen = l2 <= 1e-8
+    t = (dx * (px - ax) + dy * (py - ay)) / torch.where(degen, torch.ones_like(l2), l2)
+    t = t.clamp(0.0, 1.0)
+    qx, qy = ax + t * dx, ay + t * dy
+    d_line = (px - qx) ** 2 + (py - qy) ** 2
+    d_pt = (px - bx) ** 2 + (py - by) ** 2
+    return torch.where(degen, d_pt, d_line)
+
+
+def frag_eval_t(face_verts, p2f, H, W, persp=True, clip=False):
+    """zbuf, bary, dists of the fragments named by p2f (N,H,W,K) from face_verts (differentiable,
+    in face_verts' dtype): RasterizeMeshesNaiveCpu's per-(pixel, face) formulas
+    at decisions already taken; background entries are -1."""
+    N, H_, W_, K = p2f.shape
+    dt = face_verts.dtype
+    valid = p2f >= 0
+    v = face_verts[p2f.clamp(min=0)]  # (N,H,W,K,3,3)
+    yi = torch.arange(H).view(1, H, 1, 1)
+    xi = torch.arange(W).view(1, 1, W, 1)
+    py = _pix_ndc_t(H - 1 - yi, H, W, dt)
+    px = _pix_ndc_t(W - 1 - xi, W, H, dt)
+    x0, y0, z0 = v[..., 0, 0], v[..., 0, 1], v[..., 0, 2]
+    x1, y1, z1 = v[..., 1, 0], v[..., 1, 1], v[..., 1, 2]
+    x2, y2, z2 = v[..., 2, 0], v[..., 2, 1], v[..., 2, 2]
+    area = _edge_t(x2, y2, x0, y0, x1, y1) + 1e-8
+    w0 = _edge_t(px, py, x1, y1, x2, y2) / area
+    w1 = _edge_t(px, py, x2, y2, x0, y0) / area
+    w2 = _edge_t(px, py, x0, y0, x1, y1) / area
+    if persp:
+        t0, t1, t2 = w0 * z1 * z2, w1 * z0 * z2, w2 * z0 * z1
+        d = (t0 + t1 + t2).clamp(min=1e-8)
+        c0, c1, c2 = t0 / d, t1 / d, t2 / d
+    else:
+        c0, c1, c2 = w0, w1, w2
+    if clip:
+        u0, u1, u2 = c0.clamp(min=0.0), c1.clamp(min=0.0), c2.clamp(min=0.0)
+        s = (u0 + u1 + u2).clamp(min=1e-5)
+        b0, b1, b2 = u0 / s, u1 / s, u2 / s
+    else:
+        b0, b1, b2 = c0, c1, c2
+    pz = b0 * z0 + b1 * z1 + b2 * z2
+    dist = torch.minimum(torch.minimum(_seg_dist2_t(px, py, x0, y0, x1, y1), _seg_dist2_t(px, py, x0, y0, x2, y2)),
+                         _seg_dist2_t(px, py, x1, y1, x2, y2))
+    inside = (c0 > 0) & (c1 > 0) & (c2 > 0)
+    sd = torch.where(inside, -dist, dist)
+    m1 = torch.full_like(pz, -1.0)
+    zbuf = torch.where(valid, pz, m1)
+    dists = torch.where(valid, sd, m1)
+    bary = torch.where(valid[..., None], torch.stack([b0, b1, b2], -1), m1[..., None].expand(*m1.shape, 3))
+    return zbuf, bary, dists
+
+
+def _shadow_fragments(verts, faces, R, T, intr, H, W, K, blur, persp, clip, z_clip, window):
+    """f32 decisions (projection + near-plane split + C raster), then the float64 differentiable
+    re-evaluation of the kept fragments. Returns (p2f, zbuf, bary, dists, face_verts64)."""
+    N = R.shape[0]
+    Fn = faces.shape[0]
+    first = torch.arange(N, dtype=torch.int64) * Fn
+    count = torch.full((N,), Fn, dtype=torch.int64)
+    with torch.no_grad():
+        fv32 = project_faces_torch(verts.detach().float(), faces, R.detach().float(), T.detach().float(),
+                                   intr.detach().float())
+        if z_clip is not None:
+            cf32 = clip_faces_ref(fv32, first, count, z_clip, persp)
+            p2f_c = raster_fwd(cf32["face_verts"], cf32["first"], cf32["count"], H, W, K, blur, persp, clip, False,
+                               cf32["neighbor"], window)[0]
+        else:
+            p2f_c = raster_fwd(fv32, first, count, H, W, K, blur, persp, clip, False, None, window)[0]
+    fv = project_faces_torch(verts.double(), faces, R.double(), T.double(), intr.double())
+    if z_clip is None:
+        zbuf, bary, dists = frag_eval_t(fv, p2f_c, H, W, persp, clip)
+        return p2f_c, zbuf, bary, dists, fv
+    cf = clip_faces_ref(fv, first, count, z_clip, persp)
+    if not torch.equal(cf["orig"], cf32["orig"]):
+        raise RuntimeError("f64 shadow: the near-plane split differs from the f32 run's")
+    zbuf, bary_c, dists = frag_eval_t(cf["face_verts"], p2f_c, H, W, persp, clip)
+    p2f, bary = unclip_fragments(p2f_c, bary_c, cf)
+    return p2f, zbuf, bary, dists, fv
 
 
 def views_tensor(R, T, intr):

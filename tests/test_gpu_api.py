@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from tests.helpers import canonical_views, fragment_grad_sensitivity, mesh_arrays, report
+from tests.helpers import canonical_views, fragment_grad_sensitivity, mesh_arrays, oracle_runs, report
 from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
 from torch_renderer_amd.cameras import PerspectiveCameras
 from torch_renderer_amd.mesh_renderer import (BlendParams, Materials, MeshRasterizer, MeshRenderer, PointLights,
@@ -44,11 +44,34 @@ def _cow_mesh(N):
     return verts, faces, (vuv, fuv, img), v, Meshes([v], [faces.to(DEV)], tex).extend(N)
 
 
-def _close(a, b, tol=1e-4):
-    a, b = a.detach().cpu(), b.detach().cpu()
-    scale = max(1.0, b.abs().max().item())
-    err = (a - b).abs().max().item()
-    assert err <= tol * scale, f"max abs err {err} (scale {scale})"
+def _close(a, b, tol=1e-4, sens=None, ref64=None):
+    """Per-entry bar |a_i - b_i| <= tol * max(1, |b_i|) (tests.helpers.report), named by call site."""
+    import inspect
+
+    fr = inspect.stack()[1]
+    report(f"{fr.function}:{fr.lineno}", a, b, tol=tol, sens=sens, ref64=ref64)
+
+
+def _oracle_cv(verts, faces, R_cv, t_cv, K, H, W, texture, grads, precision="f32", faces_per_pixel=1):
+    """Oracle fwd+bwd of OpenCV-pose views (torch_renderer.py:73-80 conversion restated); returns the
+    outputs and the leaves (verts, R_cv, t_cv) holding the gradients. precision="f64": the float64
+    shadow (conditioning, tests.helpers.report)."""
+    N = R_cv.shape[0]
+    vr = verts.clone().requires_grad_(True)
+    Rr = R_cv.clone().requires_grad_(True)
+    tr = t_cv.clone().requires_grad_(True)
+    Rp, Tp = _cv_to_p3d(Rr, tr)
+    ref = O.render_ref(vr, faces, Rp, Tp, _intr(K, H, W, N).contiguous(), H, W, texture=texture, precision=precision,
+                       K=faces_per_pixel)
+    gD, gS, gC = grads
+    ((ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()).backward()
+    return ref, (vr, Rr, tr)
+
+
+def _oracle_cv_flat(*a, **kw):
+    """_oracle_cv as a flat tuple (depth, sil, rgb, grad verts, grad R_cv, grad t_cv) for oracle_runs."""
+    ref, (vr, Rr, tr) = _oracle_cv(*a, **kw)
+    return ref["depth"], ref["sil"], ref["rgba"][..., :3], vr.grad, Rr.grad, tr.grad
 
 
 def test_depth_color_render_match_oracle():
@@ -56,31 +79,23 @@ def test_depth_color_render_match_oracle():
     verts, faces, (vuv, fuv, img), v, meshes = _cow_mesh(N)
     _, _, _, (R_cv, t_cv, K) = canonical_views(verts, N, H, W)
     # reference path on the CPU
-    vr = verts.clone().requires_grad_(True)
-    Rr = R_cv.clone().requires_grad_(True)
-    tr = t_cv.clone().requires_grad_(True)
-    Rp, Tp = _cv_to_p3d(Rr, tr)
-    ref = O.render_ref(vr, faces, Rp, Tp, _intr(K, H, W, N).contiguous(), H, W, texture=("uv", vuv, fuv, img))
     g = torch.Generator().manual_seed(3)
     gD, gS, gC = (torch.rand(N, H, W, generator=g) - 0.5, torch.rand(N, H, W, generator=g) - 0.5,
                   torch.rand(N, H, W, 3, generator=g) - 0.5)
-    ((ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()).backward()
+    ref, r64, sp = oracle_runs(lambda p: _oracle_cv_flat(verts, faces, R_cv, t_cv, K, H, W, ("uv", vuv, fuv, img),
+                                                         (gD, gS, gC), precision=p))
     # drop-in classes
     Rg = R_cv.to(DEV).requires_grad_(True)
     tg = t_cv.to(DEV).requires_grad_(True)
     depth, sil = DepthRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg, return_silhouette=True)
     rgb = ColorRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg)
-    _close(depth, ref["depth"])
-    _close(sil, ref["sil"])
-    _close(rgb, ref["rgba"][..., :3])
+    for i, x in enumerate((depth, sil, rgb)):
+        _close(x, ref[i], ref64=r64[i], sens=sp[i])
     assert torch.equal(DepthRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg).cpu(), depth.cpu())
     d3, s3, c3 = DepthColorRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg)
     ((d3 * gD.to(DEV)).sum() + (s3 * gS.to(DEV)).sum() + (c3 * gC.to(DEV)).sum()).backward()
-    _close(d3, ref["depth"])
-    _close(c3, ref["rgba"][..., :3])
-    _close(v.grad, vr.grad)
-    _close(Rg.grad, Rr.grad)
-    _close(tg.grad, tr.grad)
+    for i, x in ((0, d3), (2, c3), (3, v.grad), (4, Rg.grad), (5, tg.grad)):
+        _close(x, ref[i], ref64=r64[i], sens=sp[i])
 
 
 @pytest.mark.parametrize("distinct", [False, True])
@@ -232,27 +247,21 @@ def test_drop_in_classes_faces_per_pixel_3_match_oracle():
     H, W, N, Kf = 48, 64, 2, 3
     verts, faces, (vuv, fuv, img), v, meshes = _cow_mesh(N)
     _, _, _, (R_cv, t_cv, K) = canonical_views(verts, N, H, W)
-    vr = verts.clone().requires_grad_(True)
-    Rr = R_cv.clone().requires_grad_(True)
-    tr = t_cv.clone().requires_grad_(True)
-    Rp, Tp = _cv_to_p3d(Rr, tr)
-    ref = O.render_ref(vr, faces, Rp, Tp, _intr(K, H, W, N).contiguous(), H, W, texture=("uv", vuv, fuv, img), K=Kf)
     g = torch.Generator().manual_seed(5)
     gD, gS, gC = (torch.rand(N, H, W, generator=g) - 0.5, torch.rand(N, H, W, generator=g) - 0.5,
                   torch.rand(N, H, W, 3, generator=g) - 0.5)
-    ((ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()).backward()
+    ref, r64, sp = oracle_runs(lambda p: _oracle_cv_flat(verts, faces, R_cv, t_cv, K, H, W, ("uv", vuv, fuv, img),
+                                                         (gD, gS, gC), precision=p, faces_per_pixel=Kf))
     Rg = R_cv.to(DEV).requires_grad_(True)
     tg = t_cv.to(DEV).requires_grad_(True)
     depth, sil = DepthRender(K.to(DEV), (H, W), faces_per_pixel=Kf, device=DEV).render(meshes, Rg, tg,
                                                                                       return_silhouette=True)
     rgb = ColorRender(K.to(DEV), (H, W), faces_per_pixel=Kf, device=DEV).render(meshes, Rg, tg)
-    _close(depth, ref["depth"])
-    _close(sil, ref["sil"])
-    _close(rgb, ref["rgba"][..., :3])
+    for i, x in enumerate((depth, sil, rgb)):
+        _close(x, ref[i], ref64=r64[i], sens=sp[i])
     ((depth * gD.to(DEV)).sum() + (sil * gS.to(DEV)).sum() + (rgb * gC.to(DEV)).sum()).backward()
-    _close(v.grad, vr.grad)
-    _close(Rg.grad, Rr.grad)
-    _close(tg.grad, tr.grad)
+    for i, x in ((3, v.grad), (4, Rg.grad), (5, tg.grad)):
+        _close(x, ref[i], ref64=r64[i], sens=sp[i])
 
 
 @pytest.mark.parametrize("shader", ["phong", "silhouette"])
@@ -286,13 +295,14 @@ def test_mesh_renderer_soft_raster_matches_oracle(shader, Kf):
     intr = cams.ndc_affine((H, W)).cpu().expand(N, 4).contiguous()
     out = {}
 
-    def run_oracle():
+    def run_oracle(precision="f32"):
         vr = verts.clone().requires_grad_(True)
         vcr = vcol.clone().requires_grad_(True)
         ref = O.render_ref(vr, faces, R, T, intr, H, W, texture=("vertex", vcr), light=light, cam_center=cc,
-                           bg=(0.2, 0.3, 0.4), K=Kf, blur=blur, clip=True)
-        out.setdefault("ref", ref)
-        loss = (ref["rgba"] * go).sum() if shader == "phong" else (ref["sil"] * go[..., 3]).sum()
+                           bg=(0.2, 0.3, 0.4), K=Kf, blur=blur, clip=True, precision=precision)
+        out.setdefault("ref" if precision == "f32" else "ref64", ref)
+        gg = go.to(ref["rgba"].dtype)
+        loss = (ref["rgba"] * gg).sum() if shader == "phong" else (ref["sil"] * gg[..., 3]).sum()
         loss.backward()
         return (vr.grad, vcr.grad) if shader == "phong" else (vr.grad,)
 
@@ -300,16 +310,17 @@ def test_mesh_renderer_soft_raster_matches_oracle(shader, Kf):
     # the teapot at 40x40 has sliver faces (projected area down to ~1e-5 px^2): the gradient of
     # their vertices is ill-conditioned in f32 on both sides, measured by the oracle's own spread
     refs, sens = fragment_grad_sensitivity(run_oracle)
+    r64 = run_oracle("f64")
     ref = out["ref"]
     assert img.shape == (N, H, W, 4)
     if shader == "phong":
-        _close(img, ref["rgba"])
+        _close(img, ref["rgba"], ref64=out["ref64"]["rgba"])
     else:
-        _close(img[..., 3], ref["sil"])
+        _close(img[..., 3], ref["sil"], ref64=out["ref64"]["sil"])
     (img * go.to(DEV)).sum().backward()
-    report(f"soft K={Kf} {shader} grad verts", vg.grad, refs[0], sens=sens[0])
+    report(f"soft K={Kf} {shader} grad verts", vg.grad, refs[0], sens=sens[0], ref64=r64[0])
     if shader == "phong":
-        report(f"soft K={Kf} {shader} grad vcolors", vc.grad, refs[1], sens=sens[1])
+        report(f"soft K={Kf} {shader} grad vcolors", vc.grad, refs[1], sens=sens[1], ref64=r64[1])
 
 
 def test_soft_raster_distinct_meshes_batch_equals_single_renders():

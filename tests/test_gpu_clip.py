@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from tests.helpers import mesh_arrays, report
+from tests.helpers import oracle_runs, mesh_arrays, report
 from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
 from torch_renderer_amd.cameras import FoVPerspectiveCameras
 from torch_renderer_amd.mesh_renderer import (BlendParams, MeshRasterizer, MeshRenderer, PointLights,
@@ -110,23 +110,26 @@ def test_fused_renderer_clipped_matches_oracle(shader):
     vg = verts.to(DEV).requires_grad_(True)
     Rg, Tg = R.to(DEV).requires_grad_(True), T.to(DEV).requires_grad_(True)
     out = renderer(meshes_world=Meshes([vg], [faces.to(DEV)], tex).extend(N), R=Rg, T=Tg)
-    vr = verts.clone().requires_grad_(True)
-    Rr, Tr = R.clone().requires_grad_(True), T.clone().requires_grad_(True)
-    ref = O.render_ref(vr, faces, Rr, Tr, torch.tensor([[FOV_T, 0.0, FOV_T, 0.0]]).expand(N, 4).contiguous(), H, W,
-                       texture=("uv", vuv, fuv, img), bg=(0.0, 0.0, 0.0), z_clip=0.5)
-    assert ((ref["zbuf"][..., 0] >= 0) & (ref["zbuf"][..., 0] < 0.6)).sum() > 100
     g = torch.Generator().manual_seed(9)
     go = torch.rand(N, H, W, 4, generator=g) - 0.5
-    if shader == "phong":
-        report("clip fused rgba", out, ref["rgba"])
-        (ref["rgba"] * go).sum().backward()
-    else:
-        report("clip fused silhouette", out[..., 3], ref["sil"])
-        (ref["sil"] * go[..., 3]).sum().backward()
+
+    def oracle(precision):
+        vr = verts.clone().requires_grad_(True)
+        Rr, Tr = R.clone().requires_grad_(True), T.clone().requires_grad_(True)
+        ref = O.render_ref(vr, faces, Rr, Tr, torch.tensor([[FOV_T, 0.0, FOV_T, 0.0]]).expand(N, 4).contiguous(), H,
+                           W, texture=("uv", vuv, fuv, img), bg=(0.0, 0.0, 0.0), z_clip=0.5, precision=precision)
+        gg = go.to(ref["rgba"].dtype)
+        ((ref["rgba"] * gg).sum() if shader == "phong" else (ref["sil"] * gg[..., 3]).sum()).backward()
+        img_ref = ref["rgba"] if shader == "phong" else ref["sil"]
+        return img_ref, vr.grad, Rr.grad, Tr.grad, ref["zbuf"]
+
+    # f32 oracle, its float64 shadow and the per-entry conditioning spread (tests.helpers.report)
+    ref, r64, sp = oracle_runs(oracle)
+    assert ((ref[4][..., 0] >= 0) & (ref[4][..., 0] < 0.6)).sum() > 100
+    report(f"clip fused {shader} image", out if shader == "phong" else out[..., 3], ref[0], ref64=r64[0], sens=sp[0])
     (out * go.to(DEV)).sum().backward()
-    report(f"clip fused {shader} grad verts", vg.grad, vr.grad)
-    report(f"clip fused {shader} grad R", Rg.grad, Rr.grad)
-    report(f"clip fused {shader} grad T", Tg.grad, Tr.grad)
+    for i, (nm, a) in enumerate(zip(("verts", "R", "T"), (vg.grad, Rg.grad, Tg.grad))):
+        report(f"clip fused {shader} grad {nm}", a, ref[i + 1], ref64=r64[i + 1], sens=sp[i + 1])
 
 
 def test_clipping_culls_faces_fully_behind_and_keeps_ids_original():

@@ -20,7 +20,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from tests.helpers import canonical_views, cv_to_p3d, intr_from_K, mesh_arrays, report
+from tests.helpers import canonical_views, cv_to_p3d, intr_from_K, mesh_arrays, oracle_runs, report
 from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
 from torch_renderer_amd.cameras import FoVPerspectiveCameras, PerspectiveCameras
 from torch_renderer_amd.kernels import ShadeConfig, rasterize_meshes_fwd
@@ -66,17 +66,36 @@ def _check_background(out, p2f, bg):
     assert (~empty).any(), "degenerate view: nothing covered"
 
 
-def _oracle_views(verts, faces, R_cv, t_cv, K, H, W, texture, grads, bg=(1.0, 1.0, 1.0), window=None):
-    """Reference fwd+bwd (CPU) of views given as OpenCV poses: outputs, leaf grads (verts, R, t)."""
+def _oracle_views(verts, faces, R_cv, t_cv, K, H, W, texture, grads, bg=(1.0, 1.0, 1.0), window=None,
+                  precision="f32"):
+    """Reference fwd+bwd (CPU) of views given as OpenCV poses: outputs, leaf grads (verts, R, t).
+    precision="f64": the oracle's float64 shadow (tests.helpers.report's conditioning measure)."""
     N = R_cv.shape[0]
     vr = verts.clone().requires_grad_(True)
     Rr = R_cv.clone().requires_grad_(True)
     tr = t_cv.clone().requires_grad_(True)
     Rp, Tp = cv_to_p3d(Rr, tr)
-    ref = O.render_ref(vr, faces, Rp, Tp, intr_from_K(K, H, W, N), H, W, texture=texture, bg=bg, window=window)
+    ref = O.render_ref(vr, faces, Rp, Tp, intr_from_K(K, H, W, N), H, W, texture=texture, bg=bg, window=window,
+                       precision=precision)
     gD, gS, gC = grads
     ((ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()).backward()
     return ref, (vr.grad, Rr.grad, tr.grad)
+
+
+def _oracle_flat(*a, **kw):
+    """_oracle_views as a flat tuple for tests.helpers.oracle_runs: (depth, sil, rgb, grad verts,
+    grad R_cv, grad t_cv, pix_to_face[..., 0])."""
+    ref, g = _oracle_views(*a, **kw)
+    return (ref["depth"], ref["sil"], ref["rgba"][..., :3]) + tuple(g) + (ref["p2f"][..., 0],)
+
+
+_NAMES = ("depth", "sil", "rgb", "grad verts", "grad R_cv", "grad t_cv")
+
+
+def _report_all(tag, gots, ref, r64, sp):
+    """report() every output and gradient against the f32 oracle, its f64 shadow and the spread."""
+    for i, (nm, a) in enumerate(zip(_NAMES, gots)):
+        report(f"{tag} {nm}", a, ref[i], ref64=r64[i], sens=sp[i])
 
 
 def _gpu_views(verts, faces, tex, R_cv, t_cv, K, H, W, grads, want_p2f=True, bg=(1.0, 1.0, 1.0)):
@@ -114,14 +133,11 @@ def test_c1_sphere_256_one_view():
     _, _, _, (R_cv, t_cv, K) = canonical_views(verts, 1, H, W)
     white = torch.ones_like(verts)
     grads = _upstream(1, H, W)
-    ref, rg = _oracle_views(verts, faces, R_cv, t_cv, K, H, W, ("vertex", white), grads)
+    ref, r64, sp = oracle_runs(lambda p: _oracle_flat(verts, faces, R_cv, t_cv, K, H, W, ("vertex", white), grads,
+                                                      precision=p))
     out, gg = _gpu_views(verts, faces, TexturesVertex([white.to(DEV)]), R_cv, t_cv, K, H, W, grads)
-    assert torch.equal(out["pix_to_face32"].cpu().long(), ref["p2f"][..., 0])
-    report("C1 depth", out["depth"], ref["depth"])
-    report("C1 sil", out["sil"], ref["sil"])
-    report("C1 rgb", out["rgb"], ref["rgba"][..., :3])
-    for nm, a, b in zip(("verts", "R_cv", "t_cv"), gg, rg):
-        report(f"C1 grad {nm}", a, b)
+    assert torch.equal(out["pix_to_face32"].cpu().long(), ref[6])
+    _report_all("C1", (out["depth"], out["sil"], out["rgb"]) + tuple(gg), ref, r64, sp)
     _check_background(out, out["pix_to_face32"], (1.0, 1.0, 1.0))
 
 
@@ -141,14 +157,15 @@ def test_c2_teapot_512_batch8_forward():
     sel = [0, 5]
     grads = _upstream(2, H, W)
     ref, _ = _oracle_views(verts, faces, R_cv[sel], t_cv[sel], K, H, W, ("vertex", vcol), grads)
+    r64, _ = _oracle_views(verts, faces, R_cv[sel], t_cv[sel], K, H, W, ("vertex", vcol), grads, precision="f64")
     Fn = faces.shape[0]
     for j, n in enumerate(sel):
         exp = ref["p2f"][j, ..., 0]
         exp = torch.where(exp >= 0, exp - j * Fn + n * Fn, exp)  # packed id of view n in the batch of 8
         assert torch.equal(p2f[n].cpu(), exp), f"view {n}: pix_to_face differs from the oracle"
-        report(f"C2 view{n} depth", out["depth"][n], ref["depth"][j])
-        report(f"C2 view{n} sil", out["sil"][n], ref["sil"][j])
-        report(f"C2 view{n} rgb", out["rgb"][n], ref["rgba"][j, ..., :3])
+        report(f"C2 view{n} depth", out["depth"][n], ref["depth"][j], ref64=r64["depth"][j])
+        report(f"C2 view{n} sil", out["sil"][n], ref["sil"][j], ref64=r64["sil"][j])
+        report(f"C2 view{n} rgb", out["rgb"][n], ref["rgba"][j, ..., :3], ref64=r64["rgba"][j, ..., :3])
 
 
 def test_metric_config_cow_512_64views_fwd_bwd():
@@ -181,13 +198,10 @@ def test_metric_config_cow_512_64views_fwd_bwd():
         assert torch.equal(torch.where(q >= 0, q - j * Fn + n * Fn, q), p2f[n])
         assert torch.equal(gg2[1][j], gg[1][n]) and torch.equal(gg2[2][j], gg[2][n]), \
             f"view {n}: pose gradients depend on the batch"
-    ref, rg = _oracle_views(verts, faces, R_cv[sel], t_cv[sel], K, H, W, ("uv", vuv, fuv, img), sub_grads)
-    assert torch.equal(out2["pix_to_face32"].cpu().long(), ref["p2f"][..., 0])
-    report("metric depth", out2["depth"], ref["depth"])
-    report("metric sil", out2["sil"], ref["sil"])
-    report("metric rgb", out2["rgb"], ref["rgba"][..., :3])
-    for nm, a, b in zip(("verts", "R_cv", "t_cv"), gg2, rg):
-        report(f"metric grad {nm}", a, b)
+    ref, r64, sp = oracle_runs(lambda p: _oracle_flat(verts, faces, R_cv[sel], t_cv[sel], K, H, W,
+                                                      ("uv", vuv, fuv, img), sub_grads, precision=p))
+    assert torch.equal(out2["pix_to_face32"].cpu().long(), ref[6])
+    _report_all("metric", (out2["depth"], out2["sil"], out2["rgb"]) + tuple(gg2), ref, r64, sp)
 
 
 def _pose_model_step(meshes, verts_leaf, cams, q_init, refs, lr=1e-3):
@@ -315,7 +329,16 @@ def test_c4_dolphin_1024_64views_sharded_equals_unsharded():
         assert torch.equal(torch.where(q >= 0, q + s0 * Fn, q), p2f[s0:s0 + n])
         assert torch.equal(gsh[1], gfull[1][s0:s0 + n]) and torch.equal(gsh[2], gfull[2][s0:s0 + n])
         vsum += gsh[0]
-    report("C4 vertex grad (sum of shards)", vsum, gfull[0])
+    # the shared vertex gradient is a sum over views (and, inside a view, over pixels) whose order
+    # differs between the sharded and unsharded runs (float atomics): its conditioning is the sum
+    # of the views' absolute contributions, measured from 64 single-view renders; an 8-ulp
+    # (1e-6 relative) change of every view's contribution bounds the spread (tests.helpers.report)
+    cond = torch.zeros_like(gfull[0])
+    for n in range(N):
+        _, g1 = _gpu_views(verts, faces, white, R_cv[n:n + 1], t_cv[n:n + 1], K, H, W,
+                           tuple(x[n:n + 1] for x in grads), want_p2f=False)
+        cond += g1[0].abs()
+    report("C4 vertex grad (sum of shards)", vsum, gfull[0], sens=1e-6 * cond)
 
 
 def test_c5_subdivided_sphere_1024_vertex_grads():
@@ -369,12 +392,22 @@ def test_c5_subdivided_sphere_1024_vertex_grads():
     ref = O.render_ref(vr, faces, R[j:j + 1], T[j:j + 1], intr, H, W, texture=("vertex", vcol),
                        light={"kind": "ambient", "ambient": (1.0, 1.0, 1.0)}, persp=False, window=win)
     (ref["rgba"] * go).sum().backward()
+    # float64 shadow of the same (conditioning of each entry, tests.helpers.report)
+    v64 = verts.clone().requires_grad_(True)
+    r64 = rgb.detach().cpu().clone().requires_grad_(True)
+    g = torch.Generator().manual_seed(3)
+    vcol64 = torch.nn.functional.hardtanh(r64 + torch.rand(r64.shape, generator=g) * 0.5, 0.0, 1.0)[0]
+    s64 = O.render_ref(v64, faces, R[j:j + 1], T[j:j + 1], intr, H, W, texture=("vertex", vcol64),
+                       light={"kind": "ambient", "ambient": (1.0, 1.0, 1.0)}, persp=False, window=win,
+                       precision="f64")
+    (s64["rgba"] * go.double()).sum().backward()
     p2f_ref = ref["p2f"][0, y0:y1, x0:x1, 0]
     assert (p2f_ref >= 0).any() and (p2f_ref < 0).any(), "window must cross the silhouette"
     assert torch.equal(frag.pix_to_face[0, y0:y1, x0:x1, 0].cpu(), p2f_ref)
-    report("C5 rgba (window)", img[0, y0:y1, x0:x1], ref["rgba"][0, y0:y1, x0:x1])
-    report("C5 grad verts", vg.grad, vr.grad)
-    report("C5 grad colours", rgb.grad, rr.grad)
+    report("C5 rgba (window)", img[0, y0:y1, x0:x1], ref["rgba"][0, y0:y1, x0:x1],
+           ref64=s64["rgba"][0, y0:y1, x0:x1])
+    report("C5 grad verts", vg.grad, vr.grad, ref64=v64.grad)
+    report("C5 grad colours", rgb.grad, rr.grad, ref64=r64.grad)
 
 
 def test_determinism_metric_config():
@@ -416,13 +449,15 @@ def test_large_image_count_scan_fill_path():
     win = (y0, y0 + 96, x0, x0 + 96)
     grads = _upstream(1, H, W, window=win)
     out, gg = _gpu_views(verts, faces, tex, R_cv, t_cv, K, H, W, grads)
-    ref, rg = _oracle_views(verts, faces, R_cv, t_cv, K, H, W, ("uv", vuv, fuv, img), grads, window=win)
-    p2f_ref = ref["p2f"][0, y0:y0 + 96, x0:x0 + 96, 0]
+    ref, r64, sp = oracle_runs(lambda p: _oracle_flat(verts, faces, R_cv, t_cv, K, H, W, ("uv", vuv, fuv, img),
+                                                      grads, window=win, precision=p))
+    p2f_ref = ref[6][0, y0:y0 + 96, x0:x0 + 96]
     assert (p2f_ref >= 0).any() and (p2f_ref < 0).any(), "window must cross the silhouette"
     assert torch.equal(out["pix_to_face32"][0, y0:y0 + 96, x0:x0 + 96].cpu().long(), p2f_ref)
-    for k, r in (("depth", ref["depth"]), ("sil", ref["sil"]), ("rgb", ref["rgba"][..., :3])):
-        report(f"1040 {k} (window)", out[k][0, y0:y0 + 96, x0:x0 + 96], r[0, y0:y0 + 96, x0:x0 + 96])
-    for nm, a, b in zip(("verts", "R_cv", "t_cv"), gg, rg):
-        report(f"1040 grad {nm}", a, b)
+    crop = lambda t: t[0, y0:y0 + 96, x0:x0 + 96]  # noqa: E731
+    for i, k in enumerate(("depth", "sil", "rgb")):
+        report(f"1040 {k} (window)", crop(out[k]), crop(ref[i]), ref64=crop(r64[i]), sens=crop(sp[i]))
+    for i, (nm, a) in enumerate(zip(("verts", "R_cv", "t_cv"), gg)):
+        report(f"1040 grad {nm}", a, ref[3 + i], ref64=r64[3 + i], sens=sp[3 + i])
     assert torch.equal(out["pix_to_face32"].long(), _modular_p2f(verts, faces, R_cv, t_cv, K, H, W))
     _check_background(out, out["pix_to_face32"], (1.0, 1.0, 1.0))

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from tests.helpers import canonical_views, mesh_arrays
+from tests.helpers import canonical_views, mesh_arrays, oracle_runs, report
 from torch_renderer_amd import kernels as Kn
 
 pytestmark = pytest.mark.gpu
@@ -35,19 +35,32 @@ def _run(name, H, W, N, texture, light_kind=0, persp=True, seed=1, bg=(1.0, 1.0,
     light = dict(O.DEFAULT_LIGHT)
     if light_kind == 1:
         light = {"kind": "ambient", "ambient": (1.0, 1.0, 1.0)}
-    # reference (CPU autograd)
-    vr = verts.clone().requires_grad_(True)
-    Rr = R.clone().requires_grad_(True)
-    Tr = T.clone().requires_grad_(True)
-    vcr = vcol.clone().requires_grad_(True) if vcol is not None else None
-    tex_r = ("vertex", vcr) if texture == "vertex" else tex_ref
-    ref = O.render_ref(vr, faces, Rr, Tr, intr, H, W, texture=tex_r, light=light, persp=persp, bg=bg)
     gen = torch.Generator().manual_seed(seed)
     gD = torch.rand(N, H, W, generator=gen) * 2 - 1
     gS = torch.rand(N, H, W, generator=gen) * 2 - 1
     gC = torch.rand(N, H, W, 3, generator=gen) * 2 - 1
-    loss = (ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()
-    loss.backward()
+
+    def oracle(precision):  # reference (CPU autograd); "f64": its float64 shadow
+        vr = verts.clone().requires_grad_(True)
+        Rr = R.clone().requires_grad_(True)
+        Tr = T.clone().requires_grad_(True)
+        vcr = vcol.clone().requires_grad_(True) if vcol is not None else None
+        tex_r = ("vertex", vcr) if texture == "vertex" else tex_ref
+        ref = O.render_ref(vr, faces, Rr, Tr, intr, H, W, texture=tex_r, light=light, persp=persp, bg=bg,
+                           precision=precision)
+        dt = ref["rgba"].dtype
+        loss = (ref["depth"] * gD.to(dt)).sum() + (ref["sil"] * gS.to(dt)).sum() + (ref["rgba"][..., :3] * gC.to(dt)).sum()
+        loss.backward()
+        return ref, (vr, Rr, Tr, vcr)
+
+    def flat(precision):
+        ref, lv = oracle(precision)
+        z = torch.zeros(1)
+        return (ref["depth"], ref["sil"], ref["rgba"][..., :3]) + tuple(x.grad if x is not None else z for x in lv)
+
+    ref, (vr, Rr, Tr, vcr) = oracle("f32")
+    r32, r64, sp = oracle_runs(flat)  # f32 oracle, float64 shadow, per-entry spread (tests.helpers.report)
+    ref["shadow"] = (r64, sp)
     # GPU
     cfg = Kn.ShadeConfig(H=H, W=W, persp=persp, light_kind=light_kind, background=bg, want_p2f=True)
     if light_kind == 1:
@@ -63,11 +76,13 @@ def _run(name, H, W, N, texture, light_kind=0, persp=True, seed=1, bg=(1.0, 1.0,
     return ref, out, (vr, Rr, Tr, vcr), (vg, Rg, Tg, vcg)
 
 
-def _close(a, b, tol=1e-4, rel_scale=True):
-    a, b = a.detach().cpu(), b.detach().cpu()
-    scale = max(1.0, b.abs().max().item()) if rel_scale else 1.0
-    err = (a - b).abs().max().item()
-    assert err <= tol * scale, f"max abs err {err} (scale {scale})"
+def _close(a, b, tol=1e-4, rel_scale=True, sens=None, ref64=None):
+    """Per-entry bar (tests.helpers.report): |a_i - b_i| <= tol * max(1, |b_i|), or tol absolute
+    (rel_scale=False, images), named by call site."""
+    import inspect
+
+    fr = inspect.stack()[1]
+    report(f"{fr.function}:{fr.lineno}", a, b, tol=tol, rel_above_one=rel_scale, sens=sens, ref64=ref64)
 
 
 @pytest.mark.parametrize("name,H,W,N,texture", [
@@ -79,20 +94,22 @@ def test_render_forward_backward(name, H, W, N, texture):
     ref, out, leaves_r, leaves_g = _run(name, H, W, N, texture)
     p2f_ref = ref["p2f"][..., 0]
     assert torch.equal(out["pix_to_face32"].cpu().long(), p2f_ref)
-    _close(out["depth"], ref["depth"], rel_scale=False)
-    _close(out["sil"], ref["sil"], rel_scale=False)
-    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False)
-    for gr, gg, nm in zip(leaves_r, leaves_g, ("verts", "R", "T", "vcolors")):
+    r64, sp = ref["shadow"]
+    _close(out["depth"], ref["depth"], rel_scale=False, ref64=r64[0], sens=sp[0])
+    _close(out["sil"], ref["sil"], rel_scale=False, ref64=r64[1], sens=sp[1])
+    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
+    for i, (gr, gg, nm) in enumerate(zip(leaves_r, leaves_g, ("verts", "R", "T", "vcolors"))):
         if gr is None:
             continue
         assert gg.grad is not None, nm
-        _close(gg.grad, gr.grad)
+        _close(gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])
 
 
 def test_render_ambient_no_perspective():
     ref, out, leaves_r, leaves_g = _run("sphere", 48, 48, 1, "vertex", light_kind=1, persp=False)
     assert torch.equal(out["pix_to_face32"].cpu().long(), ref["p2f"][..., 0])
-    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False)
-    for gr, gg in zip(leaves_r, leaves_g):
+    r64, sp = ref["shadow"]
+    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
+    for i, (gr, gg) in enumerate(zip(leaves_r, leaves_g)):
         if gr is not None:
-            _close(gg.grad, gr.grad)
+            _close(gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])

@@ -12,7 +12,7 @@ import pytest
 import torch
 
 from oracle import oracle as O
-from tests.helpers import canonical_views, mesh_arrays, report
+from tests.helpers import canonical_views, mesh_arrays, oracle_runs, report
 from torch_renderer_amd import Meshes, TexturesUV, TexturesVertex
 from torch_renderer_amd.cameras import PerspectiveCameras
 from torch_renderer_amd.mesh_renderer import (BlendParams, Fragments, HardPhongShader, Materials, PointLights,
@@ -44,32 +44,61 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
     mat = {"ambient": (1.0, 0.9, 0.8), "diffuse": (1.0, 1.0, 0.7), "specular": (0.6, 1.0, 1.0), "shininess": 32.0}
     cc = torch.tensor([[0.1, -0.2, 0.3]])
     bg = (0.1, 0.2, 0.3)
-    # oracle shading on leaves
-    zb, ba, di = _leaf(ref["zbuf"]), _leaf(ref["bary"]), _leaf(ref["dists"])
-    vr = _leaf(verts)
-    local = p2f.clone()
-    local[p2f >= 0] = p2f[p2f >= 0] % faces.shape[0]
-    if texture == "vertex":
-        vcr = _leaf(torch.rand(verts.shape, generator=g))
-        texels = O.sample_textures_vertex(local, ba, vcr, faces)
-        tex_gpu_src = vcr
-    else:
+    vcol0 = torch.rand(verts.shape, generator=g) if texture == "vertex" else None
+    if texture == "uv":
         img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
-        mr = _leaf(img * 0.9 + 0.05)
+        map0 = img * 0.9 + 0.05
         vuv = torch.from_numpy(d["verts_uvs"]).float()
         fuv = torch.from_numpy(d["faces_uvs"]).long()
-        texels = O.sample_textures_uv(local, ba, vuv, fuv, mr)
-    if shader == "phong":
-        colors = O.phong_colors(local, ba, vr, faces, texels, light, mat, cc)
-        out_ref = O.softmax_rgb_blend(colors, p2f, zb, di, 1e-4, 1e-4, bg)
-    elif shader == "hard":  # HardPhongShader: hard_rgb_blend of the same Phong colours
-        colors = O.phong_colors(local, ba, vr, faces, texels, light, mat, cc)
-        out_ref = O.hard_rgb_blend(colors, p2f, bg)
-    else:
-        sil = O.sigmoid_alpha(p2f, di, 1e-4)
-        out_ref = torch.cat([torch.ones(sil.shape + (3,)), sil[..., None]], -1)
+    local = p2f.clone()
+    local[p2f >= 0] = p2f[p2f >= 0] % faces.shape[0]
+
+    def oracle(dt):  # oracle shading on leaves; float64: its shadow (tests.helpers.report's conditioning)
+        L = {k: _leaf(ref[k].to(dt)) for k in ("zbuf", "bary", "dists")}
+        zbf, bry, dst = (O._jitter(L[k]) for k in ("zbuf", "bary", "dists"))  # probe (inside O.perturbed only)
+        L["verts"] = _leaf(verts.to(dt))
+        if texture == "vertex":
+            L["tex"] = _leaf(vcol0.to(dt))
+            texels = O.sample_textures_vertex(local, bry, L["tex"], faces)
+        else:
+            L["tex"] = _leaf(map0.to(dt))
+            texels = O.sample_textures_uv(local, bry, vuv.to(dt), fuv, L["tex"])
+        if shader == "phong":
+            colors = O.phong_colors(local, bry, L["verts"], faces, texels, light, mat, cc.to(dt))
+            o = O.softmax_rgb_blend(colors, p2f, zbf, dst, 1e-4, 1e-4, bg)
+        elif shader == "hard":  # HardPhongShader: hard_rgb_blend of the same Phong colours
+            colors = O.phong_colors(local, bry, L["verts"], faces, texels, light, mat, cc.to(dt))
+            o = O.hard_rgb_blend(colors, p2f, bg)
+        else:
+            sil = O.sigmoid_alpha(p2f, dst, 1e-4)
+            o = torch.cat([torch.ones(sil.shape + (3,), dtype=dt), sil[..., None]], -1)
+        return O._jitter(o, False), L
+
+    out_ref, Lr = oracle(torch.float32)
     go = torch.rand(out_ref.shape, generator=g) - 0.5
     (out_ref * go).sum().backward()
+    zb, ba, di, vr = Lr["zbuf"], Lr["bary"], Lr["dists"], Lr["verts"]
+    tex_gpu_src = Lr["tex"]
+    if texture == "vertex":
+        vcr = Lr["tex"]
+    else:
+        mr = Lr["tex"]
+    keys = ("out", "zbuf", "bary", "dists", "verts", "tex")
+
+    def flat(precision):
+        o, L = oracle(torch.float32 if precision == "f32" else torch.float64)
+        (o * go.to(o.dtype)).sum().backward()
+        z = torch.zeros(1)
+        return (o,) + tuple(L[k].grad if L[k].grad is not None else z for k in keys[1:])
+
+    _, r64l, spl = oracle_runs(flat)
+    out64 = r64l[0]
+
+    def g64(k):
+        return r64l[keys.index(k)] if Lr[k].grad is not None else None
+
+    def spread(k):
+        return spl[keys.index(k)] if Lr[k].grad is not None else None
     # HIP shader on the same fragments
     zg, bgp, dg = (_leaf(t.to(DEV)) for t in (ref["zbuf"], ref["bary"], ref["dists"]))
     vg = _leaf(verts.to(DEV))
@@ -93,19 +122,19 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
     else:
         out = SoftSilhouetteShader(blend_params=blend)(frags, meshes, cameras=cams)
     tag = f"K={K} {texture} {shader}"
-    report(f"{tag} rgba", out, out_ref)
+    report(f"{tag} rgba", out, out_ref, ref64=out64, sens=spl[0])
     (out * go.to(DEV)).sum().backward()
     if shader == "hard":  # no depth / distance dependence
         assert not zg.grad.any() and not dg.grad.any()
         assert zb.grad is None or not zb.grad.any()
     else:
-        report(f"{tag} grad dists", dg.grad, di.grad)
+        report(f"{tag} grad dists", dg.grad, di.grad, ref64=g64("dists"), sens=spread("dists"))
     if shader in ("phong", "hard"):
         if shader == "phong":
-            report(f"{tag} grad zbuf", zg.grad, zb.grad)
-        report(f"{tag} grad bary", bgp.grad, ba.grad)
-        report(f"{tag} grad verts", vg.grad, vr.grad)
+            report(f"{tag} grad zbuf", zg.grad, zb.grad, ref64=g64("zbuf"), sens=spread("zbuf"))
+        report(f"{tag} grad bary", bgp.grad, ba.grad, ref64=g64("bary"), sens=spread("bary"))
+        report(f"{tag} grad verts", vg.grad, vr.grad, ref64=g64("verts"), sens=spread("verts"))
         if texture == "vertex":
-            report(f"{tag} grad vcolors", vcg.grad, vcr.grad)
+            report(f"{tag} grad vcolors", vcg.grad, vcr.grad, ref64=g64("tex"), sens=spread("tex"))
         else:
-            report(f"{tag} grad map", mg.grad, mr.grad)
+            report(f"{tag} grad map", mg.grad, mr.grad, ref64=g64("tex"), sens=spread("tex"))

@@ -54,6 +54,8 @@ class CamerasBase:
         n = len(self)
         if not -n <= i < n:
             raise IndexError(f"camera index {i} out of range for a batch of {n}")
+        if i < 0:  # cams[-1] is the last camera (a slice v[-1:0] would be empty)
+            i += n
         c = copy.copy(self)
         c.__dict__ = {k: v for k, v in self.__dict__.items() if not k.startswith("_") or k in ("_in_ndc",)}
         for k, v in list(c.__dict__.items()):

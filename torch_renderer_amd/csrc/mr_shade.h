@@ -117,8 +117,14 @@ MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b,
   c = ok[2] ? v[2] : z;
   d = ok[3] ? v[3] : z;
 }
+// The sample position (and so the texel cell, where the bilinear gradient jumps) is computed in
+// IEEE float32 with torch's operation order — uv = (b0 u0 + b1 u1) + b2 u2 (interpolate_face_
+// attributes), uv * 2 - 1 (TexturesUV), ((g + 1) / 2) * (size - 1) (grid_sample, align_corners) —
+// so that, given bitwise-equal barycentrics, the cell is the oracle's: a contracted (FMA) position
+// one ulp off a texel boundary picks the neighbouring cell and a different gradient. The weights and
+// the blend after it are continuous in the position and keep fast arithmetic.
+MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3]);
 MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t) {
-  MR_FP_FAST
   const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
   float ix = ((gx + 1.0f) / 2.0f) * (float)(S.tex_w - 1);
   float iy = ((gy + 1.0f) / 2.0f) * (float)(S.tex_h - 1);
@@ -130,6 +136,11 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
   t.iy = iy;
   t.x0 = (int)floorf(ix);
   t.y0 = (int)floorf(iy);
+  tex_blend(S, t, out);
+}
+MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3]) {
+  MR_FP_FAST
+  const float ix = t.ix, iy = t.iy;
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   const float nw = (x1 - ix) * (y1 - iy), ne = (ix - x0) * (y1 - iy);
   const float sw = (x1 - ix) * (iy - y0), se = (ix - x0) * (iy - y0);
@@ -235,6 +246,11 @@ MR_DEV float interp3(float b0, float b1, float b2, float a0, float a1, float a2)
   MR_FP_FAST
   return (b0 * a0 + b1 * a1) + b2 * a2;
 }
+// The same in IEEE float32, torch's order ((p0 + p1) + p2, no contraction): the uv interpolant that
+// picks the texel cell (tex_sample).
+MR_DEV float interp3_ieee(float b0, float b1, float b2, float a0, float a1, float a2) {
+  return (b0 * a0 + b1 * a1) + b2 * a2;
+}
 
 // Intermediate values kept for the backward pass.
 struct ShadeCache {
@@ -264,8 +280,8 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
       C.amb[k] = S.mat_amb[k] * S.light_amb[k];
     }
     if (S.tex_kind == 2) {
-      const float u = interp3(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
-      const float v = interp3(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
+      const float u = interp3_ieee(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
+      const float v = interp3_ieee(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
       tex_sample(S, u, v, C.texel, C.tap);
     } else if (S.tex_kind == 1) {
       for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);
@@ -655,8 +671,8 @@ MR_DEV void phong_fwd(const ShadeParams& S, int n, const PixGeom& G, float b0, f
     C.amb[k] = S.mat_amb[k] * S.light_amb[k];
   }
   if (S.tex_kind == 2) {
-    const float u = interp3(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
-    const float v = interp3(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
+    const float u = interp3_ieee(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
+    const float v = interp3_ieee(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
     tex_sample(S, u, v, C.texel, C.tap);
   } else if (S.tex_kind == 1) {
     for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);

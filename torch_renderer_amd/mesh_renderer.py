@@ -68,11 +68,17 @@ class BlendParams:
 
 
 def _bg_triple(bp):
-    """background_color as floats, converted once per BlendParams object (cached on it)."""
-    key = id(bp.background_color)
+    """background_color as floats. Upstream reads the field on every call, so a colour mutated in
+    place or reassigned takes effect: cached only for an unchanged tensor (same storage and
+    version; its conversion is a host read), re-read for lists / tuples (three floats, no device
+    work)."""
+    bc = bp.background_color
+    if not torch.is_tensor(bc):
+        return _triple(bc, None, "BlendParams.background_color")
+    key = (bc.data_ptr(), bc._version, tuple(bc.shape), str(bc.device))
     c = bp.__dict__.get("_bg_cache")
     if c is None or c[0] != key:
-        c = (key, _triple(bp.background_color, None, "BlendParams.background_color"))
+        c = (key, _triple(bc, None, "BlendParams.background_color"))
         bp.__dict__["_bg_cache"] = c
     return c[1]
 
@@ -94,42 +100,88 @@ def _triple(x, default, what="lights/materials"):
     return tuple(float(v) for v in t.cpu())
 
 
+def _triple_property(name, what):
+    """A light / material field that re-converts on assignment (upstream reads the tensors on every
+    call, so e.g. renderer.py:82-83 ``lights.location = ...`` takes effect on the next render). The
+    getter returns what was assigned; ``_name`` holds the float triple the kernels take."""
+    def get(self):
+        return self.__dict__["_raw_" + name]
+
+    def set_(self, v):
+        self.__dict__["_" + name] = _triple(v, None, what)  # validates (grad, shape) on assignment
+        self.__dict__["_raw_" + name] = v
+
+    return property(get, set_)
+
+
 class PointLights:
     """upstream lighting.py PointLights (one light shared by the batch)."""
 
+    location = _triple_property("location", "PointLights.location")
+    ambient_color = _triple_property("ambient", "PointLights.ambient_color")
+    diffuse_color = _triple_property("diffuse", "PointLights.diffuse_color")
+    specular_color = _triple_property("specular", "PointLights.specular_color")
+
     def __init__(self, ambient_color=((0.5, 0.5, 0.5),), diffuse_color=((0.3, 0.3, 0.3),),
                  specular_color=((0.2, 0.2, 0.2),), location=((0, 1, 0),), device="cpu"):
-        self.ambient_color = _triple(ambient_color, None)
-        self.diffuse_color = _triple(diffuse_color, None)
-        self.specular_color = _triple(specular_color, None)
-        self.location = location
-        self._location = _triple(location, None, "PointLights.location")
         self.device = device
+        self.ambient_color = ambient_color
+        self.diffuse_color = diffuse_color
+        self.specular_color = specular_color
+        self.location = location
 
     def location_tuple(self):
-        return self._location
+        return self.__dict__["_location"]
+
+    def color_tuples(self):
+        """(ambient, diffuse, specular) as float triples."""
+        return self.__dict__["_ambient"], self.__dict__["_diffuse"], self.__dict__["_specular"]
 
 
 class AmbientLights:
     """upstream lighting.py AmbientLights (mesh_deformer.py:113): colour = ambient * texel."""
 
+    ambient_color = _triple_property("ambient", "AmbientLights.ambient_color")
+
     def __init__(self, ambient_color=((1.0, 1.0, 1.0),), device="cpu"):
-        self.ambient_color = _triple(ambient_color, None)
         self.device = device
+        self.ambient_color = ambient_color
+
+    def ambient_tuple(self):
+        return self.__dict__["_ambient"]
 
 
 class Materials:
     """upstream materials.py Materials."""
 
+    ambient_color = _triple_property("ambient", "Materials.ambient_color")
+    diffuse_color = _triple_property("diffuse", "Materials.diffuse_color")
+    specular_color = _triple_property("specular", "Materials.specular_color")
+
     def __init__(self, ambient_color=((1, 1, 1),), diffuse_color=((1, 1, 1),), specular_color=((1, 1, 1),),
                  shininess=64, device="cpu"):
-        self.ambient_color = _triple(ambient_color, None)
-        self.diffuse_color = _triple(diffuse_color, None)
-        self.specular_color = _triple(specular_color, None)
-        if torch.is_tensor(shininess) and shininess.requires_grad:
-            raise NotImplementedError("Materials.shininess: parameters that require grad are not supported")
-        self.shininess = float(torch.as_tensor(shininess).reshape(-1)[0].cpu())
         self.device = device
+        self.ambient_color = ambient_color
+        self.diffuse_color = diffuse_color
+        self.specular_color = specular_color
+        self.shininess = shininess
+
+    @property
+    def shininess(self):
+        return self.__dict__["_raw_shininess"]
+
+    @shininess.setter
+    def shininess(self, v):
+        if torch.is_tensor(v) and v.requires_grad:
+            raise NotImplementedError("Materials.shininess: parameters that require grad are not supported")
+        self.__dict__["_shininess"] = float(torch.as_tensor(v).reshape(-1)[0].cpu())
+        self.__dict__["_raw_shininess"] = v
+
+    def color_tuples(self):
+        return self.__dict__["_ambient"], self.__dict__["_diffuse"], self.__dict__["_specular"]
+
+    def shininess_value(self):
+        return self.__dict__["_shininess"]
 
 
 @dataclass
@@ -180,7 +232,7 @@ class MeshRasterizer(torch.nn.Module):
         cameras = kwargs.get("cameras", self.cameras)
         if cameras is None:
             raise ValueError("Cameras must be specified either at initialization or in the forward pass")
-        hw = self.raster_settings.hw()
+        hw = kwargs.get("raster_settings", self.raster_settings).hw()  # a per-call raster_settings wins
         R, T, intr = _views(meshes, cameras, hw, kwargs)
         if meshes.is_shared():
             return ProjectFaces.apply(meshes.shared_verts(), R, T, meshes.shared_faces(), intr.contiguous())
@@ -252,18 +304,15 @@ def _shade_config(sh, cameras, H, W, kwargs):
     mats = kwargs.get("materials", sh.materials)
     if isinstance(lights, AmbientLights):
         cfg.light_kind = 1
-        cfg.light_ambient = lights.ambient_color
+        cfg.light_ambient = lights.ambient_tuple()
     elif isinstance(lights, PointLights):
         cfg.light_kind = 0
         cfg.light_location = lights.location_tuple()
-        cfg.light_ambient = lights.ambient_color
-        cfg.light_diffuse = lights.diffuse_color
-        cfg.light_specular = lights.specular_color
+        cfg.light_ambient, cfg.light_diffuse, cfg.light_specular = lights.color_tuples()
     else:
         raise NotImplementedError(f"lights of type {type(lights).__name__}")
-    cfg.mat_ambient, cfg.mat_diffuse, cfg.mat_specular = (mats.ambient_color, mats.diffuse_color,
-                                                          mats.specular_color)
-    cfg.shininess = mats.shininess
+    cfg.mat_ambient, cfg.mat_diffuse, cfg.mat_specular = mats.color_tuples()
+    cfg.shininess = mats.shininess_value()
     cfg.want_sil = False
     cfg.rgb_channels = 4
     return cfg

@@ -193,8 +193,11 @@ class DepthColorRender(DifferentiableRenderer):
                 self._soft = (_soft_renderers(self, 1, None), _soft_renderers(self, 1, self._light_location))
             (rast, sil_r), (_, phong_r) = self._soft
             Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
-            depth = torch.relu(rast(meshes, R=Rs, T=ts).zbuf[..., 0])
-            return depth, sil_r(meshes, R=Rs, T=ts)[..., 3], phong_r(meshes, R=Rs, T=ts)[..., :3]
+            # one raster pass feeds all three (the three renderers' rasterizers are identical)
+            frags = rast(meshes, R=Rs, T=ts)
+            depth = torch.relu(frags.zbuf[..., 0])
+            sil = sil_r.shader(frags, meshes, R=Rs, T=ts)[..., 3]
+            return depth, sil, phong_r.shader(frags, meshes, R=Rs, T=ts)[..., :3]
         cfg = ShadeConfig(H=self._image_size[0], W=self._image_size[1], light_location=self._light_location)
         out = render_mesh_batch(meshes, self._cameras, self._image_size, R, tvec, cfg, pose_cv=True)
         return out["depth"], out["sil"], out["rgb"]

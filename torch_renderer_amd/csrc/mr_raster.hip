@@ -171,6 +171,7 @@ struct RasterWS {
   int* sface;  // (N*T*64) per slot, per tile pixel (row-major 8x8): winning face record or -1
   ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
   float* grows;    // (F, 27) the fused backward's per-face gradient rows, cleared by the forward
+  float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
   size_t bytes;
 };
@@ -215,6 +216,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
   w.grows = (float*)(b + off);
   off = align_up(off + sizeof(float) * 27 * (size_t)Fshade, 256);
+  w.frec = (float4*)(b + off);
+  off = align_up(off + sizeof(float4) * (Fshade > 0 ? 64 * NT : 0), 256);
   w.crec = (ClipRec*)(b + off);
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.bytes = off;
@@ -1398,6 +1401,7 @@ struct FwdParams {
   float* sil;
   float* rgb;
   int32_t* p2f32;  // optional
+  float4* frec;    // MODE 1: the winners' fragments for the backward (slot-major, 64 per slot)
 };
 
 // One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).
@@ -1918,6 +1922,9 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
       P.bary[3 * q + 1] = ev.b1;
       P.bary[3 * q + 2] = ev.b2;
     } else {
+      // the fragment the backward shades again (its barycentrics must be these bits: they pick the
+      // texel cell), so k_bwd_fused does not re-run eval_face's IEEE divisions
+      P.frec[(int64_t)s * 64 + lane] = make_float4(ev.b0, ev.b1, ev.b2, ev.sdist);
       ShadeOut o;
       ShadeCache C;
       shade_fwd(P.S, n, true, G, ev.b0, ev.b1, ev.b2, ev.pz, ev.sdist, o, C);
@@ -1959,6 +1966,7 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
   P.recs = w.recs; P.list = w.list; P.units = w.units; P.ctr = w.ctr; P.tkey = w.tkey;
   P.cnt = w.cnt; P.start = w.start; P.vbase = w.vbase; P.list_cap = g.list_cap; P.mfpb = g.mfpb;
   P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
+  P.frec = w.frec;
   return P;
 }
 
@@ -2690,6 +2698,7 @@ struct RenderBwdParams {
   const ViewRec* views;
   float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
+  const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
 };
 
 MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& px, int& py) {
@@ -2709,11 +2718,13 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // gradient; such values are never used): written as guarded loads they become branches whose
 // phi copies wait on the load right away, which defeats the prefetch.
 __device__ float g_zero4[4];
-MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int gt, int f, int lane, FaceRec& r, float g[5]) {
+MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
+                             float4& fr) {
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
   r = load_rec(P.recs, f < 0 ? 0 : f);
+  fr = P.frec[(int64_t)slot * 64 + lane];
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + pix : g_zero4;
   const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
@@ -2764,11 +2775,26 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 #else
 #define MR_BWD_ATTR
 #endif
+// The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
+// through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
+// loop, overflow the SGPR file and are spilled into VGPR lanes (one v_readlane per use; k_bwd_fused had
+// 70 spilled SGPRs and ~400 readlanes per slot iteration). Re-read per iteration, each is a scalar
+// load from the (cached) kernarg segment, live only where it is used.
+template <typename T>
+MR_DEV const T& kernarg_params() {
+  typedef const char __attribute__((address_space(4))) * cptr;
+  cptr p = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const T*)(const char*)p;
+}
+
 template <int ACC, bool CLIP>
-__global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P) {
+__global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
+  const RenderBwdParams& P = P0;
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
   __shared__ float4 lrec[4][MR_BWD_REC][64];
+  const bool lut = stage_tex_lut(P.S);  // the u8 texture table in LDS
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
@@ -2782,12 +2808,15 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   const int lz = lane_zero();
   const int slast = max(nslots - 1, 0);
   int sc = min(s, slast);
+  int sl_c = sc;  // slot of gt_c / f_c (clamped)
   int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
   sc = min(s + G, slast);
+  int sl_n = sc;
   int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
   FaceRec r_c;
   float g_c[5];
-  bwd_slot_inputs(P, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c);
+  float4 fr_c;
+  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
 #ifdef MR_PROF
@@ -2799,15 +2828,19 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 #define BACC(i) do {} while (0)
 #endif
   for (; s < send; s += G) {
+    const RenderBwdParams& P = kernarg_params<RenderBwdParams>();  // see kernarg_params
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c;
     const FaceRec r = r_c;
+    const float4 frag = fr_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
     gt_c = gt_n;
     f_c = f_n;
-    bwd_slot_inputs(P, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c);
+    sl_c = sl_n;
+    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
     sc = min(s + 2 * G, slast);
+    sl_n = sc;
     gt_n = P.stile[sc + lz];
     f_n = P.sface[(int64_t)sc * 64 + lane];
     int n, px, py;
@@ -2822,28 +2855,38 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
       const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
       FragEval e;
       float4 o[MR_BWD_REC];
+      // the forward's fragment (k_shade<1> wrote the winner's barycentrics, original-face ones for a
+      // near-plane sub-triangle, and signed distance); the depth from the record's corners in
+      // eval_face's operation order, or, for a sub-triangle (whose corners are not the original
+      // face's), from eval_face itself
+      e.b0 = frag.x;
+      e.b1 = frag.y;
+      e.b2 = frag.z;
+      e.sdist = frag.w;
+      e.pz = (e.b0 * r.z0 + e.b1 * r.z1) + e.b2 * r.z2;
+      if (CLIP && (r.flags & FR_CLIP)) {
+        FragEval es;
+        eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, es);
+        e.pz = es.pz;
+      }
 #ifdef MR_EXP_NOHALF1
       if (false) {  // experiment build: no shading backward (half 2 gets zero records)
 #else
-      if (eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, e)) {
+      {
 #endif
-        if (CLIP && (r.flags & FR_CLIP)) clip_unconvert(P.crec[f], e.b0, e.b1, e.b2, e.b0, e.b1, e.b2);
         ShadeOut so;
         ShadeCache C;
         BACC(1);
-        shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C);
+        shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C, lut);
         BACC(2);
         ShadeGrad SG;
-        shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG);
+        shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
         BACC(3);
         o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
         o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
         o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
         o[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
         o[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
-      } else {  // unreachable (slots hold kept fragments); a zero record contributes nothing
-#pragma unroll
-        for (int k = 0; k < MR_BWD_REC; ++k) o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][k][lane] = o[k];
@@ -3440,7 +3483,9 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
       } else if (k == R.kmax) {
         // silhouette: no depth dependence
       }
-      const float gd = -((g_prob * (prob * (1.0f - prob))) * isig);
+      float sp_, sq_;  // prob and 1 - prob, each accurate (sigmoid2): the derivative's factor
+      sigmoid2((-d) * isig, sp_, sq_);
+      const float gd = -((g_prob * (sp_ * sq_)) * isig);
       P.g_zbuf[base + k] = gz;
       P.g_dists[base + k] = gd;
       P.g_bary[3 * (base + k)] = gb[0];
@@ -4256,6 +4301,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.views = (const ViewRec*)views;
   P.gface = gface;
   P.rt_part = rt_part;
+  P.frec = w.frec;
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;

@@ -74,6 +74,18 @@ MR_DEV float dot3(const float a[3], const float b[3]) {
   return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
 }
 MR_DEV float sigmoidf_(float x) { return frcp(1.0f + fexp(-x)); }
+// sigmoid(x) and 1 - sigmoid(x), each to a few ulp of ITS OWN value. 1 - p is not formed as a
+// difference: near saturation (p -> 1, i.e. a pixel a few sigma inside a face) that cancels every
+// significant bit, and the blends' derivative p (1 - p) / sigma (x 1e4) carries the loss straight into
+// the vertex gradients (torch's sigmoid backward has the same cancellation; the oracle's float64
+// shadow does not, and tests.helpers.report measures against both).
+MR_DEV void sigmoid2(float x, float& p, float& q) {
+  const float t = fexp(-fabsf(x));  // (0, 1]
+  const float r = frcp(1.0f + t);
+  const float big = r, small = t * r;  // 1 / (1 + t), t / (1 + t)
+  p = x >= 0.0f ? big : small;
+  q = x >= 0.0f ? small : big;
+}
 
 // ---- texture: grid_sample(bilinear, align_corners=True, border) on flipped map ----
 struct TexTap {
@@ -85,32 +97,48 @@ struct TexTap {
 // clamped and all four loads issued unconditionally, then the values selected: written as
 // guarded loads, the compiler sinks each into its own branch with a load + wait per tap. The
 // empty asm consumes the loaded values unconditionally, so the loads cannot be sunk.
-MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b, float4& c, float4& d) {
+// The 256-entry u8 -> float texture table staged in LDS by kernels that call stage_tex_lut (a
+// namespace-scope LDS array, so its reads are ds_read by construction).
+__shared__ float g_tex_lut[256];
+
+// lds_lut: read the table from g_tex_lut (the kernel staged it) instead of S.tex_lut. Texel indices
+// are 32-bit (maps < 2^32 texels): one 64-bit address add per tap instead of 64-bit index math.
+MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b, float4& c, float4& d,
+                     bool lds_lut = false) {
   const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
   bool ok[4];
   float4 v[4];
-  int64_t idx[4];
+  uint32_t idx[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int xc = xs[i & 1], yc = ys[i >> 1];
     ok[i] = (unsigned)xc < (unsigned)S.tex_w && (unsigned)yc < (unsigned)S.tex_h;
     const int x = ok[i] ? xc : 0, y = ok[i] ? yc : S.tex_h - 1;
-    idx[i] = (int64_t)(S.tex_h - 1 - y) * S.tex_w + x;  // torch.flip(maps, [H])
+    idx[i] = (uint32_t)(S.tex_h - 1 - y) * (uint32_t)S.tex_w + (uint32_t)x;  // torch.flip(maps, [H])
   }
-  if (S.tex8) {  // 4-B texels, the exact values through the 256-entry table (L1-resident)
+  if (S.tex8) {  // 4-B texels, the exact values through the 256-entry table (LDS or L1-resident)
     uchar4 u[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) u[i] = S.tex8[idx[i]];
     asm volatile("" ::"v"(*(const int*)&u[0]), "v"(*(const int*)&u[1]), "v"(*(const int*)&u[2]),
                  "v"(*(const int*)&u[3]));
+    if (lds_lut) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = make_float4(S.tex_lut[u[i].x], S.tex_lut[u[i].y], S.tex_lut[u[i].z], 0.0f);
+      for (int i = 0; i < 4; ++i) v[i] = make_float4(g_tex_lut[u[i].x], g_tex_lut[u[i].y], g_tex_lut[u[i].z], 0.0f);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = make_float4(S.tex_lut[u[i].x], S.tex_lut[u[i].y], S.tex_lut[u[i].z], 0.0f);
+    }
+    // consumed inside the branch: the table reads and the float-map loads below must not be merged
+    // into one load through a phi of pointers (that is a flat load, LDS or global unknown)
+    asm volatile("" ::"v"(v[0].x), "v"(v[0].y), "v"(v[0].z), "v"(v[1].x), "v"(v[1].y), "v"(v[1].z), "v"(v[2].x),
+                 "v"(v[2].y), "v"(v[2].z), "v"(v[3].x), "v"(v[3].y), "v"(v[3].z));
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = S.tex[idx[i]];
+    asm volatile("" ::"v"(v[0].x), "v"(v[0].y), "v"(v[0].z), "v"(v[1].x), "v"(v[1].y), "v"(v[1].z), "v"(v[2].x),
+                 "v"(v[2].y), "v"(v[2].z), "v"(v[3].x), "v"(v[3].y), "v"(v[3].z));
   }
-  asm volatile("" ::"v"(v[0].x), "v"(v[0].y), "v"(v[0].z), "v"(v[1].x), "v"(v[1].y), "v"(v[1].z), "v"(v[2].x),
-               "v"(v[2].y), "v"(v[2].z), "v"(v[3].x), "v"(v[3].y), "v"(v[3].z));
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   a = ok[0] ? v[0] : z;
   b = ok[1] ? v[1] : z;
@@ -123,8 +151,8 @@ MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b,
 // so that, given bitwise-equal barycentrics, the cell is the oracle's: a contracted (FMA) position
 // one ulp off a texel boundary picks the neighbouring cell and a different gradient. The weights and
 // the blend after it are continuous in the position and keep fast arithmetic.
-MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3]);
-MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t) {
+MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3], bool lut);
+MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t, bool lut = false) {
   const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
   float ix = ((gx + 1.0f) / 2.0f) * (float)(S.tex_w - 1);
   float iy = ((gy + 1.0f) / 2.0f) * (float)(S.tex_h - 1);
@@ -136,37 +164,50 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
   t.iy = iy;
   t.x0 = (int)floorf(ix);
   t.y0 = (int)floorf(iy);
-  tex_blend(S, t, out);
+  tex_blend(S, t, out, lut);
 }
-MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3]) {
+MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3], bool lut) {
   MR_FP_FAST
   const float ix = t.ix, iy = t.iy;
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   const float nw = (x1 - ix) * (y1 - iy), ne = (ix - x0) * (y1 - iy);
   const float sw = (x1 - ix) * (iy - y0), se = (ix - x0) * (iy - y0);
   float4 a, b, c, d;
-  tex_taps(S, t.x0, t.y0, a, b, c, d);
+  tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
   out[0] = ((a.x * nw + b.x * ne) + c.x * sw) + d.x * se;
   out[1] = ((a.y * nw + b.y * ne) + c.y * sw) + d.y * se;
   out[2] = ((a.z * nw + b.z * ne) + c.z * sw) + d.z * se;
 }
 // d(texel)/d(u,v) contracted with g (3 channels) -> (gu, gv)
-MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[3], float& gu, float& gv) {
+MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[3], float& gu, float& gv,
+                           bool lut = false) {
   MR_FP_FAST
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   float4 a, b, c, d;
-  tex_taps(S, t.x0, t.y0, a, b, c, d);
+  tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
   const float ga = (g[0] * a.x + g[1] * a.y) + g[2] * a.z;
   const float gb = (g[0] * b.x + g[1] * b.y) + g[2] * b.z;
   const float gc = (g[0] * c.x + g[1] * c.y) + g[2] * c.z;
   const float gd = (g[0] * d.x + g[1] * d.y) + g[2] * d.z;
-  float gix = -ga * (y1 - t.iy) + gb * (y1 - t.iy) - gc * (t.iy - y0) + gd * (t.iy - y0);
-  float giy = -ga * (x1 - t.ix) - gb * (t.ix - x0) + gc * (x1 - t.ix) + gd * (t.ix - x0);
+  // factored as differences of taps: exactly 0 where the four taps are equal (a uniform texture
+  // region), as in torch's grid_sample backward; the unfactored sum contracted into FMAs left the
+  // rounding error of one product there (x (W - 1) x 1 / face area at the vertices).
+  float gix = (gb - ga) * (y1 - t.iy) + (gd - gc) * (t.iy - y0);
+  float giy = (gc - ga) * (x1 - t.ix) + (gd - gb) * (t.ix - x0);
   gix = t.gx_ok ? gix : 0.0f;
   giy = t.gy_ok ? giy : 0.0f;
   // ix = ((2u-1+1)/2)*(W-1)  ->  d ix / d u = W-1
   gu = gix * (float)(S.tex_w - 1);
   gv = giy * (float)(S.tex_h - 1);
+}
+
+// Stage the 256-entry u8 -> float texture table in the workgroup's LDS (g_tex_lut; uniform call, every
+// thread of the workgroup; ends with a barrier). Returns the flag the shading functions take.
+MR_DEV bool stage_tex_lut(const ShadeParams& S) {
+  if (S.tex8)
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) g_tex_lut[i] = S.tex_lut[i];
+  __syncthreads();
+  return true;
 }
 
 // Per-pixel inputs gathered once for shading
@@ -257,12 +298,13 @@ struct ShadeCache {
   float P[3], Nn[3], nh[3], nlen, nden, l[3], lh[3], llen, lden, v[3], vh[3], vlen, vden;
   float cosd, r[3], vr, as, spow, texel[3], amb[3], diff[3], spec[3], col[3];
   float ps, pc, zi, zimax, E, w, ex, delta, den;
+  float qs, qc;  // 1 - ps, 1 - pc (unmasked: the derivatives' factor; sigmoid2)
   TexTap tap;
 };
 
 // Forward shading of one pixel (hit = face found). b = bary (after clip), z, sd = signed dist.
 MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, float b0, float b1, float b2,
-                      float z, float sd, ShadeOut& o, ShadeCache& C) {
+                      float z, float sd, ShadeOut& o, ShadeCache& C, bool lut = false) {
   MR_FP_FAST
   const float m = hit ? 1.0f : 0.0f;
   const float zb = hit ? z : -1.0f;    // zbuf background = -1
@@ -270,7 +312,8 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
   // DepthRender: relu(zbuf[..., 0])
   o.depth = zb > 0.0f ? zb : 0.0f;
   // SoftSilhouetteShader / sigmoid_alpha_blend
-  C.ps = sigmoidf_((-dd) * S.inv_sigma_sil) * m;
+  sigmoid2((-dd) * S.inv_sigma_sil, C.ps, C.qs);
+  C.ps *= m;
   o.sil = 1.0f - (1.0f - C.ps);
   // Phong colours (only meaningful for hit pixels; background weight is 0)
   for (int k = 0; k < 3; ++k) C.col[k] = 0.0f;
@@ -282,7 +325,7 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
     if (S.tex_kind == 2) {
       const float u = interp3_ieee(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
       const float v = interp3_ieee(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
-      tex_sample(S, u, v, C.texel, C.tap);
+      tex_sample(S, u, v, C.texel, C.tap, lut);
     } else if (S.tex_kind == 1) {
       for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);
     } else {
@@ -314,7 +357,8 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
   }
   // softmax_rgb_blend (K = 1)
   const float eps = 1e-10f;
-  C.pc = sigmoidf_((-dd) * S.inv_sigma_rgb) * m;
+  sigmoid2((-dd) * S.inv_sigma_rgb, C.pc, C.qc);
+  C.pc *= m;
   const float alpha = 1.0f - C.pc;
   C.zi = ((S.zfar - zb) * S.inv_zrange) * m;
   C.zimax = smax(C.zi, eps);
@@ -337,7 +381,8 @@ struct ShadeGrad {
 };
 
 MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1, float b2, float z,
-                      const ShadeCache& C, float gD, float gS, const float gRGB[3], float gA, ShadeGrad& R) {
+                      const ShadeCache& C, float gD, float gS, const float gRGB[3], float gA, ShadeGrad& R,
+                      bool lut = false) {
   MR_FP_FAST
   const float b[3] = {b0, b1, b2};
   R.gz = 0.0f;
@@ -350,7 +395,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   if (z > 0.0f) R.gz += gD;
   // silhouette: sil = 1 - (1 - ps), ps = sigmoid(-sd / sigma_sil)
   {
-    const float gx = gS * (C.ps * (1.0f - C.ps));
+    const float gx = gS * (C.ps * C.qs);
     R.gsd += -(gx * S.inv_sigma_sil);
   }
   // rgb = (w*col + delta*bg) / den
@@ -381,7 +426,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
     gzimax += -(gv * S.inv_gamma);
     gzi += (C.zi >= 1e-10f) ? gzimax : 0.0f;  // max over K=1, then clamp(min=eps)
     R.gz += -(gzi * S.inv_zrange);
-    const float gx = gp * (C.pc * (1.0f - C.pc));
+    const float gx = gp * (C.pc * C.qc);
     R.gsd += -(gx * S.inv_sigma_rgb);
   }
   // colours = (amb + diff) * texel + spec
@@ -433,7 +478,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   }
   if (S.tex_kind == 2) {
     float gu, gv;
-    tex_sample_bwd(S, C.tap, gtex, gu, gv);
+    tex_sample_bwd(S, C.tap, gtex, gu, gv, lut);
     for (int c = 0; c < 3; ++c) R.gb[c] += G.uv[c][0] * gu + G.uv[c][1] * gv;
   } else if (S.tex_kind == 1) {
     for (int c = 0; c < 3; ++c) {

@@ -171,9 +171,13 @@ def main():
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
     ap.add_argument("--texture", choices=("uv", "white"), default="uv",
                     help="experiments only: 'white' drops the UV texture (not the benchmark workload)")
-    ap.add_argument("--mode", choices=("render", "fragments", "soft"), default="render",
+    ap.add_argument("--mode", choices=("render", "fragments", "soft", "gather", "pose"), default="render",
                     help="render: the headline fwd+bwd step; fragments: the rasterizer alone "
-                         "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline)")
+                         "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline); "
+                         "soft: K=50 soft silhouette fwd+bwd (deform_mesh_with_color.py); gather: C4, depth "
+                         "render of --views views IN TOTAL sharded over the ranks + RCCL gather to rank 0 "
+                         "(batch_rendering_test.py, strong scaling); pose: C3, camera_pose_optimizer.py's step "
+                         "(three renders, calc_loss, backward, Adam) for --views poses per GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,6 +199,10 @@ def main():
         return bench_fragments(args, dev, world, rank)
     if args.mode == "soft":
         return bench_soft(args, dev, world, rank)
+    if args.mode == "gather":
+        return bench_gather(args, dev, world, rank)
+    if args.mode == "pose":
+        return bench_pose(args, dev, world, rank)
     from torch_renderer_amd import _lib
     from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset, load_asset_arrays
@@ -265,10 +273,18 @@ def main():
             fwd_bwd()
         run_fwd_bwd = graph.replay
 
-    def step():
+    ar_events = []  # (start, end) HIP events around each timed step's all_reduce (on the compute stream)
+
+    def step(timed=False):
         run_fwd_bwd()
         if world > 1:
+            if timed:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
             D.allreduce_grads([verts])  # the step's only exchange: shared vertex grads
+            if timed:
+                e1.record()
+                ar_events.append((e0, e1))
 
     for _ in range(2):
         step()
@@ -277,11 +293,19 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # the collective's share of the step as the compute stream sees it (RCCL's stream waits on it and
+    # the compute stream waits on RCCL): mean over the timed steps, max over ranks
+    allreduce_us = None
+    if ar_events:
+        allreduce_us = sum(a.elapsed_time(b) for a, b in ar_events) / len(ar_events) * 1e3
+        t_ar = torch.tensor([allreduce_us], device=dev, dtype=torch.float64)
+        dist.all_reduce(t_ar, op=dist.ReduceOp.MAX)
+        allreduce_us = t_ar.item()
     if world > 1:
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -350,6 +374,8 @@ def main():
                    "parallelism": f"view-sharded x{world}"},
         "roofline": roof, "forward_roofline": fwd_roof, "path_roofline": path_roof, "cpu_baseline": cpu,
         "work": wstats, "kernels": kernels,
+        "allreduce_us": None if allreduce_us is None else round(allreduce_us, 2),
+        "allreduce_bytes": 4 * 3 * int(verts0.shape[0]) if world > 1 else 0,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
@@ -524,6 +550,21 @@ def bench_soft(args, dev, world, rank):
         return
     value = nv * world * args.steps / elapsed
     kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    # the forward fragment pass's API-minimum bytes (SURVEY §8d at K = 50: 28 B per fragment slot + 36 B
+    # per face) against its kernels' summed time; the whole step's kernels beside it
+    Fn = faces.shape[0]
+    per_frame = 28 * K * H * W + 36 * Fn
+    frag_k = [k for k in ("k_bin_rect", "k_bin_view", "k_fill<0>", "k_raster_k") if k in kt]
+    us = sum(kt[k][1] / kt[k][0] * 1e3 for k in frag_k)
+    ach = per_frame * nv / max(us, 1e-9) * 1e-3
+    roof = {"bound": "hbm", "kernel": "fragment kernels (sum): " + ", ".join(frag_k), "bytes_per_frame": per_frame,
+            "us_per_step": round(us, 2), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4),
+            "step_kernels_us": round(sum(v[1] / max(v[0], 1) * 1e3 for v in kt.values()), 2)}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = soft_cpu_baseline(verts, faces, R, T, H, W, K, rs.blur_radius, sigma, target,
+                                n_views=min(args.cpu_views, nv))
     line = {
         "metric": f"frames/sec fwd+bwd, soft silhouette K={K}, {H}x{W} (deform_mesh_with_color.py)",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -533,11 +574,291 @@ def bench_soft(args, dev, world, rank):
                                "blur=ln(1/1e-4-1)*1e-4, perspective_correct=False, SoftSilhouetteShader, "
                                "L2 silhouette loss -> vertex grads",
                    "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "K": K, "parallelism": f"view-sharded x{world}"},
+        "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _time_steps(step, args, dev, world):
+    """warmup, then K timed steps between barrier + synchronize on both sides; max over ranks (s)."""
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = e.item()
+    return elapsed
+
+
+def _kernel_times(step, n):
+    from torch_renderer_amd import _lib
+
+    torch.cuda.synchronize()
+    _lib.timing_enable(True)
+    for _ in range(n):
+        step()
+    torch.cuda.synchronize()
+    kt = _lib.timing_read()
+    _lib.timing_enable(False)
+    return kt
+
+
+def bench_gather(args, dev, world, rank):
+    """C4 (batch_rendering_test.py:263-280, 320-328): the depth of a batch of --views views IN TOTAL
+    (dolphin at 1024x1024 for C4: --mesh dolphin --size 1024), rendered view-sharded across the ranks
+    (DepthRender's fused forward: relu(zbuf), background 0, as render_depth's `-1 -> 0`), then the
+    slices gathered to rank 0 over RCCL point-to-point (distributed.gather_to_root) inside the timed
+    step (the reference copies the batch to the host at :277). Strong scaling: the batch is fixed.
+    After timing, rank 0 renders the whole batch alone and checks the gathered depth bitwise."""
+    from torch_renderer_amd import distributed as D
+    from torch_renderer_amd.assets import load_asset
+    from torch_renderer_amd.torch_renderer import DepthRender
+
+    H = W = args.size
+    meshes = load_asset(args.mesh, device=dev, textures=False)
+    verts0 = meshes.shared_verts().detach().cpu()
+    Fn = meshes.shared_faces().shape[0]
+    n_total = args.views
+    R_all, t_all, K = canonical_views(verts0, n_total, H, W, dist_m=view_distance(args.mesh, verts0))
+    R_cv, t_cv = D.shard_views(R_all, t_all, rank=rank, world_size=world)
+    R_cv, t_cv = R_cv.to(dev).contiguous(), t_cv.to(dev).contiguous()
+    nv = R_cv.shape[0]
+    bmesh = meshes.extend(max(nv, 1))
+    renderer = DepthRender(K.to(dev), (H, W), device=dev)
+    g_events = []
+
+    def render():
+        with torch.no_grad():
+            return renderer.render(bmesh, R_cv, t_cv)
+
+    def step(timed=False):
+        depth = render()
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        out = D.gather_to_root(depth, n_total)
+        if timed:
+            e1.record()
+            g_events.append((e0, e1))
+        return out
+
+    elapsed = _time_steps(lambda: step(True), args, dev, world)
+    g_events[:] = g_events[args.warmup:]
+    gather_us = sum(a.elapsed_time(b) for a, b in g_events) / max(len(g_events), 1) * 1e3
+    if world > 1:
+        t = torch.tensor([gather_us], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gather_us = t.item()
+    kt = _kernel_times(render, min(args.steps, 10))
+    gathered = step()
+    equal = None
+    if rank == 0:
+        full = DepthRender(K.to(dev), (H, W), device=dev)
+        with torch.no_grad():
+            ref = full.render(meshes.extend(n_total), R_all.to(dev).contiguous(), t_all.to(dev).contiguous())
+        equal = bool(torch.equal(gathered, ref))
+    if world > 1:
+        dist.barrier()
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    value = n_total * args.steps / elapsed
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    per_frame = 4 * H * W + 36 * Fn  # depth out + face geometry (the fused depth-only forward)
+    us = sum(v[1] / max(v[0], 1) * 1e3 for v in kt.values())
+    line = {
+        "metric": f"frames/sec C4 depth render + RCCL gather to rank 0, {args.mesh} {H}x{W}, {n_total} views total",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32", "launch": "eager", "data": "synthetic camera poses on the reference mesh",
+        "config": {"workload": f"{args.mesh} (F={Fn}), {H}x{W}, {n_total} views in total split over {world} rank(s), "
+                               "DepthRender forward (relu(zbuf)), depth slices gathered to rank 0",
+                   "mesh": args.mesh, "H": H, "W": W, "global_views": n_total, "parallelism": f"view-sharded x{world}"},
+        "gather_us": round(gather_us, 2), "gather_bytes": 4 * H * W * n_total,
+        "gather_equals_single_gpu_render": equal,
+        "roofline": {"bound": "hbm", "kernel": "forward kernels (sum)", "bytes_per_frame": per_frame,
+                     "us_per_step": round(us, 2),
+                     "achieved": round(per_frame * nv / max(us, 1e-9) * 1e-3, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(per_frame * nv / max(us, 1e-9) * 1e-3 / HBM_PEAK_GBS, 4)},
         "kernels": kernels,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pose_refs(meshes, renderers, R, T):
+    """camera_pose_optimizer.py:173-191: the reference silhouette mask, depth (-1 -> 0) and colour."""
+    rast, sil_r, phong = renderers
+    with torch.no_grad():
+        depth = rast(meshes_world=meshes, R=R, T=T).zbuf[..., 0]
+        rgb = phong(meshes_world=meshes, R=R, T=T)[..., :3]
+    depth = torch.where(depth == -1.0, torch.zeros_like(depth), depth)
+    mask = depth != 0.0
+    rgb = torch.where(mask[..., None], rgb, torch.zeros_like(rgb))
+    return mask, depth, rgb
+
+
+def pose_cpu_baseline(verts, faces, d, q0, refs, H, W, n_views=2, reps=2):
+    """The same step on the oracle (C naive rasterizer + torch-CPU shading, FoV camera, near-plane
+    clipping, calc_loss with torch, backward, Adam) for `n_views` poses."""
+    import numpy as np
+
+    from oracle import oracle as O
+    from torch_renderer_amd.transforms import quaternion_to_matrix
+
+    img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0)
+    tex = ("uv", torch.from_numpy(d["verts_uvs"]).float(), torch.from_numpy(d["faces_uvs"]).long(), img)
+    t = 1.0 / math.tan(math.radians(30.0))
+    intr = torch.tensor([[t, 0.0, t, 0.0]]).expand(n_views, 4).contiguous()
+    mask, dref, rref = (x[:n_views].cpu() for x in refs)
+    q = torch.nn.Parameter(q0[:n_views].cpu().clone())
+    opt = torch.optim.Adam([q], lr=1e-3)
+    F_ = torch.nn.functional
+
+    def one():
+        opt.zero_grad()
+        ref = O.render_ref(verts, faces, quaternion_to_matrix(q[:, 3:]), q[:, :3], intr, H, W, texture=tex,
+                           bg=(0.0, 0.0, 0.0), z_clip=0.5)
+        depth = torch.relu(ref["zbuf"][..., 0])
+        loss = (F_.l1_loss(ref["sil"], mask.float()) + F_.huber_loss(depth[mask], dref[mask], delta=0.05)
+                + 0.01 * F_.mse_loss(ref["rgba"][..., :3], rref))
+        loss.backward()
+        opt.step()
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores, cores)
+    O.set_threads(threads)
+    one()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    sec = (time.perf_counter() - t0) / reps
+    return {"value": n_views / sec, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n_views} poses of the same step (cow {H}x{W}, FoV camera, clipping, calc_loss, backward, "
+                      f"Adam), 1 warm-up + {reps} timed steps, {sec:.2f} s/step, C naive rasterizer (OpenMP "
+                      f"{threads} threads) + torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
+
+
+def bench_pose(args, dev, world, rank):
+    """C3 as the caller runs it (camera_pose_optimizer.py:237-305), batched: --views independent pose
+    problems per GPU (the cow from look_at_view_transform(0.7, elev, azim) + N(0, 0.03) noise on the
+    7-vector pose), each step the caller's three calls — rasterizer(meshes_world=, R=, T=) for the
+    depth, the silhouette MeshRenderer, the Phong MeshRenderer — FoVPerspectiveCameras (znear 1: the
+    near plane clips at 0.5), calc_loss (fused pose_loss), backward through quaternion_to_matrix and
+    one Adam step. Eager launches, as the caller's Python loop."""
+    from torch_renderer_amd import distributed as D
+    from torch_renderer_amd.assets import load_asset, load_asset_arrays
+    from torch_renderer_amd.cameras import FoVPerspectiveCameras
+    from torch_renderer_amd.losses import pose_loss
+    from torch_renderer_amd.mesh_renderer import (BlendParams, MeshRasterizer, MeshRenderer, PointLights,
+                                                  RasterizationSettings, SoftPhongShader, SoftSilhouetteShader)
+    from torch_renderer_amd.transforms import look_at_view_transform, matrix_to_quaternion, quaternion_to_matrix
+
+    H = W = args.size
+    nv = args.views
+    n_total = nv * world
+    d = load_asset_arrays("cow")
+    base = load_asset("cow", device=dev)
+    meshes = base.extend(nv)
+    cams = FoVPerspectiveCameras(device=dev)
+    blend = BlendParams(sigma=1e-4, gamma=1e-4, background_color=(0, 0, 0))
+    rs = RasterizationSettings(image_size=H, blur_radius=0.0, faces_per_pixel=1)
+    sil_r = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs), SoftSilhouetteShader(blend_params=blend))
+    rast = MeshRasterizer(cameras=cams, raster_settings=rs)
+    lights = PointLights(device=dev, location=[[0.0, 0.0, -3.0]])
+    phong = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs),
+                         SoftPhongShader(device=dev, cameras=cams, lights=lights, blend_params=blend))
+    elev = torch.linspace(10.0, 50.0, n_total)[rank * nv:(rank + 1) * nv]
+    azim = torch.linspace(0.0, 360.0, n_total + 1)[:-1][rank * nv:(rank + 1) * nv]
+    R, T = look_at_view_transform(0.7, elev, azim, device=dev)
+    refs = _pose_refs(meshes, (rast, sil_r, phong), R, T)
+    mask, depth_ref, rgb_ref = refs
+    g = torch.Generator().manual_seed(rank)
+    q_ref = torch.cat((T, matrix_to_quaternion(R)), -1)
+    q0 = q_ref + (torch.randn(q_ref.shape, generator=g) * 0.03).to(dev)
+    q = torch.nn.Parameter(q0.clone())
+    opt = torch.optim.Adam([q], lr=1e-3)
+
+    def step():
+        opt.zero_grad()
+        Rq = quaternion_to_matrix(q[:, 3:])
+        Tq = q[:, :3]
+        frags = rast(meshes_world=meshes, R=Rq, T=Tq)
+        depth = torch.relu(frags.zbuf[..., 0])
+        sil = sil_r(meshes, R=Rq, T=Tq)[..., 3]
+        color = phong(meshes, R=Rq, T=Tq)[..., :3]
+        loss = pose_loss(depth, sil, color, mask, depth_ref, rgb_ref)
+        loss.backward()
+        opt.step()
+
+    elapsed = _time_steps(step, args, dev, world)
+    kt = _kernel_times(step, min(args.steps, 10))
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        verts0 = base.shared_verts().detach().cpu()
+        cpu = pose_cpu_baseline(verts0, base.shared_faces().cpu(), d, q0.detach(), refs, H, W,
+                                n_views=min(args.cpu_views, nv))
+    value = n_total * args.steps / elapsed
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    line = {
+        "metric": f"frames/sec C3 pose-optimiser step (3 renders + calc_loss + backward + Adam), cow {H}x{W}",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "launch": "eager", "data": "synthetic poses around the reference mesh",
+        "config": {"workload": f"cow (F={base.shared_faces().shape[0]}), {H}x{W}, {nv} pose problems/GPU, "
+                               "camera_pose_optimizer.py step: rasterizer + silhouette + Phong renders (FoV camera, "
+                               "near-plane clip), calc_loss, backward, Adam",
+                   "mesh": "cow", "H": H, "W": W, "views_per_gpu": nv, "parallelism": f"view-sharded x{world}"},
+        "cpu_baseline": cpu, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def soft_cpu_baseline(verts, faces, R, T, H, W, K, blur, sigma, target, n_views=2, reps=2):
+    """The soft silhouette step on the oracle (C naive K-deep rasterizer, sigmoid_alpha_blend, L2 loss,
+    backward) for `n_views` views."""
+    from oracle import oracle as O
+
+    intr = torch.tensor([[1.0, 0.0, 1.0, 0.0]]).expand(n_views, 4).contiguous()
+    Rc, Tc, tg = R[:n_views].cpu(), T[:n_views].cpu(), target[:n_views].cpu()
+
+    def one():
+        v = verts.detach().cpu().clone().requires_grad_(True)
+        ref = O.render_ref(v, faces.cpu(), Rc, Tc, intr, H, W, persp=False, K=K, blur=blur, clip=True,
+                           sigma_sil=sigma, light={"kind": "ambient", "ambient": (1.0, 1.0, 1.0)})
+        ((ref["sil"] - tg) ** 2).mean().backward()
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores, cores)
+    O.set_threads(threads)
+    one()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    sec = (time.perf_counter() - t0) / reps
+    return {"value": n_views / sec, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n_views} views of the same workload ({H}x{W}, K={K}, fwd+bwd), 1 warm-up + {reps} timed "
+                      f"passes, {sec:.2f} s/pass: C naive K-deep rasterizer (OpenMP {threads} threads) + torch-CPU "
+                      f"blend/autograd"}
 
 
 def _spawn_ranks(n):

@@ -73,16 +73,20 @@ def allreduce_grads(params, group=None):
 
 def gather_to_root(local: torch.Tensor, n_total: int, root: int = 0, group=None):
     """Assemble the per-rank view slices into the full (n_total, ...) tensor on `root`
-    (returns None elsewhere) with one batched set of point-to-point transfers."""
+    (returns None elsewhere) with one batched set of point-to-point transfers. Over gloo (the CPU
+    tests, and the 1-GPU rehearsal of the N-rank path) device tensors travel through host copies."""
     rank, w = world()
     if w == 1:
         return local
+    host = local.is_cuda and dist.get_backend(group) == "gloo"
     if rank != root:
         s, e = shard_range(n_total, rank, w)
         if e > s:
-            dist.batch_isend_irecv([dist.P2POp(dist.isend, local.contiguous(), root, group)])[0].wait()
+            src = local.contiguous().cpu() if host else local.contiguous()
+            dist.batch_isend_irecv([dist.P2POp(dist.isend, src, root, group)])[0].wait()
         return None
-    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=local.device)
+    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype,
+                      device="cpu" if host else local.device)
     ops = []
     for r in range(w):
         s, e = shard_range(n_total, r, w)
@@ -92,4 +96,4 @@ def gather_to_root(local: torch.Tensor, n_total: int, root: int = 0, group=None)
             ops.append(dist.P2POp(dist.irecv, out[s:e], r, group))
     for req in dist.batch_isend_irecv(ops) if ops else []:
         req.wait()
-    return out
+    return out.to(local.device) if host else out

@@ -1252,17 +1252,90 @@ __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) { bin_view_b
 // (blur == 0, FR_FAST) the edge signs reject before any division: a pixel whose edge
 // functions do not all carry the area's strict sign has some w_i <= 0, hence c_i <= 0
 // (all z > 0), hence is not inside, hence eval_face rejects it too.
-// The cheap prefix of frag_keep (bbox, and on the fast path the edge signs): false only where
-// frag_keep is false too, so the pairs it passes are a superset of the kept fragments.
-MR_DEV bool frag_cand(const FaceRec& r, float x, float y, float pad, bool fast) {
-  if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) return false;
-  if (!fast) return true;
-  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
-  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
-  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
-  const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
-  const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
-  return r.area > 0.0f ? inp : inn;
+// Candidate pixels of one face in one 8x8 tile, as a 64-bit coverage mask (bit 8 * row + col,
+// tile-local): the rectangle [rx0, rx1] x [ry0, ry1] (the face's padded bbox clipped to the
+// tile), narrowed on the fast path to the columns of each row whose centre can pass the
+// edge-sign test. Every pixel frag_keep keeps is in the mask; a few columns within 0.02 px of an
+// edge are extra (frag_keep rejects them exactly).
+// Edge E_i(p) = (px - ax)(by - ay) - (py - ay)(bx - ax), kept iff s E_i > 0 (s = sign of the
+// area). On row py this is linear in px: A (px - ax) > g with A = s dy, g = s dx (py - ay), i.e.
+// px > T (A > 0) or px < T (A < 0), T = ax + g / A. Columns run right to left in NDC (tile column
+// c of NDC x: c = C0 - x C1), so px > T is c < c(T) and px < T is c > c(T). g is lowered by a
+// slack of 2 tol, tol bounding the float rounding of the edge function evaluated in frag_keep
+// and of this threshold; a horizontal edge (A = 0) is the limit A -> +0 (all or no columns).
+struct TileCols {
+  float C0, C1;  // tile column of an NDC x: c = C0 - x * C1
+  float omax;    // bound on |NDC| of any pixel centre
+};
+MR_DEV TileCols tile_cols(int x0, int H, int W) {
+  TileCols t;
+  t.C1 = W > H ? 0.5f * (float)H : 0.5f * (float)W;
+  t.C0 = 0.5f * (float)W - 0.5f - (float)x0;
+  t.omax = (float)max(W, H) / (float)min(W, H);
+  return t;
+}
+MR_DEV unsigned long long rect_mask(int rx0, int rx1, int ry0, int ry1) {
+  const unsigned long long row = (2ull << rx1) - (1ull << rx0);
+  const unsigned long long rows = (0x0101010101010101ull >> (8 * (7 - ry1))) & (~0ull << (8 * ry0));
+  return row * rows;
+}
+MR_DEV unsigned long long tri_mask(const FaceRec& r, const float* ys, int rx0, int rx1, int ry0, int ry1,
+                                   const TileCols& tc) {
+  const float s = r.area > 0.0f ? 1.0f : -1.0f;
+  float Gx[3], K[3], rA[3], ax[3], sC1[3], sC0[3];
+  bool up[3];  // A > 0 (or = 0): the edge bounds the columns from above
+  const float vx[3] = {r.x0, r.x1, r.x2}, vy[3] = {r.y0, r.y1, r.y2};
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int a = (i + 1) % 3, b = (i + 2) % 3;  // E_0 = E(p, v1, v2), E_1 = E(p, v2, v0), E_2 = E(p, v0, v1)
+    const float dx = vx[b] - vx[a], dy = vy[b] - vy[a];
+    const float A = s * dy;
+    const float tol = 1e-6f * (fabsf(dx) + fabsf(dy)) * (tc.omax + fabsf(vx[a]) + fabsf(vy[a]));
+    Gx[i] = s * dx;
+    K[i] = Gx[i] * vy[a] + 2.0f * tol;  // g - 2 tol = Gx py - K
+    up[i] = A >= 0.0f;
+    rA[i] = A != 0.0f ? __builtin_amdgcn_rcpf(A) : 1e30f;
+    ax[i] = vx[a];
+    // sigma c(T) + eps, sigma = +1 (up) / -1: floor of it bounds hi (up) or -lo
+    sC1[i] = up[i] ? -tc.C1 : tc.C1;
+    sC0[i] = (up[i] ? tc.C0 : -tc.C0) + 0.02f;
+  }
+  unsigned long long m = 0;
+#pragma unroll
+  for (int ry = 0; ry < MR_TS; ++ry) {
+    if (ry < ry0 || ry > ry1) continue;
+    const float py = ys[ry];
+    int hi = rx1, lo = rx0;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float T = fmaf(fmaf(Gx[i], py, -K[i]), rA[i], ax[i]);
+      const float v = __builtin_amdgcn_fmed3f(fmaf(T, sC1[i], sC0[i]), -10.0f, 10.0f);  // NaN -> -10: no column
+      const int h = (int)floorf(v);
+      if (up[i]) hi = min(hi, h);
+      else lo = max(lo, -h);
+    }
+    if (lo <= hi) m |= ((2ull << hi) - (1ull << lo)) << (8 * ry);
+  }
+  return m;
+}
+
+// The k-th (from 0) set bit of m (k < popcount(m)).
+MR_DEV int kth_bit(unsigned long long m, int k) {
+  const unsigned lo = (unsigned)m;
+  const int clo = __popc(lo);
+  const bool hi = k >= clo;
+  unsigned x = hi ? (unsigned)(m >> 32) : lo;
+  int pos = hi ? 32 : 0;
+  k = hi ? k - clo : k;
+#pragma unroll
+  for (int sh = 16; sh >= 1; sh >>= 1) {
+    const int c = __popc(x & ((1u << sh) - 1u));
+    const bool go = k >= c;
+    x = go ? x >> sh : x;
+    k = go ? k - c : k;
+    pos = go ? pos + sh : pos;
+  }
+  return pos;
 }
 
 MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur, bool persp, bool clipb,
@@ -1412,11 +1485,11 @@ struct FwdParams {
 struct WaveStage {
   float rec[16][64];
   int id[64];
-  int meta[64];  // first pair index | (rect width - 1) << 13 | tile col << 16 | tile row << 19
-  int mark[64];  // pass-local: pair slot -> entry lane that starts there
+  int meta[64];  // index of the entry's first candidate pixel
+  int mark[64];  // pass-local: candidate slot -> entry lane that starts there
   unsigned long long key[64];
+  unsigned long long cmask[64];  // the entry's candidate pixels (bit 8 * row + col)
   float xs[MR_TS], ys[MR_TS];
-  int queue[128];  // ring of candidate pairs: face lane << 6 | tile row << 3 | tile column
 };
 
 // Background values of every output (view-independent: a pixel without a face has zero
@@ -1637,6 +1710,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
     const int n = U.x / P.T, t = U.x - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
     const int x0 = tx * MR_TS, y0 = ty * MR_TS;
+    const TileCols tc = tile_cols(x0, H, W);
     if (lane < MR_TS) S.xs[lane] = col_ndc(x0 + lane < W ? x0 + lane : W - 1, H, W);
     else if (lane < 2 * MR_TS) S.ys[lane - MR_TS] = row_ndc(y0 + lane - MR_TS < H ? y0 + lane - MR_TS : H - 1, H, W);
     S.key[lane] = MR_KEY_EMPTY;
@@ -1646,7 +1720,8 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
 #pragma unroll 1
     for (int eb = 0; eb < U.z; eb += 64) {
       const int e = eb + lane;
-      int np = 0, meta = 0, prect = 0;
+      int prect = 0;
+      unsigned long long cmask = 0;
       if (e < U.z) {
         int id;
         FaceRec r;
@@ -1683,9 +1758,12 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
           if (CLIP && (r.flags & FR_PAIR)) {  // a split face's triangle: its own per-lane loop after the passes
             prect = 0x1000 | (cx0 - x0) | ((cx1 - x0) << 3) | ((cy0 - y0) << 6) | ((cy1 - y0) << 9);
           } else {
-            const int w = cx1 - cx0 + 1;
-            np = w * (cy1 - cy0 + 1);
-            meta = ((w - 1) << 13) | ((cx0 - x0) << 16) | ((cy0 - y0) << 19);
+            const int rx0 = cx0 - x0, rx1 = cx1 - x0, ry0 = cy0 - y0, ry1 = cy1 - y0;
+            // coverage rows from the edges (fast path; coordinates small enough that the
+            // threshold arithmetic stays finite), else the whole rectangle
+            const bool tm = fast_ok && (r.flags & FR_FAST) &&
+                            fmaxf(fmaxf(fabsf(r.xmin), fabsf(r.xmax)), fmaxf(fabsf(r.ymin), fabsf(r.ymax))) < 1e12f;
+            cmask = tm ? tri_mask(r, S.ys, rx0, rx1, ry0, ry1, tc) : rect_mask(rx0, rx1, ry0, ry1);
           }
         }
         stage_rec_put(S.rec, lane, r);
@@ -1699,32 +1777,17 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
         U2v = U3v;
         U3v = P.units[min(u + 3 * Gp, ulast) + lz];
       }
-      // pair numbering
+      // candidate numbering: a DPP prefix sum over the masks' popcounts
       ACC(acc_load);
+      const int np = __popcll(cmask);
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
-      S.meta[lane] = meta | pexcl;
-      // Two phases: every pass runs the cheap test (bbox + edge signs) on 64 (face, pixel) pairs
-      // and appends the candidates to the wave's LDS ring; whenever 64 candidates are queued a
-      // full wave evaluates them exactly (divisions, perspective correction, depth) and merges
-      // the keys. Evaluated in place, a pass would run the exact path whenever any one lane of
-      // it needed it, i.e. almost always, for ~20-30% useful lanes.
-      int qhead = 0, qtail = 0;  // ring positions (wave-uniform)
-      auto eval_queued = [&](int cnt) {
-        ACC(acc_pass);
-        wave_lds_sync();
-        if (lane < cnt) {
-          const int pk = S.queue[(qhead + lane) & 127];
-          const int m = pk >> 6, sy = (pk >> 3) & 7, sx = pk & 7;
-          const FaceRec r = stage_rec_get(S.rec, m);
-          float pz;
-          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
-            atomicMin(&S.key[sy * MR_TS + sx], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
-        }
-        qhead += cnt;
-        ACC(acc_eval);
-      };
+      S.meta[lane] = pexcl;
+      S.cmask[lane] = cmask;
+      ACC(acc_pass);
+      // 64 candidates per pass, one per lane, each evaluated exactly (frag_keep: bbox, edge
+      // signs, divisions, perspective correction, depth) and merged into the tile's keys
 #pragma unroll 1
       for (int pb = 0; pb < NP; pb += 64) {
 #ifdef MR_PROF
@@ -1742,30 +1805,16 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
         if (lane == 0) m = straddle;
         m = wave_incl_max(m);
         const int q = pb + lane;
-        bool cand = false;
-        int pk = 0;
         if (q < NP) {
-          // one (face, pixel) pair per lane
-          const int mt = S.meta[m];
-          const int loc = q - (mt & 0x1fff);
-          const int w = ((mt >> 13) & 7) + 1;
-#ifdef MR_DBG_IDIV
-          const int ly = loc / w;
-#else
-          const int ly = (int)((float)loc * __builtin_amdgcn_rcpf((float)w) + 1e-3f);
-#endif
-          const int lx = loc - ly * w;
-          const int sx = ((mt >> 16) & 7) + lx, sy = ((mt >> 19) & 7) + ly;
+          const int p = kth_bit(S.cmask[m], q - S.meta[m]);
+          const int sx = p & 7, sy = p >> 3;
           const FaceRec r = stage_rec_get(S.rec, m);
-          cand = frag_cand(r, S.xs[sx], S.ys[sy], pad, fast_ok && (r.flags & FR_FAST));
-          pk = (m << 6) | (sy << 3) | sx;
+          float pz;
+          if (frag_keep(r, S.xs[sx], S.ys[sy], pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz))
+            atomicMin(&S.key[p], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
         }
-        const unsigned long long cb = __ballot(cand);
-        if (cand) S.queue[(qtail + __popcll(cb & ((1ull << lane) - 1ull))) & 127] = pk;
-        qtail += __popcll(cb);
-        if (qtail - qhead >= 64) eval_queued(64);
       }
-      if (qtail > qhead) eval_queued(qtail - qhead);
+      ACC(acc_eval);
       if (CLIP && __builtin_expect(__ballot(prect != 0) != 0ull, 0)) {
         // near-plane split faces (rare): each such lane walks its rectangle, resolving the pair
         if (prect) raster_pair_rect(P.recs, P.NF, S.rec, S.id, S.xs, S.ys, S.key, lane, prect, pad, blur, persp, clipb);

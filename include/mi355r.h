@@ -82,9 +82,16 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
         * forward left them (cleared), i.e. this is the first backward over that forward; the
         * backward then skips clearing them. Leave it unset for any later backward over the same
         * forward workspace (e.g. autograd retain_graph). */
-       MR_GRAD_ROWS_CLEARED = 16 };
+       MR_GRAD_ROWS_CLEARED = 16,
+       /* with MR_OUT_SIL, mr_render_forward/_backward[_opencv]: the silhouette buffer is (N,H,W,4)
+        * RGBA as SoftSilhouetteShader returns it, (1, 1, 1, alpha) per pixel, written by the
+        * kernels; its gradient is the (N,H,W,4) gradient of that tensor (channel 3 is read) */
+       MR_OUT_SIL_RGBA = 32 };
 
-/* One triangle mesh shared by all N views (Meshes.extend(N)). */
+/* One triangle mesh shared by all N views (Meshes.extend(N)) — or, with
+ * view_face_first set, a batch of N distinct meshes (renderer.py:78-80: N OBJ files in one Meshes),
+ * view n rendering mesh n: the arrays then hold the meshes' union (each mesh's faces index its own
+ * vertices inside the union; no vertex is shared between meshes). */
 typedef struct mr_mesh {
   const float* verts;        /* (V,3) world */
   int64_t V;
@@ -109,6 +116,14 @@ typedef struct mr_mesh {
    * convert through the 256-entry table, bitwise the same values at a quarter of the bytes. */
   const uint8_t* tex_u8;
   const float* tex_lut;      /* (256) f32, required with tex_u8 */
+  /* Distinct meshes (mr_render_*, mr_shade_fragments_*; NULL: one shared mesh). Device arrays:
+   * view_face_first (N+1) the first union face of view n's mesh (view_face_first[N] = F) and
+   * view_face_count (N) its face count; max_view_faces (host) = the largest count. Face ids stay
+   * union face ids (= PyTorch3D's packed ids of the batch). Size the forward workspace with
+   * mr_render_workspace_meshes. */
+  const int64_t* view_face_first;
+  const int64_t* view_face_count;
+  int64_t max_view_faces;
 } mr_mesh_t;
 
 const char* mr_last_error(void);
@@ -158,7 +173,9 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
  * fused render); k_tile_raster writes the rest. */
 int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W, int32_t mode);
 
-/* grad_face_verts (F,3,3) is overwritten (zeroed then accumulated). */
+/* grad_face_verts (F,3,3) is overwritten (zeroed then accumulated). Any of grad_zbuf, grad_bary,
+ * grad_dists may be NULL (PyTorch passes None for an output the loss did not use): it counts as
+ * zero, and no zero-filled tensor needs to be allocated for it. */
 int32_t mr_rasterize_meshes_backward(const float* face_verts, const int64_t* pix_to_face,
                                      const float* grad_zbuf, const float* grad_bary, const float* grad_dists,
                                      int64_t num_meshes, int64_t total_faces, const mr_raster_settings_t* settings,
@@ -172,6 +189,19 @@ int32_t mr_project_faces(const float* verts, int64_t V, const int32_t* faces, in
 int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
                                   const int32_t* vadj_ptr, const int32_t* vadj, const mr_view_t* views, int64_t N,
                                   const float* grad_face_verts, float* grad_verts, float* grad_views, void* stream);
+/* The same for a batch of N distinct meshes (MeshRasterizer.transform of a Meshes of different
+ * meshes, renderer.py:78-80): verts / faces are their union (see mr_mesh_t), view n projects only
+ * mesh n's faces [view_face_first[n], view_face_first[n+1]) into face_verts rows of the same ids
+ * (the packed order). The backward walks view n's own vertices [view_vert_first[n],
+ * view_vert_first[n+1]); max_view_faces / max_view_verts are the largest per-mesh counts. */
+int32_t mr_project_faces_meshes(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                const int64_t* view_face_first, int64_t max_view_faces, const mr_view_t* views,
+                                int64_t N, float* face_verts, void* stream);
+int32_t mr_project_faces_meshes_backward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                         const int32_t* vadj_ptr, const int32_t* vadj, const int64_t* view_vert_first,
+                                         int64_t max_view_verts, const mr_view_t* views, int64_t N,
+                                         const float* grad_face_verts, float* grad_verts, float* grad_views,
+                                         void* stream);
 
 /* ---------------- camera poses (DifferentiableRenderer._camera_pose_from_opencv_to_pytorch) ---------------- */
 /* torch_renderer.py:73-80: R_p3d = R_cv^T with columns 0,1 negated; T = t_cv with entries 0,1 negated.
@@ -191,8 +221,10 @@ int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, i
 
 /* ---------------- fused render (one raster pass -> depth, silhouette, rgb) ---------------- */
 size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
+/* The same for N distinct meshes of F faces in total (mr_mesh_t.view_face_first set). */
+size_t mr_render_workspace_meshes(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
 /* Outputs (each optional per out_flags): depth (N,H,W), silhouette (N,H,W), rgb (N,H,W,C);
- * pix_to_face32 (N,H,W) int32 packed face id n*F+f or -1 — optional (NULL: not written; the
+ * pix_to_face32 (N,H,W) int32 packed face id n*F+f (distinct meshes: the union face id) or -1 — optional (NULL: not written; the
  * backward does not need it: the workspace keeps a compact list of covered pixels).
  * cam_centers (Nc,3) world-space specular camera centres, Nc in {1, N}. */
 int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t N, const float* cam_centers,

@@ -139,10 +139,12 @@ def test_mesh_rasterizer_fragments_bitexact(distinct):
         _close(a.grad, b.grad)
 
 
-@pytest.mark.parametrize("shader", ["phong", "silhouette"])
-def test_mesh_renderer_matches_oracle(shader):
-    """Cameras built with R, T (renderer.py:65-69): specular uses the real camera centre."""
-    H, W, N = 64, 64, 2
+@pytest.mark.parametrize("shader,W", [("phong", 64), ("silhouette", 64), ("silhouette", 66)])
+def test_mesh_renderer_matches_oracle(shader, W):
+    """Cameras built with R, T (renderer.py:65-69): specular uses the real camera centre. The
+    silhouette's RGBA (1, 1, 1, alpha) comes straight from the kernels (W = 66: the per-pixel
+    background stores instead of the 4-pixel vector ones)."""
+    H, N = 64, 2
     verts, faces, d = mesh_arrays("teapot")
     R, T, intr, (R_cv, t_cv, K) = canonical_views(verts, N, H, W)
     g = torch.Generator().manual_seed(11)
@@ -375,3 +377,58 @@ def test_second_backward_over_one_forward_accumulates_exactly():
     torch.autograd.backward([d, s, c], [gd, gs, gc])
     for a, b, nm in zip((vg.grad, Rg.grad, tg.grad), first, ("verts", "R", "t")):
         report(f"second backward {nm}", a.cpu(), b.cpu())
+
+
+@pytest.mark.parametrize("texture", ["vertex", "uv_shared_map"])
+def test_distinct_meshes_one_launch_equals_per_mesh_renders(texture):
+    """renderer.py:78-80,100-101: a Meshes of N different meshes rendered in one call. The fused
+    path renders their union in ONE launch (view n rasterizes only mesh n's faces); images must
+    equal rendering each mesh alone bitwise, gradients within float-summation-order noise."""
+    from torch_renderer_amd import kernels as Kn
+    from torch_renderer_amd.torch_renderer import render_mesh_batch
+
+    H, W = 56, 64
+    g = torch.Generator().manual_seed(8)
+    cv, cf, d = mesh_arrays("cow")
+    if texture == "vertex":
+        names = ("cow", "teapot", "sphere")
+        mv = []
+        for name in names:
+            v, f, _ = mesh_arrays(name)
+            v = (v - v.mean(0)) / (v - v.mean(0)).abs().max() * 0.4 + cv.mean(0)  # every mesh cow-sized
+            mv.append((v, f))
+        tex_of = lambda vs: TexturesVertex([torch.rand(v.shape, generator=g).to(DEV) for v in vs])  # noqa: E731
+    else:  # two cows (one deformed) sharing ONE texture map: the union keeps one map
+        img = torch.from_numpy(d["texture_u8"].astype(np.float32) / 255.0).to(DEV)
+        vuv = torch.from_numpy(d["verts_uvs"]).float().to(DEV)
+        fuv = torch.from_numpy(d["faces_uvs"]).long().to(DEV)
+        mv = [(cv, cf), (cv + 0.01 * torch.randn(cv.shape, generator=g), cf)]
+        tex_of = lambda vs: TexturesUV(maps=[img] * len(vs), faces_uvs=[fuv] * len(vs), verts_uvs=[vuv] * len(vs))  # noqa: E731
+    N = len(mv)
+    R, T, intr, (R_cv, t_cv, K) = canonical_views(cv, N, H, W)
+    cams = PerspectiveCameras(focal_length=((K[0, 0].item(), K[1, 1].item()),),
+                              principal_point=((K[0, 2].item(), K[1, 2].item()),), in_ndc=False,
+                              image_size=torch.tensor([[H, W]]), device=DEV)
+    cfg = Kn.ShadeConfig(H=H, W=W, want_p2f=True, light_location=(0.0, 1.0, -2.0))
+    vb = [m[0].to(DEV).requires_grad_(True) for m in mv]
+    tex = tex_of(vb)
+    Rg, Tg = R.to(DEV).requires_grad_(True), T.to(DEV).requires_grad_(True)
+    out = render_mesh_batch(Meshes(vb, [m[1].to(DEV) for m in mv], tex), cams, (H, W), Rg, Tg, cfg)
+    gD, gS, gC = (torch.rand(out[k].shape, generator=g).to(DEV) - 0.5 for k in ("depth", "sil", "rgb"))
+    ((out["depth"] * gD).sum() + (out["sil"] * gS).sum() + (out["rgb"] * gC).sum()).backward()
+    Fsum = 0
+    for i, (v, f) in enumerate(mv):
+        vs = v.to(DEV).requires_grad_(True)
+        Ri, Ti = R[i:i + 1].to(DEV).requires_grad_(True), T[i:i + 1].to(DEV).requires_grad_(True)
+        one = render_mesh_batch(Meshes([vs], [f.to(DEV)], tex[i]), cams, (H, W), Ri, Ti, cfg)
+        ((one["depth"] * gD[i:i + 1]).sum() + (one["sil"] * gS[i:i + 1]).sum() +
+         (one["rgb"] * gC[i:i + 1]).sum()).backward()
+        for k in ("depth", "sil", "rgb"):
+            assert torch.equal(out[k][i:i + 1], one[k]), (i, k)
+        p1 = one["pix_to_face32"]
+        assert torch.equal(out["pix_to_face32"][i:i + 1], torch.where(p1 >= 0, p1 + Fsum, p1)), i
+        assert (p1 >= 0).sum() > 0.02 * H * W
+        Fsum += f.shape[0]
+        _close(vb[i].grad, vs.grad, tol=1e-5)
+        _close(Rg.grad[i:i + 1], Ri.grad, tol=1e-5)
+        _close(Tg.grad[i:i + 1], Ti.grad, tol=1e-5)

@@ -77,11 +77,11 @@ def test_transform_uses_the_per_call_image_size(monkeypatch):
 
     seen = {}
 
-    def fake_apply(v, R, T, f, intr):
+    def fake_apply(v, R, T, f, intr, *ranges):
         seen["intr"] = intr.clone()
-        return torch.zeros(f.shape[0] * R.shape[0], 3, 3)
+        return torch.zeros(f.shape[0], 3, 3)
 
-    monkeypatch.setattr(M.ProjectFaces, "apply", fake_apply)
+    monkeypatch.setattr(M.ProjectFacesMeshes, "apply", fake_apply)  # two distinct meshes: one union launch
     cams = PerspectiveCameras(focal_length=((100.0, 100.0),), principal_point=((40.0, 30.0),), in_ndc=False,
                               image_size=torch.tensor([[60, 80]]))
     v = torch.rand(4, 3)

@@ -24,6 +24,7 @@ MR_OUT_DEPTH = 1
 MR_OUT_SIL = 2
 MR_OUT_RGB = 4
 MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
+MR_OUT_SIL_RGBA = 32  # silhouette as (N,H,W,4) RGBA (1, 1, 1, alpha), fused render path
 MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
 
 
@@ -67,7 +68,9 @@ class MrMesh(ctypes.Structure):
                 ("vnormals", ctypes.c_void_p), ("tex_kind", ctypes.c_int32), ("vcolors", ctypes.c_void_p),
                 ("verts_uvs", ctypes.c_void_p), ("faces_uvs", ctypes.c_void_p), ("tex_rgba", ctypes.c_void_p),
                 ("tex_h", ctypes.c_int32), ("tex_w", ctypes.c_int32), ("vnormals_out", ctypes.c_void_p),
-                ("vraw_out", ctypes.c_void_p), ("tex_u8", ctypes.c_void_p), ("tex_lut", ctypes.c_void_p)]
+                ("vraw_out", ctypes.c_void_p), ("tex_u8", ctypes.c_void_p), ("tex_lut", ctypes.c_void_p),
+                ("view_face_first", ctypes.c_void_p), ("view_face_count", ctypes.c_void_p),
+                ("max_view_faces", ctypes.c_int64)]
 
 
 # (name, restype, argtypes) — mirrors include/mi355r.h
@@ -90,11 +93,15 @@ _SIGS = [
                                          _VP]),
     ("mr_binning_background_pixels", _I64, [_I64, _I64, _I32, _I32, _I32]),
     ("mr_project_faces", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
+    ("mr_project_faces_meshes", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
+    ("mr_project_faces_meshes_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP,
+                                                _VP]),
     ("mr_views_from_opencv", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _I64, _VP, _VP]),
     ("mr_view_grads_to_opencv", _I32, [_VP, _I64, _VP, _VP, _VP]),
     ("mr_project_faces_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _VP, _VP]),
     ("mr_vertex_normals", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _VP, _VP]),
     ("mr_render_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32]),
+    ("mr_render_workspace_meshes", _SZ, [_I64, _I64, _I32, _I32, _I32]),
     ("mr_render_forward", _I32, [ctypes.POINTER(MrMesh), _VP, _I64, _VP, _I64, ctypes.POINTER(MrRasterSettings),
                                  ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("mr_render_forward_opencv", _I32, [ctypes.POINTER(MrMesh), ctypes.POINTER(MrOpencvPoses), _VP, _I64, _VP, _I64,

@@ -249,6 +249,7 @@ struct SetupParams {
   const int* vbase;
   uint32_t* rects;  // k_bin_view path: per-record tile rectangles
   float* fv_out;    // k_bin_rect_world: face_verts (N*F,3,3) written beside the records (NULL: none)
+  const int64_t* vff;  // world mode, distinct meshes: first union face of each view (N+1); NULL: shared mesh
 };
 
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
@@ -453,14 +454,19 @@ __global__ void __launch_bounds__(256) k_bin_count_world(SetupParams P, const fl
   }
   int mine = 0;
   const ViewRec V = views[n];
+  int64_t Fv = F, rbase = (int64_t)n * F, fbase = 0;  // as k_bin_rect_world
+  if (P.vff) {
+    rbase = fbase = P.vff[n];
+    Fv = P.vff[n + 1] - rbase;
+  }
   for (int k = 0; k < fpt; ++k) {
     const int64_t f = ((int64_t)blockIdx.x * fpt + k) * blockDim.x + threadIdx.x;
-    if (f >= F) break;
+    if (f >= Fv) break;
     float v[3][3];
-    world_face_verts(verts, faces, f, V, v);
+    world_face_verts(verts, faces, fbase + f, V, v);
     FaceRec r2;
-    const FaceRec r = build_records(P, (int64_t)n * F + f, (uint32_t)f, v, r2);
-    P.recs[(int64_t)n * F + f] = r;
+    const FaceRec r = build_records(P, rbase + f, (uint32_t)(fbase + f), v, r2);
+    P.recs[rbase + f] = r;
     for (int q = 0; q < 2; ++q) {
       const FaceRec& rq = q == 0 ? r : r2;
       int tx0, tx1, ty0, ty1;
@@ -498,9 +504,14 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
     return;
   }
   const int64_t f0 = (int64_t)blockIdx.x * fpt * blockDim.x + threadIdx.x;
+  int64_t Fv = F, rbase = (int64_t)n * F;  // view n's records [rbase, rbase + Fv), as k_bin_count_world
+  if (P.vff) {
+    rbase = P.vff[n];
+    Fv = P.vff[n + 1] - rbase;
+  }
   // q = 0: the face instance's record; q = 1: the second triangle of a split face (FR_PAIR)
   auto rec_q = [&](int64_t f, int q, FaceRec& r) -> bool {
-    const int64_t rid = (int64_t)n * F + f;
+    const int64_t rid = rbase + f;
     r = P.recs[rid];
     if (q == 0) return true;
     if (!(r.flags & FR_PAIR)) return false;
@@ -513,7 +524,7 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
     __syncthreads();
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      for (int q = 0; q < nq && f < F; ++q) {
+      for (int q = 0; q < nq && f < Fv; ++q) {
         FaceRec r;
         int tx0, tx1, ty0, ty1;
         if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
@@ -528,8 +539,8 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
     __syncthreads();
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      for (int q = 0; q < nq && f < F; ++q) {
-        const int rid = (int)((int64_t)n * F + f + (q ? P.NF : 0));
+      for (int q = 0; q < nq && f < Fv; ++q) {
+        const int rid = (int)(rbase + f + (q ? P.NF : 0));
         FaceRec r;
         int tx0, tx1, ty0, ty1;
         if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
@@ -543,8 +554,8 @@ __global__ void __launch_bounds__(256) k_bin_fill_world(SetupParams P, int64_t F
   } else {
     for (int k = 0; k < fpt; ++k) {
       const int64_t f = f0 + (int64_t)k * blockDim.x;
-      for (int q = 0; q < nq && f < F; ++q) {
-        const int rid = (int)((int64_t)n * F + f + (q ? P.NF : 0));
+      for (int q = 0; q < nq && f < Fv; ++q) {
+        const int rid = (int)(rbase + f + (q ? P.NF : 0));
         FaceRec r;
         int tx0, tx1, ty0, ty1;
         if (rec_q(f, q, r) && rec_tiles(P, r, tx0, tx1, ty0, ty1))
@@ -875,9 +886,6 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
 #define MR_RECT_NONE 0x000000ffu        // tx0 = 255 > tx1 = 0: an empty rectangle
 #define MR_CURSOR_OFF 0x40000000        // fill cursor of a tile whose list is not filled (list_cap <= it)
 #define MR_VIEW_RPT 8                   // rectangles per thread per chunk
-#ifndef MR_RECT_FPT
-#define MR_RECT_FPT 1                   // faces per thread of k_bin_rect_world
-#endif
 MR_DEV uint32_t rec_rect(const SetupParams& P, const FaceRec& r) {
   int tx0, tx1, ty0, ty1;
   if (!rec_tiles(P, r, tx0, tx1, ty0, ty1)) return MR_RECT_NONE;
@@ -946,60 +954,24 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     return;
   }
 static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
-#if MR_RECT_FPT == 1 && !defined(MR_RECT_NOSTAGE)
   // One face per thread; the workgroup's records (and face_verts rows) are contiguous in HBM, so
   // they are staged through LDS and stored as whole lines (each store instruction writes 1 KB of
   // consecutive bytes instead of 64 lanes' 16-B pieces 64 B apart).
   __shared__ float4 s4[4 * 256];
   __shared__ float s9[9 * 256];
-  {
-    const int t = threadIdx.x;
-    const int64_t fb = (int64_t)blockIdx.x * 256;
-    const int64_t f = fb + t;
-    const int nf = (int)(F - fb < 256 ? F - fb : 256);
-    const int64_t rid0 = (int64_t)n * F + fb;
-    if (f < F) {
-      float v[3][3];
-      ViewRec V;
-      if (C.R) {
-        float* e = (float*)&V;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) e[k] = cv_view_elem(C, n, k);
-      } else {
-        V = views[n];
-      }
-      world_face_verts(verts, faces, f, V, v);
-      const int64_t rid = rid0 + t;
-#pragma unroll
-      for (int c = 0; c < 3; ++c)
-#pragma unroll
-        for (int q = 0; q < 3; ++q) s9[9 * t + 3 * c + q] = v[c][q];
-      FaceRec r2;
-      const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
-      float4 q4[4];
-      __builtin_memcpy(q4, &r, sizeof(q4));
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s4[4 * t + q] = q4[q];
-      P.rects[rid] = rec_rect(P, r);
-      if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
-    }
-    __syncthreads();
-    float4* d4 = (float4*)(P.recs + rid0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (j * 256 + t < 4 * nf) d4[j * 256 + t] = s4[j * 256 + t];
-    if (P.fv_out) {
-      float* d9 = P.fv_out + rid0 * 9;
-#pragma unroll
-      for (int j = 0; j < 9; ++j)
-        if (j * 256 + t < 9 * nf) d9[j * 256 + t] = s9[j * 256 + t];
-    }
+  // view n's faces: mesh faces [fbase, fbase + Fv) -> records [rbase, rbase + Fv)
+  int64_t Fv = F, rbase = (int64_t)n * F, fbase = 0;
+  if (P.vff) {  // distinct meshes: view n renders mesh n (records = union faces)
+    rbase = fbase = P.vff[n];
+    Fv = P.vff[n + 1] - rbase;
   }
-#else
-#pragma unroll
-  for (int k = 0; k < MR_RECT_FPT; ++k) {
-    const int64_t f = ((int64_t)blockIdx.x * MR_RECT_FPT + k) * blockDim.x + threadIdx.x;
-    if (f >= F) return;
+  const int t = threadIdx.x;
+  const int64_t fb = (int64_t)blockIdx.x * 256;
+  if (fb >= Fv) return;  // uniform over the workgroup
+  const int64_t fl = fb + t;
+  const int nf = (int)(Fv - fb < 256 ? Fv - fb : 256);
+  const int64_t rid0 = rbase + fb;
+  if (fl < Fv) {
     float v[3][3];
     ViewRec V;
     if (C.R) {
@@ -1009,22 +981,33 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
     } else {
       V = views[n];
     }
+    const int64_t f = fbase + fl;
     world_face_verts(verts, faces, f, V, v);
-    const int64_t rid = (int64_t)n * F + f;
-    if (P.fv_out) {
-      float* o = P.fv_out + rid * 9;
+    const int64_t rid = rid0 + t;
 #pragma unroll
-      for (int c = 0; c < 3; ++c)
+    for (int c = 0; c < 3; ++c)
 #pragma unroll
-        for (int q = 0; q < 3; ++q) o[3 * c + q] = v[c][q];
-    }
+      for (int q = 0; q < 3; ++q) s9[9 * t + 3 * c + q] = v[c][q];
     FaceRec r2;
     const FaceRec r = CLIP ? build_records(P, rid, (uint32_t)f, v, r2) : make_rec(P, (uint32_t)f, v);
-    P.recs[rid] = r;
+    float4 q4[4];
+    __builtin_memcpy(q4, &r, sizeof(q4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) s4[4 * t + q] = q4[q];
     P.rects[rid] = rec_rect(P, r);
     if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
   }
-#endif
+  __syncthreads();
+  float4* d4 = (float4*)(P.recs + rid0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (j * 256 + t < 4 * nf) d4[j * 256 + t] = s4[j * 256 + t];
+  if (P.fv_out) {
+    float* d9 = P.fv_out + rid0 * 9;
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+      if (j * 256 + t < 9 * nf) d9[j * 256 + t] = s9[j * 256 + t];
+  }
 }
 
 // face_verts mode (record = packed face id): the workgroup's face_verts staged through LDS
@@ -1535,7 +1518,15 @@ MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) 
       q3[0] = m1; q3[1] = m1; q3[2] = m1;
     } else {
       if (P.out_flags & MR_OUT_DEPTH) *(float4*)(P.depth + pix) = make_float4(b.d, b.d, b.d, b.d);
-      if (P.out_flags & MR_OUT_SIL) *(float4*)(P.sil + pix) = make_float4(b.s, b.s, b.s, b.s);
+      if (P.out_flags & MR_OUT_SIL) {
+        if (P.out_flags & MR_OUT_SIL_RGBA) {
+          float4* q = (float4*)(P.sil + pix * 4);
+          const float4 v = make_float4(1.0f, 1.0f, 1.0f, b.s);
+          q[0] = v; q[1] = v; q[2] = v; q[3] = v;
+        } else {
+          *(float4*)(P.sil + pix) = make_float4(b.s, b.s, b.s, b.s);
+        }
+      }
       if (P.p2f32) *(int4*)(P.p2f32 + pix) = make_int4(-1, -1, -1, -1);
       if (P.out_flags & MR_OUT_RGB) {
         float4* q = (float4*)(P.rgb + pix * CH);
@@ -1564,7 +1555,10 @@ MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) 
       for (int k = 0; k < 3; ++k) P.bary[q * 3 + k] = -1.0f;
     } else {
       if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = b.d;
-      if (P.out_flags & MR_OUT_SIL) P.sil[q] = b.s;
+      if (P.out_flags & MR_OUT_SIL) {
+        if (P.out_flags & MR_OUT_SIL_RGBA) *(float4*)(P.sil + q * 4) = make_float4(1.0f, 1.0f, 1.0f, b.s);
+        else P.sil[q] = b.s;
+      }
       if (P.p2f32) P.p2f32[q] = -1;
       if (P.out_flags & MR_OUT_RGB)
         for (int k = 0; k < CH; ++k) P.rgb[q * CH + k] = b.c[k];
@@ -1978,7 +1972,10 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
       ShadeCache C;
       shade_fwd(P.S, n, true, G, ev.b0, ev.b1, ev.b2, ev.pz, ev.sdist, o, C);
       if (P.out_flags & MR_OUT_DEPTH) P.depth[q] = o.depth;
-      if (P.out_flags & MR_OUT_SIL) P.sil[q] = o.sil;
+      if (P.out_flags & MR_OUT_SIL) {
+        if (P.out_flags & MR_OUT_SIL_RGBA) *(float4*)(P.sil + q * 4) = make_float4(1.0f, 1.0f, 1.0f, o.sil);
+        else P.sil[q] = o.sil;
+      }
       if (P.out_flags & MR_OUT_RGB) {
         P.rgb[q * CH + 0] = o.rgb[0];
         P.rgb[q * CH + 1] = o.rgb[1];
@@ -2520,7 +2517,9 @@ MR_DEV void raster_bwd_fragment(const RasterBwdParams& P, int px, int py, int64_
   r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
   r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
   r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
-  const float gb[3] = {P.gb[3 * pix], P.gb[3 * pix + 1], P.gb[3 * pix + 2]};
+  // an upstream gradient PyTorch passed as None arrives as NULL: zero
+  const float gb[3] = {P.gb ? P.gb[3 * pix] : 0.0f, P.gb ? P.gb[3 * pix + 1] : 0.0f, P.gb ? P.gb[3 * pix + 2] : 0.0f};
+  const float gzp = P.gz ? P.gz[pix] : 0.0f, gdp = P.gd ? P.gd[pix] : 0.0f;
   const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
   int ci = 0;
   const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};
@@ -2551,10 +2550,10 @@ MR_DEV void raster_bwd_fragment(const RasterBwdParams& P, int px, int py, int64_
     const float bs[3] = {es.b0, es.b1, es.b2};
     float gs[3], gsub[3][3];
     clip_gb_sub(cr, gb, gs);
-    raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, P.gz[pix], gs, P.gd[pix], gsub);
+    raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, gzp, gs, gdp, gsub);
     clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
   } else {
-    raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, P.gz[pix], gb, P.gd[pix], g);
+    raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, gzp, gb, gdp, g);
   }
 }
 
@@ -2738,6 +2737,7 @@ struct RenderBwdParams {
   const float* gS;
   const float* gRGB;
   int rgb_ch;
+  int sil_rgba;  // gS is the (N,H,W,4) gradient of an RGBA silhouette (MR_OUT_SIL_RGBA)
   ShadeParams S;
   const ShadeRec* srec;
   int64_t F;     // faces of the shared mesh: record id rid = n*F + face
@@ -2775,7 +2775,7 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
   r = load_rec(P.recs, f < 0 ? 0 : f);
   fr = P.frec[(int64_t)slot * 64 + lane];
   const float* pD = P.gD ? P.gD + pix : g_zero4;
-  const float* pS = P.gS ? P.gS + pix : g_zero4;
+  const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
   const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
   g[0] = *pD;
   g[1] = *pS;
@@ -3210,19 +3210,29 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
     for (int k = 0; k < 3; ++k) gcol[3 * v + k] = gc[k];
 }
 
-// projection: face_verts[n*F+f][c] = ndc(view n, X)
+// projection: face_verts[n*F+f][c] = ndc(view n, X); distinct meshes (ff = first union face of
+// each view, N+1): face_verts[f] for the faces f of view n's mesh
 __global__ void __launch_bounds__(256) k_project_faces(const float* __restrict__ verts, const int32_t* __restrict__ faces,
-                                                       int64_t F, const ViewRec* __restrict__ views, float* __restrict__ fv) {
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                       int64_t F, const ViewRec* __restrict__ views, float* __restrict__ fv,
+                                                       const int64_t* __restrict__ ff) {
+  int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = blockIdx.y;
-  if (f >= F) return;
+  int64_t o0;  // face_verts row
+  if (ff) {
+    f += ff[n];
+    if (f >= ff[n + 1]) return;
+    o0 = f;
+  } else {
+    if (f >= F) return;
+    o0 = (int64_t)n * F + f;
+  }
   const ViewRec V = views[n];
   for (int c = 0; c < 3; ++c) {
     const int32_t vi = faces[3 * f + c];
     const float X[3] = {verts[3 * (int64_t)vi], verts[3 * (int64_t)vi + 1], verts[3 * (int64_t)vi + 2]};
     float vx, vy, vz, nx, ny;
     project_point(V, X, vx, vy, vz, nx, ny);
-    float* o = fv + (((int64_t)n * F + f) * 3 + c) * 3;
+    float* o = fv + (o0 * 3 + c) * 3;
     o[0] = nx;
     o[1] = ny;
     o[2] = vz;
@@ -3230,21 +3240,29 @@ __global__ void __launch_bounds__(256) k_project_faces(const float* __restrict__
 }
 
 // projection backward: thread per (n, v); grads summed over incident faces (CSR order).
+// Distinct meshes (vf = first union vertex of each view's mesh, N+1): view n's own vertices, whose
+// faces' rows are face_verts[f].
 __global__ void __launch_bounds__(256) k_project_faces_bwd(const float* __restrict__ verts, int64_t V, int64_t F,
                                                            const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                                                            const ViewRec* __restrict__ views,
                                                            const float* __restrict__ gfv, float* __restrict__ gverts,
-                                                           float* __restrict__ gviews) {
+                                                           float* __restrict__ gviews, const int64_t* __restrict__ vf) {
   __shared__ float red[4][12];
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int n = blockIdx.y;
   const ViewRec Vw = views[n];
+  const int64_t rb = vf ? 0 : (int64_t)n * F;  // face_verts row of face f: rb + f
+  int64_t vend = V;
+  if (vf) {
+    v += vf[n];
+    vend = vf[n + 1];
+  }
   float gR[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, gT[3] = {0, 0, 0};
-  if (v < V) {
+  if (v < vend) {
     float gn[3] = {0.f, 0.f, 0.f};
     for (int e = ptr[v]; e < ptr[v + 1]; ++e) {
       const int f = adj[e] >> 2, c = adj[e] & 3;
-      const float* q = gfv + (((int64_t)n * F + f) * 3 + c) * 3;
+      const float* q = gfv + ((rb + f) * 3 + c) * 3;
       gn[0] += q[0];
       gn[1] += q[1];
       gn[2] += q[2];
@@ -3727,6 +3745,7 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.vbase = w.vbase;
   P.rects = w.rects;
   P.fv_out = nullptr;
+  P.vff = nullptr;
   return P;
 }
 
@@ -3956,7 +3975,7 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   NormalsArgs NA;
   memset(&NA, 0, sizeof(NA));
-  dim3 rgrid((unsigned)ceil_div(F, 256 * MR_RECT_FPT), (unsigned)N + 1);  // row 0: counter clear
+  dim3 rgrid((unsigned)ceil_div(F, 256), (unsigned)N + 1);  // row 0: counter clear
   if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
   else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
   MR_CHECK_LAUNCH("k_bin_rect_world");
@@ -3974,11 +3993,11 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
   int rc = check_settings(s);
   if (rc) return rc;
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "num_meshes out of range");
-  if (!p2f || !gz || !gb || !gd || !gfv) return set_err(MR_EINVAL, "NULL tensor argument");
+  if (!p2f || !gfv) return set_err(MR_EINVAL, "NULL tensor argument");
   hipStream_t st = (hipStream_t)stream;
   if (Ftot > 0 && hipMemsetAsync(gfv, 0, sizeof(float) * 9 * (size_t)Ftot, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
-  if (Ftot == 0) return MR_OK;
+  if (Ftot == 0 || (!gz && !gb && !gd)) return MR_OK;  // NULL gradients are zero
   RasterBwdParams P;
   P.N = (int)N; P.H = s->H; P.W = s->W; P.NBX = ceil_div(s->W, MR_BT); P.K = s->faces_per_pixel;
   P.persp = s->perspective_correct; P.clipb = s->clip_barycentric_coords;
@@ -4002,7 +4021,19 @@ int32_t mr_project_faces(const float* verts, int64_t V, const int32_t* faces, in
   if (F == 0) return MR_OK;
   if (!verts || !faces || !views || !fv) return set_err(MR_EINVAL, "NULL argument");
   dim3 grid(ceil_div(F, 256), (unsigned)N);
-  MR_TIMED(KID_PROJECT, (hipStream_t)stream, (k_project_faces<<<grid, 256, 0, (hipStream_t)stream>>>(verts, faces, F, (const ViewRec*)views, fv)));
+  MR_TIMED(KID_PROJECT, (hipStream_t)stream, (k_project_faces<<<grid, 256, 0, (hipStream_t)stream>>>(verts, faces, F, (const ViewRec*)views, fv, nullptr)));
+  MR_CHECK_LAUNCH("k_project_faces");
+  return MR_OK;
+}
+
+int32_t mr_project_faces_meshes(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                const int64_t* view_face_first, int64_t max_view_faces, const mr_view_t* views,
+                                int64_t N, float* fv, void* stream) {
+  if (N <= 0 || N > 65535 || F < 0 || V < 0 || max_view_faces < 0) return set_err(MR_EINVAL, "bad sizes");
+  if (F == 0 || max_view_faces == 0) return MR_OK;
+  if (!verts || !faces || !views || !fv || !view_face_first) return set_err(MR_EINVAL, "NULL argument");
+  dim3 grid(ceil_div(max_view_faces, 256), (unsigned)N);
+  MR_TIMED(KID_PROJECT, (hipStream_t)stream, (k_project_faces<<<grid, 256, 0, (hipStream_t)stream>>>(verts, faces, F, (const ViewRec*)views, fv, view_face_first)));
   MR_CHECK_LAUNCH("k_project_faces");
   return MR_OK;
 }
@@ -4019,7 +4050,26 @@ int32_t mr_project_faces_backward(const float* verts, int64_t V, const int32_t* 
     return set_err(MR_ELAUNCH, "memset failed");
   if (V == 0) return MR_OK;
   dim3 grid(ceil_div(V, 256), (unsigned)N);
-  MR_TIMED(KID_PROJECT_BWD, st, (k_project_faces_bwd<<<grid, 256, 0, st>>>(verts, V, F, ptr, adj, (const ViewRec*)views, gfv, gverts, gviews)));
+  MR_TIMED(KID_PROJECT_BWD, st, (k_project_faces_bwd<<<grid, 256, 0, st>>>(verts, V, F, ptr, adj, (const ViewRec*)views, gfv, gverts, gviews, nullptr)));
+  MR_CHECK_LAUNCH("k_project_faces_bwd");
+  return MR_OK;
+}
+
+int32_t mr_project_faces_meshes_backward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                         const int32_t* ptr, const int32_t* adj, const int64_t* view_vert_first,
+                                         int64_t max_view_verts, const mr_view_t* views, int64_t N, const float* gfv,
+                                         float* gverts, float* gviews, void* stream) {
+  (void)faces;
+  if (N <= 0 || N > 65535 || F < 0 || V < 0 || max_view_verts < 0) return set_err(MR_EINVAL, "bad sizes");
+  if (!view_vert_first) return set_err(MR_EINVAL, "NULL argument");
+  hipStream_t st = (hipStream_t)stream;
+  if (V > 0 && hipMemsetAsync(gverts, 0, sizeof(float) * 3 * (size_t)V, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
+  if (hipMemsetAsync(gviews, 0, sizeof(float) * 12 * (size_t)N, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
+  if (V == 0 || max_view_verts == 0) return MR_OK;
+  dim3 grid(ceil_div(max_view_verts, 256), (unsigned)N);
+  MR_TIMED(KID_PROJECT_BWD, st, (k_project_faces_bwd<<<grid, 256, 0, st>>>(verts, V, F, ptr, adj, (const ViewRec*)views, gfv, gverts, gviews, view_vert_first)));
   MR_CHECK_LAUNCH("k_project_faces_bwd");
   return MR_OK;
 }
@@ -4152,6 +4202,10 @@ size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t m
   BinGeom g = bin_geom(H, W, N, N * F, max_faces_per_bin);
   return carve_raster_ws(nullptr, N, N * F, H, W, g, F).bytes;
 }
+size_t mr_render_workspace_meshes(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin) {
+  BinGeom g = bin_geom(H, W, N, F, max_faces_per_bin);
+  return carve_raster_ws(nullptr, N, F, H, W, g, F).bytes;
+}
 
 static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
                               const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
@@ -4185,7 +4239,11 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
   if (sp->out_flags & MR_OUT_HARD) return set_err(MR_EUNSUPPORTED, "hard_rgb_blend runs on the fragment-shader path (mr_shade_fragments_*)");
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
-  if ((int64_t)N * m->F >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
+  // record ids: n*F + f for one shared mesh; the union face id for distinct meshes
+  const bool multi = m->view_face_first != nullptr;
+  const int64_t NF = multi ? m->F : N * m->F, maxvf = multi ? m->max_view_faces : m->F;
+  if (multi && (!m->view_face_count || maxvf <= 0)) return set_err(MR_EINVAL, "distinct meshes: face ranges missing");
+  if (NF >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*F >= 2^31");
   if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
   if (!views) return set_err(MR_EINVAL, "NULL views");
   if ((sp->out_flags & MR_OUT_DEPTH) && !depth) return set_err(MR_EINVAL, "depth output NULL");
@@ -4193,12 +4251,14 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   if ((sp->out_flags & MR_OUT_RGB) && !rgb) return set_err(MR_EINVAL, "rgb output NULL");
   if (sp->light_kind == 0 && (!cc || (ncc != 1 && ncc != N))) return set_err(MR_EINVAL, "camera centres");
   hipStream_t st = (hipStream_t)stream;
-  BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws(ws, N, N * m->F, s->H, s->W, g, m->F);
+  BinGeom g = bin_geom(s->H, s->W, N, NF, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws(ws, N, NF, s->H, s->W, g, m->F);
   if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
   SetupParams SP = make_setup(s, g, w);
-  SP.NF = N * m->F;
-  FwdParams P = make_fwd(s, g, w, N, nullptr, m->F, N * m->F);
+  SP.NF = NF;
+  SP.vff = m->view_face_first;
+  FwdParams P = make_fwd(s, g, w, N, m->view_face_first, multi ? 0 : m->F, NF);
+  P.view_count = m->view_face_count;
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = w.srec;
   P.out_flags = sp->out_flags;
@@ -4206,7 +4266,7 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  const bool vpath = view_binning(g, N, N * m->F);
+  const bool vpath = view_binning(g, N, NF);
   const int64_t nzero = (int64_t)(zero_bytes(N, g, vpath) / sizeof(int));
   // normals computed here (the mesh's vnormals_out) or passed in (vnormals)
   const int64_t vb = (sp->light_kind == 0 && m->vnormals_out) ? ceil_div(m->V, 256) : 0;
@@ -4221,16 +4281,16 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     NA.vraw = m->vraw_out;
     NA.zero4 = (float4*)w.grows;
     NA.nzero4 = (27 * m->F + 3) / 4;
-    const int64_t bx = std::max<int64_t>(ceil_div(m->F, 256 * MR_RECT_FPT), ceil_div(m->V, 256));
+    const int64_t bx = std::max<int64_t>(ceil_div(maxvf, 256), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
     if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
     else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
     MR_CHECK_LAUNCH("k_bin_rect_world");
     if (sp->rgb_channels == 4) {
-      if ((rc = launch_bin_view<1, 4>(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S, &P))) return rc;
+      if ((rc = launch_bin_view<1, 4>(SP, w, g, N, m->view_face_first, m->view_face_count, m->F, false, st, &P.S, &P))) return rc;
       return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
     }
-    if ((rc = launch_bin_view<1, 3>(SP, w, g, N, nullptr, nullptr, m->F, false, st, &P.S, &P))) return rc;
+    if ((rc = launch_bin_view<1, 3>(SP, w, g, N, m->view_face_first, m->view_face_count, m->F, false, st, &P.S, &P))) return rc;
     return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
   }
   if (hipMemsetAsync(w.grows, 0, sizeof(float) * 27 * (size_t)m->F, st) != hipSuccess)
@@ -4242,8 +4302,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.ctr, nzero)));
   MR_CHECK_LAUNCH("k_setup_zero");
   const int fpt = MR_BIN_FPT;
-  dim3 sgrid(ceil_div(m->F, 256 * fpt), (unsigned)N);
-  dim3 fgrid(sgrid.x, (unsigned)N + 1);  // + the ShadeRec row
+  dim3 sgrid(ceil_div(maxvf, 256 * fpt), (unsigned)N);
+  dim3 fgrid(ceil_div(m->F, 256 * fpt), (unsigned)N + 1);  // + the ShadeRec row (every face of the mesh(es))
   const bool lds = g.T <= MR_LDS_HIST;
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   if (lds)
@@ -4251,7 +4311,7 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   else
     MR_TIMED(KID_BIN_COUNT, st, (k_bin_count_world<false><<<sgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, fpt)));
   MR_CHECK_LAUNCH("k_bin_count_world");
-  if ((rc = launch_scan(w, N, g, nullptr, m->F, st))) return rc;
+  if ((rc = launch_scan(w, N, g, m->view_face_count, m->F, st))) return rc;
   if (lds)
     MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<fgrid, 256, shm, st>>>(SP, m->F, fpt, (int)N, P.S, w.srec)));
   else
@@ -4311,8 +4371,10 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   const size_t need = mr_render_backward_workspace(N, m->V, m->F, s->H, s->W);
   if (bws_bytes < need) return set_err(MR_EWORKSPACE, "backward workspace too small");
   hipStream_t st = (hipStream_t)stream;
-  BinGeom g = bin_geom(s->H, s->W, N, N * m->F, s->max_faces_per_bin);
-  RasterWS w = carve_raster_ws((void*)fws, N, N * m->F, s->H, s->W, g, m->F);
+  const bool multi = m->view_face_first != nullptr;  // distinct meshes: record id = union face id
+  const int64_t NF = multi ? m->F : N * m->F;
+  BinGeom g = bin_geom(s->H, s->W, N, NF, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws((void*)fws, N, NF, s->H, s->W, g, m->F);
   const bool vcol = m->tex_kind == 1;
   const int ACC = vcol ? 27 : 18;
   const int64_t NT = N * (int64_t)g.T;
@@ -4341,10 +4403,11 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.gS = (sp->out_flags & MR_OUT_SIL) ? gS : nullptr;
   P.gRGB = (sp->out_flags & MR_OUT_RGB) ? gRGB : nullptr;
   P.rgb_ch = sp->rgb_channels;
+  P.sil_rgba = (sp->out_flags & MR_OUT_SIL_RGBA) ? 1 : 0;
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = w.srec;
-  P.F = m->F;
-  P.NF = N * m->F;
+  P.F = multi ? 0 : m->F;
+  P.NF = NF;
   P.crec = w.crec;
   P.zc = s->z_clip_value;
   P.views = (const ViewRec*)views;
@@ -4402,7 +4465,7 @@ static FragShadeParams make_frag(const mr_mesh_t* m, const mr_shade_params_t* sp
   FragShadeParams P;
   memset(&P, 0, sizeof(P));
   P.N = (int)N; P.H = H; P.W = W; P.K = K;
-  P.F = m->F;
+  P.F = m->view_face_first ? 0 : m->F;  // face of packed id p: p - n*F (distinct meshes: p itself)
   P.sil = (sp->out_flags & MR_OUT_SIL) ? 1 : 0;
   P.hard = (!P.sil && (sp->out_flags & MR_OUT_HARD)) ? 1 : 0;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;

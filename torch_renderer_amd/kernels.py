@@ -109,9 +109,10 @@ def rasterize_meshes_bwd(face_verts, p2f, gz, gb, gd, H, W, K=1, persp=True, cli
     N = p2f.shape[0]
     s = raster_settings_struct(H, W, K, blur, persp, clip, cull, None, z_clip)
     g = torch.empty_like(fv)
-    check(L.mr_rasterize_meshes_backward(ptr(fv), ptr(p2f.contiguous()), ptr(gz.float().contiguous()),
-                                         ptr(gb.float().contiguous()), ptr(gd.float().contiguous()), N,
-                                         fv.shape[0], ctypes.byref(s), ptr(g), _lib.stream_handle(fv.device)))
+    # a gradient PyTorch passed as None goes down as NULL (zero) instead of a zero-filled tensor
+    gz, gb, gd = (None if t is None else t.float().contiguous() for t in (gz, gb, gd))
+    check(L.mr_rasterize_meshes_backward(ptr(fv), ptr(p2f.contiguous()), ptr(gz), ptr(gb), ptr(gd),
+                                         N, fv.shape[0], ctypes.byref(s), ptr(g), _lib.stream_handle(fv.device)))
     return g
 
 
@@ -132,9 +133,6 @@ class RasterizeFaceVerts(torch.autograd.Function):
     def backward(ctx, _gp, gz, gb, gd):
         fv, p2f = ctx.saved_tensors
         H, W, K, persp, clip, blur, cull, z_clip = ctx.cfg
-        gz = torch.zeros_like(p2f, dtype=torch.float32) if gz is None else gz
-        gb = torch.zeros(p2f.shape + (3,), device=p2f.device) if gb is None else gb
-        gd = torch.zeros_like(p2f, dtype=torch.float32) if gd is None else gd
         g = rasterize_meshes_bwd(fv, p2f, gz, gb, gd, H, W, K, persp, clip, blur, cull, z_clip)
         return (g,) + (None,) * 11
 
@@ -196,6 +194,40 @@ class ProjectFaces(torch.autograd.Function):
         return gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], None, None
 
 
+class ProjectFacesMeshes(torch.autograd.Function):
+    """MeshRasterizer.transform for a batch of N distinct meshes (view n projects mesh n): verts /
+    faces are the meshes' union, face_verts rows are the packed face ids; one launch each way
+    (mr_project_faces_meshes / _backward)."""
+
+    @staticmethod
+    def forward(ctx, verts, R, T, faces, intr, face_first, max_faces, vert_first, max_verts):
+        _require_cuda(verts, R, T, faces)
+        L = _lib.load()
+        v = verts.detach().float().contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
+        views = make_views(R.detach(), T.detach(), intr)
+        N = views.shape[0]
+        out = torch.empty((f.shape[0], 3, 3), device=v.device, dtype=torch.float32)
+        check(L.mr_project_faces_meshes(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(face_first), int(max_faces),
+                                        ptr(views), N, ptr(out), _lib.stream_handle(v.device)))
+        ctx.save_for_backward(v, f, views, vptr, vadj, vert_first)
+        ctx.max_verts = int(max_verts)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        v, f, views, vptr, vadj, vert_first = ctx.saved_tensors
+        L = _lib.load()
+        N = views.shape[0]
+        gv = torch.empty_like(v)
+        gviews = torch.empty((N, 12), device=v.device)
+        check(L.mr_project_faces_meshes_backward(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(vptr), ptr(vadj),
+                                                 ptr(vert_first), ctx.max_verts, ptr(views), N,
+                                                 ptr(g.float().contiguous()), ptr(gv), ptr(gviews),
+                                                 _lib.stream_handle(v.device)))
+        return gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], None, None, None, None, None, None
+
+
 def _poses_struct(R, T, intr):
     """mr_poses_t over (N,3,3) R, (N,3) T, (N,4) intr (a batch stride of 0 broadcasts one row);
     returns the struct and the tensors it points into (keep them alive for the call)."""
@@ -244,9 +276,6 @@ class RasterizeMeshesWorld(torch.autograd.Function):
     def backward(ctx, _gp, gz, gb, gd):
         v, f, views, vptr, vadj, fv, p2f = ctx.saved_tensors
         H, W, K, persp, clip, blur, cull, z_clip = ctx.cfg
-        gz = torch.zeros_like(p2f, dtype=torch.float32) if gz is None else gz
-        gb = torch.zeros(p2f.shape + (3,), device=p2f.device) if gb is None else gb
-        gd = torch.zeros_like(p2f, dtype=torch.float32) if gd is None else gd
         gfv = rasterize_meshes_bwd(fv, p2f, gz, gb, gd, H, W, K, persp, clip, blur, cull, z_clip)
         L = _lib.load()
         N = views.shape[0]
@@ -307,6 +336,7 @@ class ShadeConfig:
     rgb_channels: int = 3
     want_p2f: bool = False  # also return the (N,H,W) int32 packed face ids (tests / tools)
     hard: bool = False  # hard_rgb_blend (HardPhongShader): fragment-shader path only
+    sil_rgba: bool = False  # silhouette as SoftSilhouetteShader's (N,H,W,4) RGBA, written by the kernels
     z_clip: float | None = None  # near clip plane (view z) of FoVPerspectiveCameras: znear / 2
 
     def raster_struct(self):
@@ -326,7 +356,8 @@ class ShadeConfig:
         sp.zfar = float(self.zfar)
         sp.sigma_sil = float(self.sigma_sil)
         sp.out_flags = ((_lib.MR_OUT_DEPTH if self.want_depth else 0) | (_lib.MR_OUT_SIL if self.want_sil else 0) |
-                        (_lib.MR_OUT_RGB if self.want_rgb else 0) | (_lib.MR_OUT_HARD if self.hard else 0))
+                        (_lib.MR_OUT_RGB if self.want_rgb else 0) | (_lib.MR_OUT_HARD if self.hard else 0) |
+                        (_lib.MR_OUT_SIL_RGBA if self.want_sil and self.sil_rgba else 0))
         sp.rgb_channels = int(self.rgb_channels)
         return sp
 
@@ -341,8 +372,12 @@ class TextureArgs:
     tex_lut: torch.Tensor | None = None
 
 
-def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol):
+def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol, ranges=None):
+    """mr_mesh_t; ranges = (view_face_first (N+1), view_face_count (N), max faces) int64 device
+    tensors + int for a batch of distinct meshes (v, f their union), None for one shared mesh."""
     m = MrMesh()
+    if ranges is not None:
+        m.view_face_first, m.view_face_count, m.max_view_faces = ranges[0].data_ptr(), ranges[1].data_ptr(), ranges[2]
     m.verts = v.data_ptr()
     m.V = v.shape[0]
     m.faces = f.data_ptr()
@@ -372,7 +407,7 @@ class RenderViews(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, verts, R, T, vcolors, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs,
-                pose_cv=False):
+                pose_cv=False, ranges=None):
         _require_cuda(verts, R, T, faces)
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled (N,H,W) grads
         L = _lib.load()
@@ -398,17 +433,19 @@ class RenderViews(torch.autograd.Function):
         cc = cam_centers.float().contiguous().reshape(-1, 3)
         rs = cfg.raster_struct()
         sp = cfg.shade_struct()
-        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol)
+        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol, ranges)
         if vn is not None:
             mesh.vnormals_out, mesh.vraw_out = vn.data_ptr(), raw.data_ptr()
         depth = torch.empty((N, H, W), device=dev) if cfg.want_depth else None
-        sil = torch.empty((N, H, W), device=dev) if cfg.want_sil else None
+        sil = torch.empty((N, H, W, 4) if cfg.sil_rgba else (N, H, W), device=dev) if cfg.want_sil else None
         rgb = torch.empty((N, H, W, cfg.rgb_channels), device=dev) if cfg.want_rgb else None
         p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
-        wsb = L.mr_render_workspace(N, f.shape[0], H, W, rs.max_faces_per_bin)
+        wsq = L.mr_render_workspace_meshes if ranges is not None else L.mr_render_workspace
+        wsb = wsq(N, f.shape[0], H, W, rs.max_faces_per_bin)
         ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
         global _LAST_RENDER
-        _LAST_RENDER = (weakref.ref(ws), (N, N * f.shape[0], H, W, rs.max_faces_per_bin))
+        nrec = f.shape[0] if ranges is not None else N * f.shape[0]
+        _LAST_RENDER = (weakref.ref(ws), (N, nrec, H, W, rs.max_faces_per_bin))
         if poses is not None:
             check(L.mr_render_forward_opencv(ctypes.byref(mesh), ctypes.byref(poses), ptr(views), N, ptr(cc),
                                              cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(depth), ptr(sil),
@@ -420,7 +457,7 @@ class RenderViews(torch.autograd.Function):
         ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
                               vn if vn is not None else torch.empty(0, device=dev),
                               raw if raw is not None else torch.empty(0, device=dev), vptr, vadj)
-        ctx.cfg, ctx.tex, ctx.has_vcol, ctx.pose_cv = cfg, tex, vcolors is not None, pose_cv
+        ctx.cfg, ctx.tex, ctx.has_vcol, ctx.pose_cv, ctx.ranges = cfg, tex, vcolors is not None, pose_cv, ranges
         outs = [x for x in (depth, sil, rgb) if x is not None]
         if p2f is not None:
             ctx.mark_non_differentiable(p2f)
@@ -449,7 +486,8 @@ class RenderViews(torch.autograd.Function):
         cfg2.want_depth = gD is not None
         cfg2.want_sil = gS is not None
         cfg2.want_rgb = gC is not None
-        mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None)
+        mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None,
+                            ctx.ranges)
         rs = cfg2.raster_struct()
         sp = cfg2.shade_struct()
         if not getattr(ctx, "rows_used", False):  # the forward cleared the face-gradient rows in ws
@@ -468,20 +506,23 @@ class RenderViews(torch.autograd.Function):
                                               ptr(cc), cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
                                               ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gR),
                                               ptr(gt), ptr(gcol), _lib.stream_handle(dev)))
-            return (gverts, gR, gt, gcol, None, None, None, None, None, None)
+            return (gverts, gR, gt, gcol, None, None, None, None, None, None, None)
         check(L.mr_render_backward(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N, ptr(cc),
                                    cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
                                    ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gviews),
                                    ptr(gcol), _lib.stream_handle(dev)))
-        return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None, None)
+        return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None, None,
+                None)
 
 
 def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs | None = None,
-                 vcolors=None, pose_cv=False):
+                 vcolors=None, pose_cv=False, ranges=None):
     """Functional entry: returns dict(depth, sil, rgb[, pix_to_face32 when cfg.want_p2f]).
-    pose_cv: R, T are OpenCV camera poses (converted on the GPU, gradients returned in kind)."""
+    pose_cv: R, T are OpenCV camera poses (converted on the GPU, gradients returned in kind).
+    ranges: (view_face_first, view_face_count, max faces) when verts / faces are the union of N
+    distinct meshes, view n rendering mesh n (one launch for the batch); None: one shared mesh."""
     tex = tex or TextureArgs()
-    outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex, pose_cv)
+    outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex, pose_cv, ranges)
     res = {}
     i = 0
     for name, want in (("depth", cfg.want_depth), ("sil", cfg.want_sil), ("rgb", cfg.want_rgb)):
@@ -526,7 +567,9 @@ class ShadeFragments(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, zbuf, bary, dists, verts, vcolors, tex_map, verts_uvs, p2f, faces, faces_uvs, cam_centers,
-                cfg: ShadeConfig):
+                cfg: ShadeConfig, ranges=None):
+        """ranges (as render_views): verts / faces are the union of N distinct meshes and
+        pix_to_face holds union face ids (PyTorch3D's packed ids of the batch)."""
         _require_cuda(zbuf, bary, dists, verts, p2f, faces)
         L = _lib.load()
         dev = verts.device
@@ -544,7 +587,7 @@ class ShadeFragments(torch.autograd.Function):
         elif tex_map is not None:
             tex = TextureArgs(2, verts_uvs.detach().float().contiguous(), faces_uvs.to(torch.int32).contiguous(),
                               _padded_rgba(tex_map))
-        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol)
+        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol, ranges)
         sp = cfg.shade_struct()
         sp.out_flags = _lib.MR_OUT_SIL if sil else (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0))
         sp.rgb_channels = 4
@@ -562,7 +605,7 @@ class ShadeFragments(torch.autograd.Function):
                                                     for t in (vn, raw, vcol, tex.verts_uvs, tex.faces_uvs,
                                                               tex.tex_rgba)]
         ctx.save_for_backward(*keep)
-        ctx.cfg, ctx.tex_kind = cfg, tex.kind
+        ctx.cfg, ctx.tex_kind, ctx.ranges = cfg, tex.kind, ranges
         ctx.map_shape = None if tex_map is None else tuple(tex_map.shape)
         ctx.n_uv = 0 if verts_uvs is None else int(verts_uvs.shape[0])
         return rgba
@@ -576,7 +619,7 @@ class ShadeFragments(torch.autograd.Function):
         N, H, W, K = p2f.shape
         e = lambda t: t if t.numel() else None  # noqa: E731
         tex = TextureArgs(ctx.tex_kind, e(vuv), e(fuv), e(rgba_map))
-        mesh = _mesh_struct(v, f, vptr, vadj, e(vn), tex, e(vcol))
+        mesh = _mesh_struct(v, f, vptr, vadj, e(vn), tex, e(vcol), ctx.ranges)
         sp = cfg.shade_struct()
         sp.out_flags = (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0)) if cfg.want_rgb else _lib.MR_OUT_SIL
         sp.rgb_channels = 4
@@ -600,4 +643,4 @@ class ShadeFragments(torch.autograd.Function):
         gm = gmap[..., :ctx.map_shape[-1]] if gmap is not None else None
         if gm is not None and ctx.map_shape[-1] > 3:
             gm = torch.cat([gmap[..., :3], torch.zeros(ctx.map_shape[:2] + (ctx.map_shape[-1] - 3,), device=dev)], -1)
-        return gz, gb, gd, gv, gc, gm, guv, None, None, None, None, None
+        return gz, gb, gd, gv, gc, gm, guv, None, None, None, None, None, None

@@ -33,7 +33,7 @@ from dataclasses import dataclass
 import torch
 
 from .cameras import CamerasBase, view_batch
-from .kernels import ProjectFaces, RasterizeFaceVerts, RasterizeMeshesWorld, ShadeConfig
+from .kernels import ProjectFaces, ProjectFacesMeshes, RasterizeFaceVerts, RasterizeMeshesWorld, ShadeConfig
 from .structures import Meshes
 
 
@@ -238,12 +238,11 @@ class MeshRasterizer(torch.nn.Module):
             return ProjectFaces.apply(meshes.shared_verts(), R, T, meshes.shared_faces(), intr.contiguous())
         if len(meshes) != R.shape[0]:
             raise ValueError(f"Meshes batch ({len(meshes)}) and camera batch ({R.shape[0]}) differ")
-        parts = []
-        for i in range(len(meshes)):
-            mi = meshes[i]
-            parts.append(ProjectFaces.apply(mi.shared_verts(), R[i:i + 1], T[i:i + 1], mi.shared_faces(),
-                                            intr[i:i + 1].contiguous()))
-        return torch.cat(parts, 0)
+        # distinct meshes: their union, view n projecting mesh n, in one launch
+        from .torch_renderer import _union_topology
+        faces_u, ffirst, _, fmax, vfirst, vmax = _union_topology(meshes)
+        return ProjectFacesMeshes.apply(torch.cat(list(meshes.verts_list()), 0), R, T, faces_u, intr.contiguous(),
+                                        ffirst, fmax, vfirst, vmax)
 
     def forward(self, meshes_world: Meshes, **kwargs) -> Fragments:
         """upstream signature: forward(meshes_world, **kwargs) (camera_pose_optimizer.py:175-177,244
@@ -320,7 +319,8 @@ def _shade_config(sh, cameras, H, W, kwargs):
 
 def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_center):
     """The shader over stored fragments on the HIP kernels (mr_shade_fragments_*): one launch for a
-    batch of one shared mesh, one per mesh for a batch of distinct meshes. Returns (N,H,W,4)."""
+    batch of one shared mesh or of distinct meshes (their union; per mesh only when their UV maps
+    differ). Returns (N,H,W,4)."""
     from .kernels import ShadeFragments
     from .structures import TexturesUV, TexturesVertex
 
@@ -352,12 +352,43 @@ def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_
 
     if meshes.is_shared():
         return one(0, N, meshes.shared_verts(), meshes.shared_faces(), tex, 0)
+    if len(meshes) == N and _union_shading_ok(tex, cfg):
+        # distinct meshes: pix_to_face already holds union (packed) face ids
+        from .torch_renderer import _union_topology
+        faces_u, ffirst, fcount, fmax = _union_topology(meshes)[:4]
+        vc = tmap = vuv = fuv = None
+        if cfg.want_rgb and isinstance(tex, TexturesVertex):
+            vc = torch.cat(list(tex.verts_features_list()), 0)
+            if vc.shape[-1] != 3:
+                raise NotImplementedError("TexturesVertex: only 3-channel features are supported")
+        elif cfg.want_rgb and isinstance(tex, TexturesUV):
+            tmap = tex.maps_list()[0]
+            offs, o = [], 0
+            for vu in tex.verts_uvs_list():
+                offs.append(o)
+                o += vu.shape[0]
+            vuv = torch.cat(list(tex.verts_uvs_list()), 0)
+            fuv = torch.cat([fu.to(torch.int64) + off for fu, off in zip(tex.faces_uvs_list(), offs)], 0)
+        return ShadeFragments.apply(fragments.zbuf, fragments.bary_coords, fragments.dists,
+                                    torch.cat(list(meshes.verts_list()), 0), vc, tmap, vuv, p2f.contiguous(), faces_u,
+                                    fuv, cc, cfg, (ffirst, fcount, fmax))
     firsts = meshes.mesh_to_faces_packed_first_idx().tolist()
     outs = []
     for i in range(N):
         mi = meshes[i]
         outs.append(one(i, i + 1, mi.shared_verts(), mi.shared_faces(), mi.textures, int(firsts[i])))
     return torch.cat(outs, 0)
+
+
+def _union_shading_ok(tex, cfg):
+    """Whether a batch of distinct meshes can be shaded as one union mesh: any texture but UV maps
+    that differ between the meshes."""
+    from .structures import TexturesUV
+
+    if not cfg.want_rgb or not isinstance(tex, TexturesUV):
+        return True
+    maps = tex.maps_list()
+    return all(m is maps[0] for m in maps)
 
 
 class _SoftShader(torch.nn.Module):
@@ -441,11 +472,9 @@ class MeshRenderer(torch.nn.Module):
             return self.shader(self.rasterizer(meshes, **kwargs), meshes, **kwargs)
         H, W = rs.hw()
         cfg = self._config(cameras, rs, H, W, kwargs)
+        cfg.sil_rgba = not cfg.want_rgb  # SoftSilhouetteShader's (1, 1, 1, alpha) straight from the kernels
         R, T, _ = _views(meshes, cameras, (H, W), kwargs)
         # specular camera position: cameras.get_camera_center() without the R/T kwargs (upstream
         # shading.py), i.e. from the camera object's own R, T
         out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg)
-        if cfg.want_rgb:
-            return out["rgb"]
-        sil = out["sil"]
-        return torch.cat([torch.ones(sil.shape + (3,), device=sil.device, dtype=sil.dtype), sil[..., None]], -1)
+        return out["rgb"] if cfg.want_rgb else out["sil"]

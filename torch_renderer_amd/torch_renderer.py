@@ -41,6 +41,75 @@ def texture_args(meshes: Meshes, need_color: bool):
     raise NotImplementedError(f"textures of type {type(tex).__name__}")
 
 
+_UNION_CACHE = {}
+
+
+def _union_topology(meshes: Meshes):
+    """(faces (F,3) int64 of the union, view_face_first (N+1), view_face_count (N) int64 device
+    tensors, largest face count, view_vert_first (N+1), largest vertex count) of a batch of distinct
+    meshes, cached on the identity and version of the faces tensors (the union faces tensor keeps
+    its identity, so its CSR stays cached too)."""
+    fl, vl = meshes.faces_list(), meshes.verts_list()
+    key = tuple((id(f), f._version, v.shape[0]) for f, v in zip(fl, vl))
+    hit = _UNION_CACHE.get(id(meshes))
+    if hit is not None and hit[0] == key:
+        return hit[1]
+    voff, out = 0, []
+    for v, f in zip(vl, fl):
+        out.append(f.to(torch.int64) + voff)
+        voff += v.shape[0]
+    counts = [f.shape[0] for f in fl]
+    vcounts = [v.shape[0] for v in vl]
+    first, vfirst = [0], [0]
+    for c, vc in zip(counts, vcounts):
+        first.append(first[-1] + c)
+        vfirst.append(vfirst[-1] + vc)
+    dev = fl[0].device
+    res = (torch.cat(out, 0).contiguous(), torch.tensor(first, dtype=torch.int64, device=dev),
+           torch.tensor(counts, dtype=torch.int64, device=dev), max(counts),
+           torch.tensor(vfirst, dtype=torch.int64, device=dev), max(vcounts))
+    if len(_UNION_CACHE) > 16:
+        _UNION_CACHE.clear()
+    _UNION_CACHE[id(meshes)] = (key, res)
+    return res
+
+
+def union_texture_args(meshes: Meshes, need_color: bool):
+    """texture_args for the union of a batch of distinct meshes, or None when the textures cannot be
+    joined (UV maps that differ between meshes: one fused launch per mesh then)."""
+    tex = meshes.textures
+    if not need_color:
+        return TextureArgs(0), None
+    if tex is None:
+        raise ValueError("Meshes does not have textures")
+    if isinstance(tex, TexturesVertex):
+        vcs = tex.verts_features_list()
+        if any(vc.shape[-1] != 3 for vc in vcs):
+            raise NotImplementedError("TexturesVertex: only 3-channel features are supported")
+        return TextureArgs(1), torch.cat(list(vcs), 0)
+    if isinstance(tex, TexturesUV):
+        maps = tex.maps_list()
+        if any(m is not maps[0] and (m.data_ptr() != maps[0].data_ptr() or m.shape != maps[0].shape) for m in maps):
+            return None
+        vl = meshes.verts_list()
+        key = ("uv",) + tuple((id(a), a._version, id(b), b._version) for a, b in
+                              zip(tex.verts_uvs_list(), tex.faces_uvs_list()))
+        hit = _UNION_CACHE.get(("uv", id(tex)))
+        if hit is None or hit[0] != key:
+            vus, fus, off = [], [], 0
+            for i in range(len(vl)):
+                vu, fu = tex.verts_uvs_list()[i], tex.faces_uvs_list()[i]
+                vus.append(vu.float())
+                fus.append(fu.to(torch.int32) + off)
+                off += vu.shape[0]
+            hit = (key, (torch.cat(vus, 0).contiguous(), torch.cat(fus, 0).contiguous()))
+            _UNION_CACHE[("uv", id(tex))] = hit
+        vuv, fuv = hit[1]
+        u8 = tex.u8_map(0)
+        return TextureArgs(2, vuv, fuv, tex.rgba_map(0), *(u8 if u8 is not None else (None, None))), None
+    raise NotImplementedError(f"textures of type {type(tex).__name__}")
+
+
 def textures_need_modular(meshes: Meshes) -> bool:
     """A TexturesUV map / uv set that requires grad cannot go through the fused K=1 kernels
     (they read a cached detached RGBA copy): route the render through the modular path instead of
@@ -67,8 +136,13 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
                             cfg, tex, vcolors=vcol, pose_cv=pose_cv)
     if len(meshes) != n:
         raise ValueError(f"Meshes batch ({len(meshes)}) and camera batch ({n}) differ")
+    ut = union_texture_args(meshes, need_color)
+    if ut is not None:  # distinct meshes: their union in one launch, view n rendering mesh n
+        faces_u, first, count, fmax = _union_topology(meshes)[:4]
+        return render_views(torch.cat(list(meshes.verts_list()), 0), Rb, Tb, faces_u, intr, cam_center, cfg, ut[0],
+                            vcolors=ut[1], pose_cv=pose_cv, ranges=(first, count, fmax))
     outs = []
-    for i in range(n):  # distinct meshes: one fused launch per view
+    for i in range(n):  # UV maps that differ between meshes: one fused launch per view
         mi = meshes[i]
         tex, vcol = texture_args(mi, need_color)
         cc = cam_center[i:i + 1] if cam_center.shape[0] > 1 else cam_center

@@ -101,24 +101,6 @@ static void timing_end(int i, int kid, hipStream_t st) {
     timing_end(_ti, kid, st);                  \
   } while (0)
 
-// Debug-only phase stamps (build with -DMR_PROF; tools/phase_stamps.py): per wave 8 u64
-// slots of s_memtime at phase boundaries, indexed by the wave's global id.
-#ifdef MR_PROF
-__device__ unsigned long long* g_prof = nullptr;
-#define PROF_T(gw, i)                                                                    \
-  do {                                                                                   \
-    if (g_prof && (threadIdx.x & 63) == 0) g_prof[(size_t)(gw) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-// workgroup-level stamp (thread 0)
-#define PROF_B(gw, i)                                                                    \
-  do {                                                                                   \
-    if (g_prof && threadIdx.x == 0) g_prof[(size_t)(gw) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define PROF_T(gw, i) do {} while (0)
-#define PROF_B(gw, i) do {} while (0)
-#endif
-
 static inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
@@ -255,10 +237,6 @@ struct SetupParams {
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP). Full EXEC required.
 MR_DEV int wave_incl_sum(int v) {
-#ifdef MR_DBG_SHFL
-  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v += u; }
-  return v;
-#endif
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
   v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
@@ -268,10 +246,6 @@ MR_DEV int wave_incl_sum(int v) {
   return v;
 }
 MR_DEV int wave_incl_max(int v) {
-#ifdef MR_DBG_SHFL
-  for (int o = 1; o < 64; o <<= 1) { const int u = __shfl_up(v, o, 64); if ((threadIdx.x & 63) >= o) v = max(v, u); }
-  return v;
-#endif
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
   v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
@@ -634,11 +608,7 @@ __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float
   extern __shared__ __attribute__((aligned(16))) int hist[];
   __shared__ __attribute__((aligned(16))) float sfv[9 * 256 * MR_FV_FPT];
   __shared__ int first32[MR_FV_NMAX];
-#ifdef MR_EXP_FV_DIRECT
-  const FvBlock B = fv_block_setup(fv, Ftot, first, N, first32, sfv, false);
-#else
   const FvBlock B = fv_block_setup(fv, Ftot, first, N, first32, sfv, true);
-#endif
   const bool lds = LDS && B.n0 == B.n1;  // uniform over the workgroup
   if (lds) {
     for (int i = threadIdx.x; i < P.T; i += blockDim.x) hist[i] = 0;
@@ -655,13 +625,8 @@ __global__ void __launch_bounds__(256) k_bin_count_fv(SetupParams P, const float
     const int64_t f = B.f0 + lf;
     const int n = fv_mesh(B, first32, first, N, f);
     float v[3][3];
-#ifdef MR_EXP_FV_DIRECT
-    for (int c = 0; c < 3; ++c)
-      for (int q = 0; q < 3; ++q) v[c][q] = fv[9 * f + 3 * c + q];
-#else
     for (int c = 0; c < 3; ++c)
       for (int q = 0; q < 3; ++q) v[c][q] = sfv[9 * lf + 3 * c + q];
-#endif
     FaceRec r2;
     const FaceRec r = build_records(P, f, (uint32_t)f, v, r2);
     P.recs[f] = r;
@@ -957,7 +922,9 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
   // One face per thread; the workgroup's records (and face_verts rows) are contiguous in HBM, so
   // they are staged through LDS and stored as whole lines (each store instruction writes 1 KB of
   // consecutive bytes instead of 64 lanes' 16-B pieces 64 B apart).
-  __shared__ float4 s4[4 * 256];
+  // s4 element e (record e / 4, quarter e % 4) at e + e / 16: the record-major writes (16-B pieces
+  // 64 B apart) then land on distinct bank groups (4-way conflicts without the pad)
+  __shared__ float4 s4[4 * 256 + 64];
   __shared__ float s9[9 * 256];
   // view n's faces: mesh faces [fbase, fbase + Fv) -> records [rbase, rbase + Fv)
   int64_t Fv = F, rbase = (int64_t)n * F, fbase = 0;
@@ -993,7 +960,7 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
     float4 q4[4];
     __builtin_memcpy(q4, &r, sizeof(q4));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) s4[4 * t + q] = q4[q];
+    for (int q = 0; q < 4; ++q) s4[4 * t + q + (t >> 2)] = q4[q];
     P.rects[rid] = rec_rect(P, r);
     if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
   }
@@ -1001,7 +968,7 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
   float4* d4 = (float4*)(P.recs + rid0);
 #pragma unroll
   for (int j = 0; j < 4; ++j)
-    if (j * 256 + t < 4 * nf) d4[j * 256 + t] = s4[j * 256 + t];
+    if (j * 256 + t < 4 * nf) d4[j * 256 + t] = s4[j * 256 + t + ((j * 256 + t) >> 4)];
   if (P.fv_out) {
     float* d9 = P.fv_out + rid0 * 9;
 #pragma unroll
@@ -1090,7 +1057,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // banks); a view's rectangles are read in chunks of MR_VIEW_RPT per thread, all loads of a
   // chunk in flight together, and a view of one chunk keeps them in registers for the fill.
   const int j = t;
-  PROF_B(60000 + n, 0);
   const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   for (int i = t; i < P.T + (P.T >> 6); i += 1024) hist[i] = 0;
@@ -1117,7 +1083,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
   }
   lds_barrier();
-  PROF_B(60000 + n, 1);
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
   const int C = (P.T + 1023) / 1024;
   const int t0 = min(t * C, P.T), t1 = min(t0 + C, P.T);
@@ -1133,7 +1098,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int ex0 = block_incl_sum<true>(le, part, te) - le;
   const int iu = block_incl_sum<true>(my_u, part, au);
   const int is = block_incl_sum<true>(my_s, part, as);
-  PROF_B(60000 + n, 2);
   // the three allocations from three waves: their round trips overlap instead of queueing
   if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
@@ -1146,7 +1110,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
   }
   lds_barrier();
-  PROF_B(60000 + n, 3);
   const long long vb = base[2];
   if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
   int u0 = (int)base[0] + iu - my_u, slot = (int)base[1] + is - my_s;
@@ -1187,7 +1150,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
-  PROF_B(60000 + n, 4);
   // fill: the view's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
   // staged in LDS and stored as consecutive lines afterwards (scattered 4-B stores issue one
   // lane per cycle), the rest (a view larger than the stage) go straight to the pool
@@ -1217,13 +1179,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   for (int i = t; i < lst; i += 1024)
     if (vb + i < P.list_cap) P.list[vb + i] = stage[i];
-#ifdef MR_PROF
-  __syncthreads();
-#endif
-  PROF_B(60000 + n, 5);
-#ifdef MR_PROF
-  if (t == 0 && g_prof) g_prof[(size_t)(60000 + n) * 8 + 7] = 1;
-#endif
 }
 __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) { bin_view_body(P); }
 
@@ -1648,11 +1603,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const int nunits = P.ctr[CTR_UNITS];
   const float pad = P.bbox_pad, blur = P.blur;
   const bool persp = P.persp != 0, clipb = P.clipb != 0;
-#ifdef MR_DBG_NOFAST
-  const bool fast_ok = false;
-#else
   const bool fast_ok = !(blur > 0.0f);
-#endif
   const int H = P.H, W = P.W;
   // background chunks of this wave: c = gw, gw + G, ... < N * cpv, written after its units (the
   // waves that finish their raster work early stream the background while the others still run;
@@ -1688,14 +1639,6 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   int id1 = P.list[(ub + jw < ue && U1v.y >= 0 && lane < U1v.z) ? U1v.y + lane : 0];
   int id2 = P.list[(ub + jw + Gp < ue && U2v.y >= 0 && lane < U2v.z) ? U2v.y + lane : 0];
   FaceRec r1 = load_rec(P.recs, (ub + jw < ue && U1v.y >= 0 && lane < U1v.z) ? id1 : 0);
-#ifdef MR_PROF
-  unsigned long long acc_load = 0, acc_pass = 0, acc_emit = 0, acc_fill = 0, acc_eval = 0, npass = 0, nunit = 0;
-  unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-  const unsigned long long tstart = tp0;
-#define ACC(v) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); v += _t - tp0; tp0 = _t; } while (0)
-#else
-#define ACC(v) do {} while (0)
-#endif
 #pragma unroll 1
   for (int u = ub + jw; u < ue; u += Gp) {
     const int4 U = make_int4(__builtin_amdgcn_readfirstlane(U1v.x), __builtin_amdgcn_readfirstlane(U1v.y),
@@ -1772,21 +1715,16 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
         U3v = P.units[min(u + 3 * Gp, ulast) + lz];
       }
       // candidate numbering: a DPP prefix sum over the masks' popcounts
-      ACC(acc_load);
       const int np = __popcll(cmask);
       const int pincl = wave_incl_sum(np);
       const int pexcl = pincl - np;
       const int NP = __builtin_amdgcn_readlane(pincl, 63);
       S.meta[lane] = pexcl;
       S.cmask[lane] = cmask;
-      ACC(acc_pass);
       // 64 candidates per pass, one per lane, each evaluated exactly (frag_keep: bbox, edge
       // signs, divisions, perspective correction, depth) and merged into the tile's keys
 #pragma unroll 1
       for (int pb = 0; pb < NP; pb += 64) {
-#ifdef MR_PROF
-        ++npass;
-#endif
         wave_lds_sync();
         // the entry starting inside this pass marks its first slot; slot 0 belongs to the
         // entry straddling pb (the last non-empty entry starting at or before it)
@@ -1808,13 +1746,11 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
             atomicMin(&S.key[p], frag_key(pz, CLIP ? (int)rec_code(S.id[m], P.NF) : 2 * S.id[m]));
         }
       }
-      ACC(acc_eval);
       if (CLIP && __builtin_expect(__ballot(prect != 0) != 0ull, 0)) {
         // near-plane split faces (rare): each such lane walks its rectangle, resolving the pair
         if (prect) raster_pair_rect(P.recs, P.NF, S.rec, S.id, S.xs, S.ys, S.key, lane, prect, pad, blur, persp, clipb);
       }
       wave_lds_sync();  // the stage is rewritten by the next batch
-      ACC(acc_pass);
     }
     unsigned long long k = S.key[lane];
     const int slot = U.w & 0x7fffffff;
@@ -1840,22 +1776,9 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
       P.sface[(int64_t)slot * 64 + lane] = hit ? (CLIP ? code_rec(code, P.NF) : (int)(code >> 1)) : -1;
     }
     wave_lds_sync();
-    ACC(acc_emit);
-#ifdef MR_PROF
-    ++nunit;
-#endif
   }
 #pragma unroll 1
   for (; chunk < nchunks; chunk += G) fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
-  ACC(acc_fill);
-#ifdef MR_PROF
-  if (g_prof && lane == 0) {
-    unsigned long long* o = g_prof + (size_t)gw * 8;
-    o[0] = acc_load; o[1] = acc_pass; o[2] = acc_emit; o[3] = acc_fill;
-    o[4] = acc_eval; o[5] = npass * 65536 + nunit; o[6] = __builtin_amdgcn_s_memtime() - tstart; o[7] = 1;
-  }
-#endif
-#undef ACC
 }
 
 // Per-face shading records of the shared mesh (one thread per face).
@@ -2122,273 +2045,233 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
   }
 }
 
-// K <= 64: the same per-tile raster with each lane's K nearest keys in REGISTERS (KP >= K slots,
-// ascending), merged by a compare-exchange network instead of a per-lane LDS insertion loop. The
-// LDS version runs one dependent LDS read / write per shifted entry, every lane waiting for the
-// longest shift of the wave, at one or two waves per SIMD (K * 512 B of LDS per wave); the network
-// is KP unconditional min / max steps of straight VALU, run only when some lane's candidate beats
-// its current KP-th key, and the keys need no LDS (only the staged face records). The KP smallest
-// keys contain the K smallest, so the output (the first K, ascending) is the same.
-template <int KP>
-__global__ void __launch_bounds__(256) k_raster_kr(FwdParams P) {
-  __shared__ FaceRec srs[4][64];
-  __shared__ int sids[4][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  FaceRec* rs = srs[wave];
-  int* ids = sids[wave];
-  const int K = P.K;
-  const int nslots = P.ctr[CTR_SLOTS];
-  const float pad = P.bbox_pad, blur = P.blur;
-  const bool persp = P.persp != 0, clipb = P.clipb != 0;
-  const bool fast_ok = !(blur > 0.0f);
-  const int H = P.H, W = P.W;
-  const int64_t HW = (int64_t)H * W;
-#pragma unroll 1
-  for (int s = blockIdx.x * 4 + wave; s < nslots; s += gridDim.x * 4) {
-    const int gt = P.stile[s];
-    const int n = gt / P.T, t = gt - n * P.T;
-    const int ty = t / P.TX, tx = t - ty * P.TX;
-    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
-    const bool in_img = px < W && py < H;
-    const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
-    const int cc = P.cnt[gt], ex = P.start[gt];
-    const int64_t vb = P.vbase[n];
-    const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
-    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
-    const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
-    const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
-    unsigned long long q[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
-#pragma unroll 1
-    for (int eb = 0; eb < count; eb += 64) {
-      const int e = eb + lane;
-      if (e < count) {
-        const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
-        rs[lane] = P.recs[id];
-        ids[lane] = id;
-      }
-      wave_lds_sync();
-      const int m = count - eb < 64 ? count - eb : 64;
-      auto cand = [&](int jj) -> unsigned long long {  // the key of staged face jj at this lane's pixel
-        const FaceRec r = rs[jj];
-        const int id = ids[jj];
-        float pz;
-        int cid = id;
-        bool keep = false;
-        if (in_img && (r.flags & FR_PAIR)) {  // as k_raster_k
-          keep = pair_keep(P.recs, P.NF, id, r, xf, yf, pad, blur, persp, clipb, cid, pz) &&
-                 (cid == id || (ovf && id < P.NF));
-        } else if (in_img && (r.flags & FR_VALID)) {
-          keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
-        }
-        return keep ? frag_key(pz, (int)rec_code(cid, P.NF)) : MR_KEY_EMPTY;
-      };
-      auto insert = [&](unsigned long long key) {
-        if (__ballot(key < q[KP - 1]) != 0ull) {
-#ifndef MR_KR_CHAIN
-          // shift-insert with every step independent: q is ascending, so key < q[k] holds from the
-          // insertion point on; walking down, slot k takes q[k-1] (if key < q[k-1] too) or key. The
-          // compare-exchange chain instead carried key through all KP steps (a KP-long dependency).
-          bool ltk = key < q[KP - 1];
-#pragma unroll
-          for (int k = KP - 1; k > 0; --k) {
-            const bool ltp = key < q[k - 1];
-            q[k] = ltk ? (ltp ? q[k - 1] : key) : q[k];
-            ltk = ltp;
-          }
-          q[0] = ltk ? key : q[0];
-#else
-#pragma unroll
-          for (int k = 0; k < KP; ++k) {
-            const unsigned long long a = q[k];
-            const bool lt = key < a;
-            q[k] = lt ? key : a;
-            key = lt ? a : key;
-          }
+// K <= 64 (PyTorch3D faces_per_pixel > 1): one wave per non-empty tile, each lane keeping its pixel's
+// K nearest (z, face) keys in REGISTERS (KP >= K slots, ascending; a shift-insert whose KP steps are
+// independent selects, shifted out through slot 0 so the array is never dynamically indexed). The
+// keys are evaluated over (face, pixel) PAIRS: as in k_tile_raster, each lane clips one list entry's
+// padded bbox to the tile, a DPP prefix numbers the pairs and a pass evaluates 64 of them exactly
+// (frag_keep / pair_keep, one per lane) — with blur a face of the deform workload covers ~a quarter
+// of the tile, and evaluating every listed face at all 64 pixels (the previous kernel) ran 4x the
+// exact tests. A kept candidate goes to its PIXEL's LDS bucket; the buckets drain into the register
+// lists when the fullest has less than MR_KP_ROOM slots left and at the end of the tile, so a list
+// takes one insert per candidate of its pixel (~4 of K = 50 on the deform workload), not one per
+// listed face, and a drain whose lists will all hold <= 8 / 16 / 32 keys runs that many shift steps
+// instead of KP. A pass is limited to the entries whose candidates the buckets can still take (an
+// entry adds at most one candidate per pixel). The K nearest keys do not depend on the insertion
+// order: the fragments are bitwise those of the face-at-a-time kernel (deform workload: 2.22 ms
+// (two waves per tile, every face at every pixel) -> see DESIGN.md for this kernel's numbers).
+#ifndef MR_KP_BC
+#define MR_KP_BC 32
 #endif
-        }
-      };
-#pragma unroll 1
-      for (int j = 0; j < m; ++j) insert(cand(j));
-      wave_lds_sync();
-    }
-    if (!in_img) continue;
-    const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
-    // the keys leave in ascending order through q[0], the array shifting down one slot per step:
-    // only constant indices into q[] (a dynamic index would demote the array to scratch), and the
-    // output body (eval_face) is not unrolled KP times
-    // only the filled slots: k_fill wrote the background (-1) of every slot, and the K nearest
-    // lists are short at large K (3.7 of 50 slots per pixel on the deform workload); the loop ends
-    // when no lane of the wave has a key left
-#pragma unroll 1
-    for (int k = 0; k < K; ++k) {
-      if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
-      const unsigned long long key = q[0];
+// Shift-insert of key into the first NS positions of the ascending list q (positions >= NS are
+// empty for every lane of the wave and stay so: no lane holds more than NS keys).
+template <int KP, int NS>
+MR_DEV void insert_ns(unsigned long long (&q)[KP], unsigned long long key) {
+  if (__ballot(key < q[NS - 1]) != 0ull) {
+    bool ltk = key < q[NS - 1];
 #pragma unroll
-      for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
-      q[KP - 1] = MR_KEY_EMPTY;
-      if (!(key < MR_KEY_EMPTY)) continue;
-      int64_t f = -1;
-      float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
-      {
-        const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
-        const FaceRec r = P.recs[id];
-        FragEval ev;
-        eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
-        if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
-        f = rec_orig(id, P.NF); z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
-      }
-      P.p2f[pix + k] = f;
-      P.zbuf[pix + k] = z;
-      P.dists[pix + k] = d;
-      P.bary[3 * (pix + k) + 0] = b0;
-      P.bary[3 * (pix + k) + 1] = b1;
-      P.bary[3 * (pix + k) + 2] = b2;
+    for (int k = NS - 1; k > 0; --k) {
+      const bool ltp = key < q[k - 1];
+      q[k] = ltk ? (ltp ? q[k - 1] : key) : q[k];
+      ltk = ltp;
     }
+    q[0] = ltk ? key : q[0];
   }
 }
 
-// The same with one WORKGROUP per tile: its four waves take a quarter of the tile's list each and
-// the partial K-lists are merged through LDS by wave 0 (workgroup-local, so no cross-XCD
-// hand-off). With one wave per tile the kernel lasted as long as the longest list (1,896 entries
-// against a mean of 451 on the deform workload); split four ways the long lists finish sooner and
-// the short ones share the CUs.
-#ifndef MR_KR_WPT
-#define MR_KR_WPT 2  // waves per tile in k_raster_kr4 (2: 2.18 ms, 4: 2.37, 8: 3.58 on the deform workload)
+#ifndef MR_KP_ROOM
+#define MR_KP_ROOM 16  // drain the buckets once the fullest one has less room than this
 #endif
+struct KpStage {
+  float rec[16][64];
+  int id[64];
+  int meta[64];
+  int mark[64];
+  int bcnt[64];
+  unsigned long long cmask[64];
+  unsigned long long bucket[MR_KP_BC][64];
+};
 template <int KP>
-__global__ void __launch_bounds__(64 * MR_KR_WPT) k_raster_kr4(FwdParams P) {
-  __shared__ FaceRec srs[MR_KR_WPT][64];
-  __shared__ int sids[MR_KR_WPT][64];
-  __shared__ unsigned long long mbuf[KP * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  FaceRec* rs = srs[wave];
-  int* ids = sids[wave];
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_raster_kp(FwdParams P) {
+  __shared__ KpStage S;
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x;
+  if (s >= P.ctr[CTR_SLOTS]) return;
   const int K = P.K;
-  const int nslots = P.ctr[CTR_SLOTS];
   const float pad = P.bbox_pad, blur = P.blur;
   const bool persp = P.persp != 0, clipb = P.clipb != 0;
   const bool fast_ok = !(blur > 0.0f);
   const int H = P.H, W = P.W;
   const int64_t HW = (int64_t)H * W;
+  const int gt = P.stile[s];
+  const int n = gt / P.T, t = gt - n * P.T;
+  const int ty = t / P.TX, tx = t - ty * P.TX;
+  const int x0 = tx * MR_TS, y0 = ty * MR_TS;
+  const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
+  const bool in_img = px < W && py < H;
+  const int cc = P.cnt[gt], ex = P.start[gt];
+  const int64_t vb = P.vbase[n];
+  const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
+  const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
+  const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
+  const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
+  const int xe = min(x0 + MR_TS, W) - 1, ye = min(y0 + MR_TS, H) - 1;  // the tile's last pixels inside the image
+  unsigned long long q[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
+  auto insert = [&](unsigned long long key) {
+    if (__ballot(key < q[KP - 1]) != 0ull) {
+      bool ltk = key < q[KP - 1];
+#pragma unroll
+      for (int k = KP - 1; k > 0; --k) {
+        const bool ltp = key < q[k - 1];
+        q[k] = ltk ? (ltp ? q[k - 1] : key) : q[k];
+        ltk = ltp;
+      }
+      q[0] = ltk ? key : q[0];
+    }
+  };
+  S.bcnt[lane] = 0;
+  S.mark[lane] = -1;
+  int mb = 0;  // the fullest bucket's fill (uniform)
+  int lc = 0;  // keys in this lane's list
+  // Drain: every bucket's keys into its lane's list. The lists' fill after the drain is known before
+  // it (all keys are distinct, so none is dropped until a list holds KP): when no lane will hold more
+  // than NS keys, only the first NS positions can change and the shift runs NS steps, not KP
+  // (most lists hold a few keys: the full KP-step shift was ~half of the kernel).
+  auto drain = [&]() {
+    wave_lds_sync();
+    const int c = S.bcnt[lane];
+    const int mc = __builtin_amdgcn_readlane(wave_incl_max(c), 63);
+    lc = min(lc + c, KP);
+    const int need = __builtin_amdgcn_readlane(wave_incl_max(lc), 63);
+    if (need <= 8 && KP > 8) {
 #pragma unroll 1
-  for (int s = blockIdx.x; s < nslots; s += gridDim.x) {  // uniform over the workgroup
-    const int gt = P.stile[s];
-    const int n = gt / P.T, t = gt - n * P.T;
-    const int ty = t / P.TX, tx = t - ty * P.TX;
-    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
-    const bool in_img = px < W && py < H;
-    const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
-    const int cc = P.cnt[gt], ex = P.start[gt];
-    const int64_t vb = P.vbase[n];
-    const bool ovf = vb + ex + cc > P.list_cap || (P.mfpb > 0 && cc > P.mfpb);
-    const int64_t vfirst = P.view_first ? P.view_first[n] : (int64_t)n * P.F;
-    const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
-    const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
-    // this wave's share of the list, in whole 64-entry batches
-    const int chunk = (((count + MR_KR_WPT - 1) / MR_KR_WPT) + 63) & ~63;
-    const int e0 = min(wave * chunk, count), e1 = min(e0 + chunk, count);
-    unsigned long long q[KP];
-#pragma unroll
-    for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
-    auto insert = [&](unsigned long long key) {
-      if (__ballot(key < q[KP - 1]) != 0ull) {
-        bool ltk = key < q[KP - 1];
-#pragma unroll
-        for (int k = KP - 1; k > 0; --k) {
-          const bool ltp = key < q[k - 1];
-          q[k] = ltk ? (ltp ? q[k - 1] : key) : q[k];
-          ltk = ltp;
+      for (int i = 0; i < mc; ++i) insert_ns<KP, (KP > 8 ? 8 : KP)>(q, i < c ? S.bucket[i][lane] : MR_KEY_EMPTY);
+    } else if (need <= 16 && KP > 16) {
+#pragma unroll 1
+      for (int i = 0; i < mc; ++i) insert_ns<KP, (KP > 16 ? 16 : KP)>(q, i < c ? S.bucket[i][lane] : MR_KEY_EMPTY);
+    } else if (need <= 32 && KP > 32) {
+#pragma unroll 1
+      for (int i = 0; i < mc; ++i) insert_ns<KP, (KP > 32 ? 32 : KP)>(q, i < c ? S.bucket[i][lane] : MR_KEY_EMPTY);
+    } else {
+#pragma unroll 1
+      for (int i = 0; i < mc; ++i) insert(i < c ? S.bucket[i][lane] : MR_KEY_EMPTY);
+    }
+    S.bcnt[lane] = 0;
+    wave_lds_sync();
+    mb = 0;
+  };
+#pragma unroll 1
+  for (int eb = 0; eb < count; eb += 64) {
+    const int e = eb + lane;
+    unsigned long long cmask = 0;
+    if (e < count) {
+      const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
+      const FaceRec r = load_rec(P.recs, id);
+      // candidate pixels: the record's padded bbox; an overflow unit scans only first triangles of
+      // split faces, so there it covers both triangles of the pair (as k_tile_raster)
+      float bx0 = r.xmin, bx1 = r.xmax, by0 = r.ymin, by1 = r.ymax;
+      bool bvalid = (r.flags & FR_VALID) != 0;
+      if (ovf && (r.flags & FR_PAIR) && id < P.NF) {
+        const FaceRec ro = load_rec(P.recs, P.NF + id);
+        if (ro.flags & FR_VALID) {
+          bx0 = bvalid ? smin(bx0, ro.xmin) : ro.xmin;
+          bx1 = bvalid ? smax(bx1, ro.xmax) : ro.xmax;
+          by0 = bvalid ? smin(by0, ro.ymin) : ro.ymin;
+          by1 = bvalid ? smax(by1, ro.ymax) : ro.ymax;
+          bvalid = true;
         }
-        q[0] = ltk ? key : q[0];
       }
-    };
+      int cx0, cx1, cy0, cy1;
+      ndc_range_to_pix(bx0 - pad, bx1 + pad, W, H, cx0, cx1);
+      ndc_range_to_pix(by0 - pad, by1 + pad, H, W, cy0, cy1);
+      cx0 = max(cx0, x0);
+      cx1 = min(cx1, xe);
+      cy0 = max(cy0, y0);
+      cy1 = min(cy1, ye);
+      if (bvalid && cx0 <= cx1 && cy0 <= cy1) cmask = rect_mask(cx0 - x0, cx1 - x0, cy0 - y0, cy1 - y0);
+      stage_rec_put(S.rec, lane, r);
+      S.id[lane] = id;
+    }
+    const int np = __popcll(cmask);
+    const int pincl = wave_incl_sum(np);
+    const int pexcl = pincl - np;
+    const int NP = __builtin_amdgcn_readlane(pincl, 63);
+    S.meta[lane] = pexcl;
+    S.cmask[lane] = cmask;
 #pragma unroll 1
-    for (int eb = e0; eb < e1; eb += 64) {
-      const int e = eb + lane;
-      if (e < e1) {
-        const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
-        rs[lane] = P.recs[id];
-        ids[lane] = id;
-      }
+    for (int pb = 0; pb < NP;) {
+      if (mb > MR_KP_BC - MR_KP_ROOM) drain();
+      // the entry straddling pb, and the first entry past what the buckets can still take
+      const int first = 63 - __builtin_clzll(__ballot(np > 0 && pexcl <= pb));
+      const int lim = first + (MR_KP_BC - mb);
+      const int pend = min(pb + 64, lim < 64 ? __builtin_amdgcn_readlane(pexcl, lim) : NP);
       wave_lds_sync();
-      const int m = e1 - eb < 64 ? e1 - eb : 64;
-#pragma unroll 1
-      for (int j = 0; j < m; ++j) {
-        const FaceRec r = rs[j];
-        const int id = ids[j];
+      if (np > 0 && pexcl > pb && pexcl < pend) S.mark[pexcl - pb] = lane;
+      wave_lds_sync();
+      int m = S.mark[lane];
+      S.mark[lane] = -1;
+      if (lane == 0) m = first;
+      m = wave_incl_max(m);
+      const int qq = pb + lane;
+      if (qq < pend) {
+        const int p = kth_bit(S.cmask[m], qq - S.meta[m]);
+        const FaceRec r = stage_rec_get(S.rec, m);
+        const int id = S.id[m];
+        const float xf = col_ndc(x0 + (p & 7), H, W), yf = row_ndc(y0 + (p >> 3), H, W);
         float pz;
         int cid = id;
         bool keep = false;
-        if (in_img && (r.flags & FR_PAIR)) {  // as k_raster_k
+        if (r.flags & FR_PAIR) {  // the split face's two triangles as one candidate (pair rule)
           keep = pair_keep(P.recs, P.NF, id, r, xf, yf, pad, blur, persp, clipb, cid, pz) &&
                  (cid == id || (ovf && id < P.NF));
-        } else if (in_img && (r.flags & FR_VALID)) {
+        } else if (r.flags & FR_VALID) {
           keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
         }
-        insert(keep ? frag_key(pz, (int)rec_code(cid, P.NF)) : MR_KEY_EMPTY);
-      }
-      wave_lds_sync();
-    }
-    // waves 1..3 hand their lists to wave 0 through LDS, one at a time
-#pragma unroll 1
-    for (int w2 = 1; w2 < MR_KR_WPT; ++w2) {
-      __syncthreads();
-      if (wave == w2) {
-#pragma unroll
-        for (int k = 0; k < KP; ++k) mbuf[k * 64 + lane] = q[k];
-      }
-      __syncthreads();
-      if (wave == 0) {
-#pragma unroll 1
-        for (int k = 0; k < KP; ++k) {
-          const unsigned long long key = mbuf[k * 64 + lane];
-          if (__ballot(key < MR_KEY_EMPTY) == 0ull) break;  // each list is ascending
-          insert(key);
+        if (keep) {
+          const int pos = atomicAdd(&S.bcnt[p], 1);
+          S.bucket[pos][p] = frag_key(pz, (int)rec_code(cid, P.NF));
         }
       }
+      pb = pend;
+      wave_lds_sync();
+      mb = __builtin_amdgcn_readlane(wave_incl_max(S.bcnt[lane]), 63);  // the fullest bucket
     }
-    if (wave == 0 && in_img) {
-      const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
-      // only the filled slots (k_fill wrote the background of every slot); keys shifted out
-      // through q[0] (constant indices only: the array stays in registers)
+    wave_lds_sync();  // the stage is rewritten by the next batch
+  }
+  drain();
+  if (!in_img) return;
+  const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
+  const float xf = col_ndc(px, H, W), yf = row_ndc(py, H, W);
+  // only the filled slots (k_fill wrote the background of every slot); keys shifted out through q[0]
+  // (constant indices only: the array stays in registers)
 #pragma unroll 1
-      for (int k = 0; k < K; ++k) {
-        if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
-        const unsigned long long key = q[0];
+  for (int k = 0; k < K; ++k) {
+    if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
+    const unsigned long long key = q[0];
 #pragma unroll
-        for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
-        q[KP - 1] = MR_KEY_EMPTY;
-        if (!(key < MR_KEY_EMPTY)) continue;
-        const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
-        const FaceRec r = P.recs[id];
-        FragEval ev;
-        eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
-        if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
-        P.p2f[pix + k] = rec_orig(id, P.NF);
-        P.zbuf[pix + k] = ev.pz;
-        P.dists[pix + k] = ev.sdist;
-        P.bary[3 * (pix + k) + 0] = ev.b0;
-        P.bary[3 * (pix + k) + 1] = ev.b1;
-        P.bary[3 * (pix + k) + 2] = ev.b2;
-      }
-    }
+    for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
+    q[KP - 1] = MR_KEY_EMPTY;
+    if (!(key < MR_KEY_EMPTY)) continue;
+    const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
+    const FaceRec r = P.recs[id];
+    FragEval ev;
+    eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
+    if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+    P.p2f[pix + k] = rec_orig(id, P.NF);
+    P.zbuf[pix + k] = ev.pz;
+    P.dists[pix + k] = ev.sdist;
+    P.bary[3 * (pix + k) + 0] = ev.b0;
+    P.bary[3 * (pix + k) + 1] = ev.b1;
+    P.bary[3 * (pix + k) + 2] = ev.b2;
   }
 }
 
 template <int KP>
 static void launch_raster_kr(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
-#ifndef MR_RASTER_KR_WAVE
-  const int grid = (int)(slots_cap < 16384 ? slots_cap : 16384);  // one workgroup per tile
-  MR_TIMED(KID_RASTER_K, st, (k_raster_kr4<KP><<<grid, 64 * MR_KR_WPT, 0, st>>>(P)));
-#else
-  const int64_t want = (slots_cap + 3) / 4;
-  const int grid = (int)(want < 8192 ? want : 8192);
-  MR_TIMED(KID_RASTER_K, st, (k_raster_kr<KP><<<grid, 256, 0, st>>>(P)));
-#endif
+  if (slots_cap >= (1ll << 31)) return;
+  MR_TIMED(KID_RASTER_K, st, (k_raster_kp<KP><<<(unsigned)slots_cap, 64, 0, st>>>(P)));  // one wave per tile
 }
 
 static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
@@ -2397,7 +2280,6 @@ static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipS
   MR_TIMED(KID_FILL_FRAG, st, (k_fill<0, 3><<<fgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_fill");
   const int K = P.K;
-#ifndef MR_RASTER_K_LDS
   if (K <= 64) {  // keys in registers (k_raster_kr)
     const int64_t sc = N * (int64_t)g.T;
     if (K <= 4) launch_raster_kr<4>(P, sc, st);
@@ -2409,7 +2291,6 @@ static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipS
     MR_CHECK_LAUNCH("k_raster_kr");
     return MR_OK;
   }
-#endif
   const size_t wb = (size_t)K * 64 * 8 + 64 * sizeof(FaceRec) + 64 * sizeof(int);
   const int wpg = wb * 4 <= 65536 ? 4 : wb * 2 <= 65536 ? 2 : 1;
   const int64_t slots_cap = N * (int64_t)g.T;
@@ -2684,11 +2565,7 @@ MR_DEV void seg_flush(int nt, float* __restrict__ dst, const float* lrow, const 
       if (j < tot) {
         const int r = j / ACC;
         const float x = lrow[j];
-#ifndef MR_EXP_NOATOMIC
         if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
-#else
-        if (x == 1234.5f) dst[0] = x;  // experiment build: keep the reduction, drop the atomics
-#endif
       }
     }
     __builtin_amdgcn_sched_barrier(0);  // one row block at a time (no hoisting: register peak)
@@ -2819,11 +2696,7 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 
 // CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
 // instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
-#ifdef MR_BWD_WAVES  // experiment builds: force an occupancy target
-#define MR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(MR_BWD_WAVES)))
-#else
 #define MR_BWD_ATTR
-#endif
 // The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
 // through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
 // loop, overflow the SGPR file and are spilled into VGPR lanes (one v_readlane per use; k_bwd_fused had
@@ -2868,14 +2741,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
-#ifdef MR_PROF
-  unsigned long long pacc[7] = {0, 0, 0, 0, 0, 0, 0}, nit = 0;
-  unsigned long long tp0 = __builtin_amdgcn_s_memtime();
-  const unsigned long long tstart = tp0;
-#define BACC(i) do { const unsigned long long _t = __builtin_amdgcn_s_memtime(); pacc[i] += _t - tp0; tp0 = _t; } while (0)
-#else
-#define BACC(i) do {} while (0)
-#endif
   for (; s < send; s += G) {
     const RenderBwdParams& P = kernarg_params<RenderBwdParams>();  // see kernarg_params
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c;
@@ -2894,7 +2759,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     f_n = P.sface[(int64_t)sc * 64 + lane];
     int n, px, py;
     slot_pixel(P, gt, lane, n, px, py);
-    BACC(0);
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (f >= 0) {
       PixGeom Gm;
@@ -2918,19 +2782,12 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, es);
         e.pz = es.pz;
       }
-#ifdef MR_EXP_NOHALF1
-      if (false) {  // experiment build: no shading backward (half 2 gets zero records)
-#else
       {
-#endif
         ShadeOut so;
         ShadeCache C;
-        BACC(1);
         shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C, lut);
-        BACC(2);
         ShadeGrad SG;
         shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
-        BACC(3);
         o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
         o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
         o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
@@ -2968,11 +2825,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 #pragma unroll
     for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
     int key = -1;
-#ifdef MR_EXP_NOHALF2
-    if (false) {  // experiment build: no raster / projection backward
-#else
     if (f >= 0) {
-#endif
       const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
       const float4 a3 = lrec[wave][3][lane];
       const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2983,7 +2836,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
       const float b[3] = {a2.w, a3.x, a3.y};
       const float gt3[3] = {a3.z, a3.w, a4.x};
       float gfv[3][3];
-      BACC(4);
       const bool clipped = CLIP && (r.flags & FR_CLIP) != 0;
       const float pxf = col_ndc(px, P.H, P.W), pyf = row_ndc(py, P.H, P.W);
       float gbr[3] = {gb[0], gb[1], gb[2]};
@@ -3003,31 +2855,14 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         }
       }
     }
-    BACC(5);
     nt_prev = seg_stage<ACC>(key, row, lrow[wave], lkey[wave]);
     rt_prev = rt_partial(gR, gT, lane);
     s_prev = s;
-    BACC(6);
-#ifdef MR_PROF
-    ++nit;
-#endif
   }
   if (nt_prev >= 0) {
     seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
     if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
   }
-#ifdef MR_PROF
-  {
-    const int gw = 32768 + blockIdx.x * 4 + wave;  // k_tile_raster's stamps use waves < 32768
-    if (g_prof && lane == 0) {
-      unsigned long long* o = g_prof + (size_t)gw * 8;
-      for (int i = 0; i < 6; ++i) o[i] = pacc[i];
-      o[6] = nit;
-      o[7] = __builtin_amdgcn_s_memtime() - tstart;
-    }
-  }
-#endif
-#undef BACC
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
@@ -3690,11 +3525,6 @@ extern "C" {
 
 const char* mr_last_error(void) { return g_err; }
 
-#ifdef MR_PROF
-int32_t mr_debug_set_prof(void* buf) {
-  return hipMemcpyToSymbol(HIP_SYMBOL(g_prof), &buf, sizeof(buf)) == hipSuccess ? MR_OK : MR_ELAUNCH;
-}
-#endif
 
 int32_t mr_version(void) { return 3; }
 
@@ -3880,11 +3710,7 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
   FwdParams P = make_fwd(s, g, w, N, first, 0, Fb);
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.view_count = count;
-#ifdef MR_EXP_FV_NOLDS
-  const bool lds = false;
-#else
   const bool lds = g.T <= MR_LDS_HIST;
-#endif
   const size_t shm = lds ? sizeof(int) * (size_t)g.T : 0;
   SP.NF = Fb;
   if (vpath) {
@@ -4004,13 +3830,8 @@ int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const 
   P.cull = s->cull_backfaces; P.clipz = s->clip_z != 0; P.zc = s->z_clip_value;
   P.blur = s->blur_radius; P.bbox_pad = sqrtf(s->blur_radius);
   P.fv = fv; P.p2f = p2f; P.gz = gz; P.gb = gb; P.gd = gd; P.gfv = gfv;
-#ifndef MR_RASTER_BWD_TILES
   const int64_t nslots = N * (int64_t)s->H * s->W * s->faces_per_pixel;
   MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd_slots<<<(unsigned)((nslots + 255) / 256), 256, 0, st>>>(P, nslots)));
-#else
-  dim3 grid(P.NBX * ceil_div(s->H, MR_BT), (unsigned)N);
-  MR_TIMED(KID_RASTER_BWD, st, (k_raster_bwd<<<grid, 256, 0, st>>>(P)));
-#endif
   MR_CHECK_LAUNCH("k_raster_bwd");
   return MR_OK;
 }

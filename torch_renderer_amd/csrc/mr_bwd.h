@@ -1,0 +1,594 @@
+// mi355r — Backward: the modular rasterizer backward (k_raster_bwd_slots) and the fused render
+// backward (k_bwd_fused) with its segmented per-face reduction and per-slot R/T partials.
+// Part of the single translation unit mr_raster.hip (included there, in this order).
+#pragma once
+
+// ---------------------------------------------------------------------------
+// 3. backward
+// ---------------------------------------------------------------------------
+// LDS hash: face key -> slot holding ACC partial sums.
+template <int ACC>
+struct LdsAcc {
+  int keys[MR_HT];
+  float acc[MR_HT * ACC];
+};
+
+MR_DEV int ht_slot(int* keys, int key) {
+  unsigned h = ((unsigned)key * 2654435761u) >> (32 - 9);
+#pragma unroll 1
+  for (int probe = 0; probe < 16; ++probe) {
+    const int k = keys[h];
+    if (k == key) return (int)h;
+    if (k == -1) {
+      const int old = atomicCAS(&keys[h], -1, key);
+      if (old == -1 || old == key) return (int)h;
+    }
+    h = (h + 1) & (MR_HT - 1);
+  }
+  return -1;
+}
+
+template <int ACC>
+MR_DEV void acc_add(LdsAcc<ACC>& L, float* __restrict__ gdst, int key, const float* v) {
+  const int s = ht_slot(L.keys, key);
+  if (s >= 0) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i)
+      if (v[i] != 0.0f) atomicAdd(&L.acc[s * ACC + i], v[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i)
+      if (v[i] != 0.0f) atomicAdd(&gdst[(int64_t)key * ACC + i], v[i]);
+  }
+}
+
+template <int ACC>
+MR_DEV void acc_init(LdsAcc<ACC>& L) {
+  for (int i = threadIdx.x; i < MR_HT; i += blockDim.x) L.keys[i] = -1;
+  for (int i = threadIdx.x; i < MR_HT * ACC; i += blockDim.x) L.acc[i] = 0.0f;
+}
+
+template <int ACC>
+MR_DEV void acc_flush(LdsAcc<ACC>& L, float* __restrict__ gdst) {
+  for (int i = threadIdx.x; i < MR_HT * ACC; i += blockDim.x) {
+    const int s = i / ACC;
+    const int k = L.keys[s];
+    const float v = L.acc[i];
+    if (k >= 0 && v != 0.0f) atomicAdd(&gdst[(int64_t)k * ACC + (i - s * ACC)], v);
+  }
+}
+
+// Modular backward (PyTorch3D _C.rasterize_meshes_backward), every one of the K faces per pixel.
+struct RasterBwdParams {
+  int N, H, W, NBX, K;
+  int persp, clipb;
+  int cull, clipz;
+  float zc, blur, bbox_pad;
+  const float* fv;
+  const int64_t* p2f;
+  const float* gz;
+  const float* gb;
+  const float* gd;
+  float* gfv;
+};
+
+// One stored fragment (pixel px, py; slot pix; packed face f) of the modular raster backward:
+// the 9 face_verts gradients of face f in g.
+MR_DEV void raster_bwd_fragment(const RasterBwdParams& P, int px, int py, int64_t pix, int64_t f, float (&g)[3][3]) {
+  FaceRec r;
+  const float* v = P.fv + 9 * f;
+  r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
+  r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
+  r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
+  r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
+  // an upstream gradient PyTorch passed as None arrives as NULL: zero
+  const float gb[3] = {P.gb ? P.gb[3 * pix] : 0.0f, P.gb ? P.gb[3 * pix + 1] : 0.0f, P.gb ? P.gb[3 * pix + 2] : 0.0f};
+  const float gzp = P.gz ? P.gz[pix] : 0.0f, gdp = P.gd ? P.gd[pix] : 0.0f;
+  const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
+  int ci = 0;
+  const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};
+  const int nb = P.clipz ? clip_class(vv, P.zc, ci) : 0;
+  if (nb == 1 || nb == 2) {
+    // the face was split at the near plane: rebuild its sub-triangle(s) exactly as the forward
+    // binning did, pick the one that produced this fragment (the forward's pair rule), and chain
+    for (int c = 0; c < 3; ++c)
+      for (int q = 0; q < 3; ++q) g[c][q] = 0.0f;
+    float sv[3][3];
+    ClipRec cr0, cr1;
+    clip_sub(vv, nb, ci, 0, P.zc, P.persp != 0, sv, cr0);
+    FaceRec r0 = make_rec_core(P.cull, P.persp, 0u, sv);
+    int use = 0;
+    FaceRec r1;
+    if (nb == 1) {
+      clip_sub(vv, nb, ci, 1, P.zc, P.persp != 0, sv, cr1);
+      r1 = make_rec_core(P.cull, P.persp, 0u, sv);
+      FragEval e0, e1;
+      const bool k0 = (r0.flags & FR_VALID) && eval_face(r0, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e0);
+      const bool k1 = (r1.flags & FR_VALID) && eval_face(r1, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, e1);
+      use = (k0 && k1) ? (fabsf(e1.sdist) < fabsf(e0.sdist) ? 1 : 0) : (k1 ? 1 : 0);
+    }
+    const FaceRec& rs = use ? r1 : r0;
+    const ClipRec& cr = use ? cr1 : cr0;
+    FragEval es;
+    eval_face(rs, xf, yf, P.bbox_pad, P.blur, P.persp, P.clipb, es);
+    const float bs[3] = {es.b0, es.b1, es.b2};
+    float gs[3], gsub[3][3];
+    clip_gb_sub(cr, gb, gs);
+    raster_bwd_pixel<false>(rs, xf, yf, P.persp, P.clipb, gzp, gs, gdp, gsub);
+    clip_bwd_chain(cr, vv, P.zc, P.persp != 0, bs, gb, gsub, g);
+  } else {
+    raster_bwd_pixel<false>(r, xf, yf, P.persp, P.clipb, gzp, gb, gdp, g);
+  }
+}
+
+// One thread per stored fragment slot (n, y, x, k) in memory order: the loads of pix_to_face and
+// of the upstream gradients are coalesced (one lane per pixel walking its K slots strided them by
+// K elements), and a block whose 256 slots hold no fragment (most of them when K is large: the
+// K-nearest lists are short) returns before touching its LDS accumulator.
+__global__ void __launch_bounds__(256) k_raster_bwd_slots(RasterBwdParams P, int64_t nslots) {
+  __shared__ LdsAcc<9> L;
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t f = pix < nslots ? P.p2f[pix] : -1;
+  if (!__syncthreads_or(f >= 0)) return;
+  acc_init(L);
+  __syncthreads();
+  if (f >= 0) {
+    const int64_t p = pix / P.K;
+    const int64_t hw = (int64_t)P.H * P.W;
+    const int rem = (int)(p % hw);
+    const int py = rem / P.W, px = rem - py * P.W;
+    float g[3][3];
+    raster_bwd_fragment(P, px, py, pix, f, g);
+    acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
+  }
+  __syncthreads();
+  acc_flush(L, P.gfv);
+}
+
+__global__ void __launch_bounds__(256) k_raster_bwd(RasterBwdParams P) {
+  __shared__ LdsAcc<9> L;
+  acc_init(L);
+  __syncthreads();
+  const int n = blockIdx.y, bt = blockIdx.x;
+  const int btx = bt % P.NBX, bty = bt / P.NBX;
+  const int px = btx * MR_BT + (threadIdx.x & 31);
+  for (int k = 0; k < 4; ++k) {
+    const int py = bty * MR_BT + (threadIdx.x >> 5) + 8 * k;
+    if (px >= P.W || py >= P.H) continue;
+    const int64_t pix0 = (((int64_t)n * P.H + py) * P.W + px) * P.K;
+    for (int kk = 0; kk < P.K; ++kk) {
+      const int64_t pix = pix0 + kk;
+      const int64_t f = P.p2f[pix];
+      if (f < 0) continue;
+      float g[3][3];
+      raster_bwd_fragment(P, px, py, pix, f, g);
+      acc_add<9>(L, P.gfv, (int)f, &g[0][0]);
+    }
+  }
+  __syncthreads();
+  acc_flush(L, P.gfv);
+}
+
+// DPP lane moves (GFX9 / CDNA): no LDS round trip (a __shfl is a ds_bpermute_b32 with LDS
+// latency; the backward issued ~180 of them per tile in dependent chains).
+MR_DEV int dpp_wave_shr1(int v, int old) { return __builtin_amdgcn_update_dpp(old, v, 0x138, 0xf, 0xf, false); }  // wave_shr:1
+MR_DEV int dpp_wave_shl1(int v, int old) { return __builtin_amdgcn_update_dpp(old, v, 0x130, 0xf, 0xf, false); }  // wave_shl:1
+template <int CTRL, int ROW_MASK>
+MR_DEV float dppf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+// Segmented inclusive sum over lanes: d = distance from the lane to the first lane of its run.
+// row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry a run across rows
+// (the structure of wave_incl_sum, each step gated on the run reaching that far back).
+// Each step is written as select(gate, x + shifted, x) so the DPP move folds into the add
+// (v_add_f32 with a DPP operand + v_cndmask: two VALU ops per step instead of three).
+MR_DEV float seg_incl_sum(float x, int d, int lane) {
+  const int r = lane & 15;
+  float s;
+  s = x + dppf<0x111, 0xf>(x); x = (d >= 1) ? s : x;
+  s = x + dppf<0x112, 0xf>(x); x = (d >= 2) ? s : x;
+  s = x + dppf<0x114, 0xf>(x); x = (d >= 4) ? s : x;
+  s = x + dppf<0x118, 0xf>(x); x = (d >= 8) ? s : x;
+  s = x + dppf<0x142, 0xa>(x); x = (d > r) ? s : x;            // rows 1, 3 <- lanes 15, 47
+  s = x + dppf<0x143, 0xc>(x); x = (d > lane - 32) ? s : x;    // rows 2, 3 <- lane 31
+  return x;
+}
+// Full-wave sum, result in lane 63.
+MR_DEV float wave_sum_f_dpp(float x) {
+  x += dppf<0x111, 0xf>(x);
+  x += dppf<0x112, 0xf>(x);
+  x += dppf<0x114, 0xf>(x);
+  x += dppf<0x118, 0xf>(x);
+  x += dppf<0x142, 0xa>(x);
+  x += dppf<0x143, 0xc>(x);
+  return x;
+}
+
+// Sum ACC-float rows over runs of equal `key` in lane order (segmented DPP scan; the
+// covered-pixel list is row-major, so a face's pixels along a row are consecutive lanes).
+// seg_stage leaves the run totals in the wave's LDS rows and returns their count; seg_flush
+// adds them with float atomics whose lanes cover consecutive components of consecutive runs
+// (contiguous 4*ACC-byte rows per run instead of one scattered dword per lane and instruction).
+// Lanes with key < 0 carry zero rows. Uniform calls (full EXEC). (Measured alternative: one LDS
+// row per distinct face filled with LDS float atomics — slower, 124 vs 102 us, the same-address
+// LDS atomics serialise.)
+template <int ACC>
+MR_DEV int seg_stage(int key, float (&v)[ACC], float* lrow, int* lkey) {
+  const int lane = threadIdx.x & 63;
+  const int prev = dpp_wave_shr1(key, -2);  // lane 0: no predecessor
+  const bool head = lane == 0 || key != prev;
+  const int d = lane - wave_incl_max(head ? lane : 0);  // distance to the run's first lane
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) v[i] = seg_incl_sum(v[i], d, lane);
+  const int next = dpp_wave_shl1(key, -2);  // lane 63: no successor
+  const bool emit = (lane == 63 || key != next) && key >= 0;
+  const unsigned long long m = __ballot(emit);
+  if (emit) {
+    const int slot = __popcll(m & ((1ull << lane) - 1ull));
+    lkey[slot] = key;
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
+  }
+  wave_lds_sync();
+  return __popcll(m);
+}
+// Straight-line (unrolled, uniform skips): as a loop, the waitcnt pass drains every pending load
+// (s_waitcnt vmcnt(0)) in the loop preheader, i.e. waits on the prefetches issued just before.
+template <int ACC>
+MR_DEV void seg_flush(int nt, float* __restrict__ dst, const float* lrow, const int* lkey) {
+  // lane id through an opaque copy: the unrolled blocks' row/column indices are invariant in the
+  // caller's slot loop, and hoisted out of it they would stay live across the whole loop
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int tot = nt * ACC;  // <= 64 * ACC
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) {
+    if (64 * i < tot) {
+      const int j = 64 * i + lane;
+      if (j < tot) {
+        const int r = j / ACC;
+        const float x = lrow[j];
+        if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one row block at a time (no hoisting: register peak)
+  }
+  wave_lds_sync();
+}
+template <int ACC>
+MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float* lrow, int* lkey) {
+  seg_flush<ACC>(seg_stage<ACC>(key, v, lrow, lkey), dst, lrow, lkey);
+}
+
+// The slot's 12 R/T partial sums (wave-wide DPP sums, fixed order: deterministic), lane i
+// holding sum i (lanes 0..11); stored later by one store instruction. Uniform call (full EXEC).
+MR_DEV float rt_partial(const float (&gR)[9], const float (&gT)[3], int lane) {
+  float o = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    const float t = wave_sum_f_dpp(i < 9 ? gR[i] : gT[i - 9]);
+    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
+    o = lane == i ? s : o;
+  }
+  return o;
+}
+
+// Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
+// tile pixel the winning face record or -1; the pixel is implied by slot and lane). Per covered
+// pixel: half 1 recomputes fragment + shading and differentiates the blends / Phong / texture ->
+// a 20-float record (grads of z, signed dist, barycentrics, interpolated point / normal / texel,
+// and the barycentrics) handed to half 2 through the wave's LDS; half 2 runs the rasterizer
+// backward (edge functions, perspective correction, distances; the near-plane clip's chain rule
+// for split faces) + projection backward -> per-face rows summed over runs of equal faces
+// (seg_scatter), and the slot's R/T partial sums. (Measured: the same two halves as two kernels
+// with the record in HBM took 123 us against 102 for the fused kernel.)
+// Waves stride over XCD-contiguous slot ranges (one 8x8 tile, one view each).
+#define MR_BWD_REC 5  // float4s per pixel record
+struct RenderBwdParams {
+  int N, H, W, TX, T;
+  float blur, bbox_pad;
+  int persp, clipb;
+  const FaceRec* recs;
+  const int* ctr;
+  const int* sface;
+  const int* stile;
+  const int* vslot;
+  const float* gD;
+  const float* gS;
+  const float* gRGB;
+  int rgb_ch;
+  int sil_rgba;  // gS is the (N,H,W,4) gradient of an RGBA silhouette (MR_OUT_SIL_RGBA)
+  ShadeParams S;
+  const ShadeRec* srec;
+  int64_t F;     // faces of the shared mesh: record id rid = n*F + face
+  int64_t NF;    // N * F: the second triangle of a split face is record NF + rid
+  const ClipRec* crec;
+  float zc;      // z_clip_value (clipped records only)
+  const ViewRec* views;
+  float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
+  float* rt_part;  // (slots, 12) per-slot R/T partial sums
+  const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
+};
+
+MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& px, int& py) {
+  n = gt / P.T;
+  const int t = gt - n * P.T;
+  const int ty = t / P.TX, tx = t - ty * P.TX;
+  px = tx * MR_TS + (lane & 7);
+  py = ty * MR_TS + (lane >> 3);
+}
+
+// Both halves in one kernel (the default): the shade backward's 20-float record goes through
+// the wave's LDS instead of HBM (80 B written + 80 B read per covered pixel), and the slot,
+// winners and face record are fetched once. Peak VGPRs stay those of the larger half: the
+// LDS hand-off ends the first half's live ranges.
+// Face record and upstream gradients (depth, silhouette, RGB) of one slot pixel. The loads are
+// unconditional (record 0 / a zero buffer when the lane has no fragment or an output has no
+// gradient; such values are never used): written as guarded loads they become branches whose
+// phi copies wait on the load right away, which defeats the prefetch.
+__device__ float g_zero4[4];
+MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
+                             float4& fr) {
+  int n, px, py;
+  slot_pixel(P, gt, lane, n, px, py);
+  const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
+  r = load_rec(P.recs, f < 0 ? 0 : f);
+  fr = P.frec[(int64_t)slot * 64 + lane];
+  const float* pD = P.gD ? P.gD + pix : g_zero4;
+  const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
+  const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
+  g[0] = *pD;
+  g[1] = *pS;
+  g[2] = pC[0];
+  g[3] = pC[1];
+  g[4] = pC[2];
+}
+
+// Near-plane sub-triangle (record f, flag FR_CLIP): gfv holds the raster backward w.r.t. the
+// sub-triangle's corners (run with C g_orig); map it to the ORIGINAL face's projected corners
+// through the clip's chain rule (sub-corners and the conversion weights), the original corners
+// re-projected from the world corners. g_orig: gradient w.r.t. the original-face barycentrics.
+MR_DEV void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f, const ViewRec& V, const float X[3][3],
+                          float px, float py, const float g_orig[3], float gfv[3][3]) {
+  const ClipRec cr = P.crec[f];
+  FragEval e;
+  eval_face(r, px, py, P.bbox_pad, P.blur, P.persp, P.clipb, e);
+  const float bs[3] = {e.b0, e.b1, e.b2};
+  float v[3][3], gsub[3][3];
+  for (int c = 0; c < 3; ++c) {
+    float vx, vy, vz, nx, ny;
+    project_point(V, X[c], vx, vy, vz, nx, ny);
+    v[c][0] = nx;
+    v[c][1] = ny;
+    v[c][2] = vz;
+    for (int q = 0; q < 3; ++q) {
+      gsub[c][q] = gfv[c][q];
+      gfv[c][q] = 0.0f;
+    }
+  }
+  clip_bwd_chain(cr, v, P.zc, P.persp != 0, bs, g_orig, gsub, gfv);
+}
+
+// Alpha-channel upstream gradient (RGBA outputs only; the drop-in frame has rgb_ch = 3).
+MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
+  int n, px, py;
+  slot_pixel(P, gt, lane, n, px, py);
+  const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
+  return P.gRGB[pix * P.rgb_ch + 3];
+}
+
+// CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
+// instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
+#define MR_BWD_ATTR
+// The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
+// through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
+// loop, overflow the SGPR file and are spilled into VGPR lanes (one v_readlane per use; k_bwd_fused had
+// 70 spilled SGPRs and ~400 readlanes per slot iteration). Re-read per iteration, each is a scalar
+// load from the (cached) kernarg segment, live only where it is used.
+template <typename T>
+MR_DEV const T& kernarg_params() {
+  typedef const char __attribute__((address_space(4))) * cptr;
+  cptr p = (cptr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const T*)(const char*)p;
+}
+
+template <int ACC, bool CLIP>
+__global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
+  const RenderBwdParams& P = P0;
+  __shared__ float lrow[4][64 * ACC];
+  __shared__ int lkey[4][64];
+  __shared__ float4 lrec[4][MR_BWD_REC][64];
+  const bool lut = stage_tex_lut(P.S);  // the u8 texture table in LDS
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
+  int s, G, send;
+  xcd_slot_range(nslots, wave, s, G, send);
+  // Three-deep software pipeline (the kernel runs at 2 waves/SIMD, so a wave must hide its own
+  // latency): while slot s is processed, the face record and upstream gradients of slot s + G
+  // and the tile id and winner of slot s + 2G are in flight.
+  // gt_* are per-lane copies of the (uniform) tile id, made uniform where they are consumed
+  // Prefetches past the wave's last slot read a clamped (valid) slot and are never consumed.
+  const int lz = lane_zero();
+  const int slast = max(nslots - 1, 0);
+  int sc = min(s, slast);
+  int sl_c = sc;  // slot of gt_c / f_c (clamped)
+  int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
+  sc = min(s + G, slast);
+  int sl_n = sc;
+  int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
+  FaceRec r_c;
+  float g_c[5];
+  float4 fr_c;
+  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
+  int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
+  float rt_prev = 0.0f;
+  for (; s < send; s += G) {
+    const RenderBwdParams& P = kernarg_params<RenderBwdParams>();  // see kernarg_params
+    const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c;
+    const FaceRec r = r_c;
+    const float4 frag = fr_c;
+    float gin[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
+    gt_c = gt_n;
+    f_c = f_n;
+    sl_c = sl_n;
+    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
+    sc = min(s + 2 * G, slast);
+    sl_n = sc;
+    gt_n = P.stile[sc + lz];
+    f_n = P.sface[(int64_t)sc * 64 + lane];
+    int n, px, py;
+    slot_pixel(P, gt, lane, n, px, py);
+    // ---- half 1: blends / Phong / texture backward -> lrec
+    if (f >= 0) {
+      PixGeom Gm;
+      load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
+      const float gD = gin[0], gS = gin[1];
+      float gC[3] = {gin[2], gin[3], gin[4]};
+      const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
+      FragEval e;
+      float4 o[MR_BWD_REC];
+      // the forward's fragment (k_shade<1> wrote the winner's barycentrics, original-face ones for a
+      // near-plane sub-triangle, and signed distance); the depth from the record's corners in
+      // eval_face's operation order, or, for a sub-triangle (whose corners are not the original
+      // face's), from eval_face itself
+      e.b0 = frag.x;
+      e.b1 = frag.y;
+      e.b2 = frag.z;
+      e.sdist = frag.w;
+      e.pz = (e.b0 * r.z0 + e.b1 * r.z1) + e.b2 * r.z2;
+      if (CLIP && (r.flags & FR_CLIP)) {
+        FragEval es;
+        eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur, P.persp, P.clipb, es);
+        e.pz = es.pz;
+      }
+      {
+        ShadeOut so;
+        ShadeCache C;
+        shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C, lut);
+        ShadeGrad SG;
+        shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
+        o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
+        o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
+        o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
+        o[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
+        o[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][k][lane] = o[k];
+    }
+    wave_lds_sync();
+    __builtin_amdgcn_sched_barrier(0);  // keep half 2's loads out of half 1's register peak
+    // ---- half 2: raster + projection backward, per-face runs, R/T partials
+    const ViewRec V = P.views[n];
+    // world corners (first 36 B of the ShadeRec), issued BEFORE the previous slot's deferred
+    // atomics: vmcnt retires in issue order, so a load issued after them would wait the
+    // atomics' ~3k-cycle completion; issued before, its wait is a precise count
+    // (unconditional: face 0 for lanes without a fragment, see bwd_slot_inputs)
+    const int face = f >= 0 ? (int)(rec_orig(f, P.NF) - n * P.F) : 0;
+    const float4* x4 = (const float4*)(P.srec + face);
+    const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
+    __builtin_amdgcn_sched_barrier(0);
+    // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
+    // half 1 and the corners above are already in flight or consumed
+    if (nt_prev >= 0) {
+      seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+      if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float gR[9], gT[3];
+#pragma unroll
+    for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
+    float row[ACC];
+#pragma unroll
+    for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
+    int key = -1;
+    if (f >= 0) {
+      const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
+      const float4 a3 = lrec[wave][3][lane];
+      const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+      const float gb[3] = {a0.z, a0.w, a1.x};
+      const float gP[3] = {a1.y, a1.z, a1.w};
+      const float gNn[3] = {a2.x, a2.y, a2.z};
+      const float b[3] = {a2.w, a3.x, a3.y};
+      const float gt3[3] = {a3.z, a3.w, a4.x};
+      float gfv[3][3];
+      const bool clipped = CLIP && (r.flags & FR_CLIP) != 0;
+      const float pxf = col_ndc(px, P.H, P.W), pyf = row_ndc(py, P.H, P.W);
+      float gbr[3] = {gb[0], gb[1], gb[2]};
+      if (clipped) clip_gb_sub(P.crec[f], gb, gbr);  // near-plane sub-triangle: C g_orig
+      raster_bwd_pixel<true>(r, pxf, pyf, P.persp, P.clipb, a0.x, gbr, a0.y, gfv);
+      if (__builtin_expect(clipped, 0)) clipped_chain(P, r, f, V, X, pxf, pyf, gb, gfv);
+      key = face;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float gX[3];
+        project_bwd(V, X[c], gfv[c], gX, gR, gT);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          row[3 * c + k] = b[c] * gP[k] + gX[k];
+          row[9 + 3 * c + k] = b[c] * gNn[k];
+          if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
+        }
+      }
+    }
+    nt_prev = seg_stage<ACC>(key, row, lrow[wave], lkey[wave]);
+    rt_prev = rt_partial(gR, gT, lane);
+    s_prev = s;
+  }
+  if (nt_prev >= 0) {
+    seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+    if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
+  }
+}
+
+// grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
+// out (N,12) PyTorch3D-frame R/T grads, or (gRcv, gtcv) non-null: the same grads written
+// straight in the OpenCV frame (k_view_grads_to_opencv's chain rule, saving its launch).
+MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N,
+                           float* __restrict__ out, float* __restrict__ gRcv, float* __restrict__ gtcv, int n) {
+  __shared__ float sm[12][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int s0 = vslot[n], ns = vslot[N + n];
+  // each thread sums whole 48-B partial rows (three 16-B loads in flight together instead of 12
+  // dependent passes over the rows); per component the order is the same as a per-component loop
+  float acc[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
+  for (int t = threadIdx.x; t < ns; t += 256) {
+    const float4* q = (const float4*)(part + ((int64_t)s0 + t) * 12);
+    const float4 a = q[0], b = q[1], c = q[2];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
+    acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) {
+    for (int o = 32; o > 0; o >>= 1) acc[i] += __shfl_xor(acc[i], o, 64);
+    if (lane == 0) sm[i][wave] = acc[i];
+  }
+  __syncthreads();
+  const int i = threadIdx.x;
+  if (i >= 12) return;
+  const float v = ((sm[i][0] + sm[i][1]) + sm[i][2]) + sm[i][3];
+  if (!gRcv) {
+    out[n * 12 + i] = v;
+  } else if (i < 9) {  // dL/dR_cv[b][a] = dL/dR_p3d[a][b] * s[b]
+    const int a = i / 3, b = i - 3 * a;
+    gRcv[(int64_t)n * 9 + 3 * b + a] = b < 2 ? -v : v;
+  } else {
+    gtcv[(int64_t)n * 3 + (i - 9)] = i < 11 ? -v : v;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
+                                                   int N, float* __restrict__ out, float* __restrict__ gRcv,
+                                                   float* __restrict__ gtcv) {
+  rt_reduce_view(part, vslot, N, out, gRcv, gtcv, blockIdx.x);
+}

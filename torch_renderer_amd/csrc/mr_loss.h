@@ -1,0 +1,120 @@
+// mi355r — Fused pose-optimiser loss (forward partial sums, final reduction, backward).
+// Part of the single translation unit mr_raster.hip (included there, in this order).
+#pragma once
+
+// ---------------------------------------------------------------------------
+// Fused pose-optimiser loss (camera_pose_optimizer.py:257-276 Model.calc_loss):
+//   sil_loss   = L1Loss()(silhouette, mask)               mean over all pixels
+//   hloss      = HuberLoss(delta)(depth[mask], depth_ref[mask])   mean over the masked pixels
+//   color_loss = MSELoss()(color, rgb_ref)                mean over all pixels x 3
+//   total      = sil_loss + hloss + w_color * color_loss
+// Forward: per-block partial sums (fixed-order wave / block reductions), then one block sums the
+// partials in block order (deterministic). Backward: the elementwise gradients of the three
+// means, scaled by the device scalar dL/dtotal (no host read).
+// ---------------------------------------------------------------------------
+struct PoseLossParams {
+  const float* depth;
+  const float* sil;
+  const float* rgb;
+  int64_t rgb_stride;  // floats between consecutive pixels' colours (3, or 4 for an RGBA view)
+  const uint8_t* mask;
+  const float* depth_ref;
+  const float* rgb_ref;  // (npix, 3)
+  int64_t npix;
+  float delta, w_color;
+};
+#define MR_LOSS_BLOCKS 512
+
+MR_DEV float huber_val(float d, float delta) {
+  const float a = fabsf(d);
+  return a < delta ? 0.5f * d * d : delta * (a - 0.5f * delta);
+}
+MR_DEV float huber_grad(float d, float delta) {
+  return fabsf(d) < delta ? d : (d > 0.0f ? delta : (d < 0.0f ? -delta : 0.0f));
+}
+MR_DEV float block_sum_256(float v, float* sm) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sm[threadIdx.x >> 6] = v;
+  __syncthreads();
+  const float t = ((sm[0] + sm[1]) + sm[2]) + sm[3];
+  __syncthreads();
+  return t;
+}
+
+__global__ void __launch_bounds__(256) k_pose_loss_partial(PoseLossParams P, float* __restrict__ part,
+                                                           int* __restrict__ pcnt) {
+  __shared__ float sm[4];
+  float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
+  int cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
+    const bool m = P.mask[i] != 0;
+    s_l1 += fabsf(P.sil[i] - (m ? 1.0f : 0.0f));
+    if (m) {
+      s_h += huber_val(P.depth[i] - P.depth_ref[i], P.delta);
+      ++cnt;
+    }
+    const float* c = P.rgb + i * P.rgb_stride;
+    const float* r = P.rgb_ref + 3 * i;
+    const float d0 = c[0] - r[0], d1 = c[1] - r[1], d2 = c[2] - r[2];
+    s_mse += (d0 * d0 + d1 * d1) + d2 * d2;
+  }
+  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), c = block_sum_256(s_mse, sm);
+  const float n = block_sum_256((float)cnt, sm);  // exact: <= 2^24 pixels per block
+  if (threadIdx.x == 0) {
+    part[3 * blockIdx.x] = a;
+    part[3 * blockIdx.x + 1] = b;
+    part[3 * blockIdx.x + 2] = c;
+    pcnt[blockIdx.x] = (int)n;
+  }
+}
+
+// out: {total, sil_loss, hloss, color_loss}; count: the number of masked pixels (backward)
+__global__ void __launch_bounds__(256) k_pose_loss_final(PoseLossParams P, const float* __restrict__ part,
+                                                         const int* __restrict__ pcnt, int nb, float* __restrict__ out,
+                                                         int64_t* __restrict__ count) {
+  __shared__ float sm[4];
+  float a = 0.0f, b = 0.0f, c = 0.0f;
+  long long n = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) {
+    a += part[3 * i];
+    b += part[3 * i + 1];
+    c += part[3 * i + 2];
+    n += pcnt[i];
+  }
+  a = block_sum_256(a, sm);
+  b = block_sum_256(b, sm);
+  c = block_sum_256(c, sm);
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  __shared__ long long sn[4];
+  if ((threadIdx.x & 63) == 0) sn[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const long long tn = ((sn[0] + sn[1]) + sn[2]) + sn[3];
+    const float l1 = a / (float)P.npix;
+    const float hl = b / (float)tn;  // an empty mask gives NaN, as torch's mean of nothing
+    const float ms = c / (float)(3 * P.npix);
+    out[0] = (l1 + hl) + P.w_color * ms;
+    out[1] = l1;
+    out[2] = hl;
+    out[3] = ms;
+    *count = tn;
+  }
+}
+
+__global__ void __launch_bounds__(256) k_pose_loss_bwd(PoseLossParams P, const float* __restrict__ g_total,
+                                                       const int64_t* __restrict__ count, float* __restrict__ g_depth,
+                                                       float* __restrict__ g_sil, float* __restrict__ g_rgb) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= P.npix) return;
+  const float g = *g_total;
+  const bool m = P.mask[i] != 0;
+  const float e = P.sil[i] - (m ? 1.0f : 0.0f);
+  g_sil[i] = g * ((e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f)) / (float)P.npix);
+  g_depth[i] = m ? g * (huber_grad(P.depth[i] - P.depth_ref[i], P.delta) / (float)*count) : 0.0f;
+  const float s = g * P.w_color * (2.0f / (float)(3 * P.npix));
+  const float* c = P.rgb + i * P.rgb_stride;
+  const float* r = P.rgb_ref + 3 * i;
+  g_rgb[3 * i] = s * (c[0] - r[0]);
+  g_rgb[3 * i + 1] = s * (c[1] - r[1]);
+  g_rgb[3 * i + 2] = s * (c[2] - r[2]);
+}

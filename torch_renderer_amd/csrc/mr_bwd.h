@@ -403,6 +403,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
+  if (nslots <= 0) return;  // no covered tile: the prefetches below would read unwritten winners
   int s, G, send;
   xcd_slot_range(nslots, wave, s, G, send);
   // Three-deep software pipeline (the kernel runs at 2 waves/SIMD, so a wave must hide its own

@@ -126,7 +126,7 @@ extern "C++" {
 #define MR_BG_CPW_RENDER 8  // 5 KB chunks (depth, silhouette, RGB)
 #endif
 #ifndef MR_BG_CPW_FRAG
-#define MR_BG_CPW_FRAG 4    // 7 KB chunks (PyTorch3D fragments)
+#define MR_BG_CPW_FRAG 8    // 7 KB chunks (PyTorch3D fragments; 4 -> 8: fragment pass 166 -> 162 us)
 #endif
 #ifndef MR_VIEW_LDS
 #define MR_VIEW_LDS 98304  // k_bin_view's LDS: the tile histogram + the list stage

@@ -662,6 +662,7 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
+  if (nslots <= 0) return;  // no covered tile: the prefetches below would read unwritten winners
   const int64_t HW = (int64_t)P.H * P.W;
   int s0, G, send;
   xcd_slot_range(nslots, wave, s0, G, send);

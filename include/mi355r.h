@@ -86,7 +86,11 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
        /* with MR_OUT_SIL, mr_render_forward/_backward[_opencv]: the silhouette buffer is (N,H,W,4)
         * RGBA as SoftSilhouetteShader returns it, (1, 1, 1, alpha) per pixel, written by the
         * kernels; its gradient is the (N,H,W,4) gradient of that tensor (channel 3 is read) */
-       MR_OUT_SIL_RGBA = 32 };
+       MR_OUT_SIL_RGBA = 32,
+       /* mr_shade_fragments_* only: every pixel's empty slots (pix_to_face = -1) follow its filled
+        * ones, as mr_rasterize_meshes[_world] (and PyTorch3D's rasterizer) write them; the kernels
+        * then stop at a pixel's first empty slot instead of reading all K (same results) */
+       MR_FRAG_SORTED = 64 };
 
 /* One triangle mesh shared by all N views (Meshes.extend(N)) — or, with
  * view_face_first set, a batch of N distinct meshes (renderer.py:78-80: N OBJ files in one Meshes),

@@ -138,3 +138,25 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
             report(f"{tag} grad vcolors", vcg.grad, vcr.grad, ref64=g64("tex"), sens=spread("tex"))
         else:
             report(f"{tag} grad map", mg.grad, mr.grad, ref64=g64("tex"), sens=spread("tex"))
+    # the same fragments flagged sorted (MR_FRAG_SORTED, as this library's rasterizer marks its own):
+    # the kernels stop at each pixel's first empty slot; outputs and fragment gradients are bitwise the
+    # full-K ones, the mesh gradients (float atomics: summation order varies run to run) within 1e-6
+    leaves = [zg, bgp, dg, vg] + ([vcg] if texture == "vertex" else [mg])
+    first = [x.grad.clone() if x.grad is not None else None for x in leaves]
+    for x in leaves:
+        x.grad = None
+    frags_s = Fragments(p2f.to(DEV), zg, bgp, dg, sorted_slots=True)
+    if shader in ("phong", "hard"):
+        out_s = cls(device=DEV, cameras=cams, lights=lights, materials=mats, blend_params=blend)(frags_s, meshes)
+    else:
+        out_s = SoftSilhouetteShader(blend_params=blend)(frags_s, meshes, cameras=cams)
+    assert torch.equal(out_s, out)
+    (out_s * go.to(DEV)).sum().backward()
+    for i, (a, b) in enumerate(zip(leaves, first)):
+        assert (a.grad is None) == (b is None)
+        if b is None:
+            continue
+        if i < 3:
+            assert torch.equal(a.grad, b)
+        else:
+            report(f"{tag} sorted vs full-K mesh grad {i}", a.grad, b, tol=1e-6)

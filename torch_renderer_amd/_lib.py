@@ -25,6 +25,7 @@ MR_OUT_SIL = 2
 MR_OUT_RGB = 4
 MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
 MR_OUT_SIL_RGBA = 32  # silhouette as (N,H,W,4) RGBA (1, 1, 1, alpha), fused render path
+MR_FRAG_SORTED = 64  # mr_shade_fragments_*: empty slots follow the filled ones (this library's rasterizer)
 MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
 
 

@@ -17,6 +17,7 @@ struct FragShadeParams {
   int64_t F;   // faces of the shared mesh; p2f holds packed ids n*F + f
   int sil;     // 1: sigmoid_alpha_blend (rgb = 1); 0: Phong + softmax_rgb_blend
   int hard;    // 1 (with sil = 0): Phong + hard_rgb_blend (HardPhongShader)
+  int sorted;  // MR_FRAG_SORTED: each pixel's empty slots follow its filled ones (loops stop at the first)
   const int64_t* p2f;
   const float* zbuf;
   const float* bary;
@@ -62,6 +63,7 @@ MR_DEV void frag_sums(const FragShadeParams& P, int64_t pix, int n, FragSums& R,
         R.zmax_raw = zi;
         R.kmax = k;
       }
+      if (!m && P.sorted) break;  // the later masked slots repeat this one's z_inv: none is greater
     }
   }
   R.zmax = smax(R.zmax_raw, 1e-10f);
@@ -73,7 +75,10 @@ MR_DEV void frag_sums(const FragShadeParams& P, int64_t pix, int n, FragSums& R,
   const float isig = P.sil ? S.inv_sigma_sil : S.inv_sigma_rgb;
   for (int k = 0; k < P.K; ++k) {
     const int64_t f = P.p2f[base + k];
-    if (f < 0) continue;  // masked: prob 0, factor 1, weight 0
+    if (f < 0) {  // masked: prob 0, factor 1, weight 0
+      if (P.sorted) break;
+      continue;
+    }
     const float prob = frag_prob(P.dists[base + k], isig);
     const float one_m = 1.0f - prob;
     if (one_m == 0.0f) {
@@ -179,6 +184,7 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
 #pragma unroll 1
   for (int k = 0; k < P.K; ++k) {  // uniform over the wave (seg_scatter inside)
     const int64_t f = act ? P.p2f[base + k] : -1;
+    if (P.sorted && __ballot(f >= 0) == 0ull) break;  // every lane past its last fragment (uniform)
     float row[ACC];
 #pragma unroll
     for (int q = 0; q < ACC; ++q) row[q] = 0.0f;

@@ -811,6 +811,7 @@ static FragShadeParams make_frag(const mr_mesh_t* m, const mr_shade_params_t* sp
   P.F = m->view_face_first ? 0 : m->F;  // face of packed id p: p - n*F (distinct meshes: p itself)
   P.sil = (sp->out_flags & MR_OUT_SIL) ? 1 : 0;
   P.hard = (!P.sil && (sp->out_flags & MR_OUT_HARD)) ? 1 : 0;
+  P.sorted = (sp->out_flags & MR_FRAG_SORTED) ? 1 : 0;
   P.p2f = p2f; P.zbuf = zbuf; P.bary = bary; P.dists = dists;
   P.S = make_shade(m, sp, cc, ncc);
   P.srec = (const ShadeRec*)ws;

@@ -338,6 +338,7 @@ class ShadeConfig:
     hard: bool = False  # hard_rgb_blend (HardPhongShader): fragment-shader path only
     sil_rgba: bool = False  # silhouette as SoftSilhouetteShader's (N,H,W,4) RGBA, written by the kernels
     z_clip: float | None = None  # near clip plane (view z) of FoVPerspectiveCameras: znear / 2
+    frag_sorted: bool = False  # fragment shading: empty slots follow the filled ones (MR_FRAG_SORTED)
 
     def raster_struct(self):
         return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,
@@ -590,6 +591,7 @@ class ShadeFragments(torch.autograd.Function):
         mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol, ranges)
         sp = cfg.shade_struct()
         sp.out_flags = _lib.MR_OUT_SIL if sil else (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0))
+        sp.out_flags |= _lib.MR_FRAG_SORTED if cfg.frag_sorted else 0
         sp.rgb_channels = 4
         if sil:
             sp.light_kind = 1  # the silhouette blend reads no lighting (no vertex normals needed)
@@ -622,6 +624,7 @@ class ShadeFragments(torch.autograd.Function):
         mesh = _mesh_struct(v, f, vptr, vadj, e(vn), tex, e(vcol), ctx.ranges)
         sp = cfg.shade_struct()
         sp.out_flags = (_lib.MR_OUT_RGB | (_lib.MR_OUT_HARD if cfg.hard else 0)) if cfg.want_rgb else _lib.MR_OUT_SIL
+        sp.out_flags |= _lib.MR_FRAG_SORTED if cfg.frag_sorted else 0
         sp.rgb_channels = 4
         if not cfg.want_rgb:
             sp.light_kind = 1

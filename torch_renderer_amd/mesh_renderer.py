@@ -28,7 +28,8 @@ rather than returning different numbers.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+import dataclasses
+from dataclasses import dataclass, field
 
 import torch
 
@@ -186,11 +187,14 @@ class Materials:
 
 @dataclass
 class Fragments:
-    """upstream mesh/rasterizer.py Fragments."""
+    """upstream mesh/rasterizer.py Fragments. ``sorted_slots`` (not upstream's): set by this library's
+    rasterizer, whose empty slots (pix_to_face = -1) follow each pixel's filled ones, so the shaders
+    stop at the first (MR_FRAG_SORTED); Fragments built elsewhere are shaded over all K slots."""
     pix_to_face: torch.Tensor
     zbuf: torch.Tensor
     bary_coords: torch.Tensor
     dists: torch.Tensor
+    sorted_slots: bool = field(default=False, repr=False, compare=False)
 
 
 # --------------------------------------------------------------------------- rasterizer
@@ -262,7 +266,7 @@ class MeshRasterizer(torch.nn.Module):
                 meshes.shared_verts(), R, T, meshes.shared_faces(), intr, R.shape[0], H, W,
                 int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
                 rs.max_faces_per_bin, _z_clip_value(cameras, rs))
-            return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+            return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists, sorted_slots=True)
         fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
         first = meshes.mesh_to_faces_packed_first_idx().to(fv.device)
         count = meshes.num_faces_per_mesh().to(fv.device)
@@ -272,7 +276,7 @@ class MeshRasterizer(torch.nn.Module):
                                                           float(rs.blur_radius), persp, clip,
                                                           bool(rs.cull_backfaces), rs.max_faces_per_bin,
                                                           _z_clip_value(cameras, rs))
-        return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists)
+        return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists, sorted_slots=True)
 
 
 def rasterize(meshes: Meshes, cameras: CamerasBase, raster_settings: RasterizationSettings, **kwargs) -> Fragments:
@@ -327,6 +331,8 @@ def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_
     p2f = fragments.pix_to_face
     N = p2f.shape[0]
     tex = meshes.textures
+    if getattr(fragments, "sorted_slots", False) and not cfg.frag_sorted:
+        cfg = dataclasses.replace(cfg, frag_sorted=True)
     if cfg.want_rgb and tex is None:
         raise ValueError("Meshes does not have textures")  # upstream Meshes.sample_textures
     cc = cam_center.to(p2f.device).float().reshape(-1, 3)

@@ -290,7 +290,9 @@ int32_t mr_shade_fragments_forward(const mr_mesh_t* mesh, const int64_t* pix_to_
 /* Backward from grad_rgba (N,H,W,4): grad_zbuf / grad_dists (N,H,W,K), grad_bary (N,H,W,K,3) (for
  * mr_rasterize_meshes_backward), grad_verts (V,3) of the attribute path (interpolated world positions and
  * vertex normals), grad_vcolors (V,3; tex_kind 1), grad_tex_rgba (Ht,Wt,4) and grad_verts_uvs
- * (num_verts_uvs,2) (tex_kind 2; either may be NULL). All are overwritten. */
+ * (num_verts_uvs,2) (tex_kind 2; either may be NULL). All are overwritten. Gradients that are zero by
+ * construction may be NULL: grad_zbuf and grad_bary with MR_OUT_SIL (the silhouette blend reads only
+ * the distances), grad_zbuf and grad_dists with MR_OUT_HARD (hard_rgb_blend reads neither). */
 size_t mr_shade_fragments_backward_workspace(int64_t V, int64_t F);
 int32_t mr_shade_fragments_backward(const mr_mesh_t* mesh, const float* vnormals_raw, const int64_t* pix_to_face,
                                     const float* zbuf, const float* bary, const float* dists, int64_t N, int32_t H,

@@ -125,10 +125,12 @@ def test_hip_shader_on_oracle_fragments(K, texture, shader):
     report(f"{tag} rgba", out, out_ref, ref64=out64, sens=spl[0])
     (out * go.to(DEV)).sum().backward()
     if shader == "hard":  # no depth / distance dependence
-        assert not zg.grad.any() and not dg.grad.any()
+        assert zg.grad is None and dg.grad is None  # no depth / distance dependence: no gradient tensors
         assert zb.grad is None or not zb.grad.any()
     else:
         report(f"{tag} grad dists", dg.grad, di.grad, ref64=g64("dists"), sens=spread("dists"))
+    if shader == "silhouette":  # the silhouette blend reads only the distances
+        assert zg.grad is None and bgp.grad is None
     if shader in ("phong", "hard"):
         if shader == "phong":
             report(f"{tag} grad zbuf", zg.grad, zb.grad, ref64=g64("zbuf"), sens=spread("zbuf"))

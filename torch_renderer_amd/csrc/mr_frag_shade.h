@@ -221,8 +221,8 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
           }
         }
       }
-      P.g_zbuf[base + k] = 0.0f;
-      P.g_dists[base + k] = 0.0f;
+      if (P.g_zbuf) P.g_zbuf[base + k] = 0.0f;
+      if (P.g_dists) P.g_dists[base + k] = 0.0f;
       P.g_bary[3 * (base + k)] = gb[0];
       P.g_bary[3 * (base + k) + 1] = gb[1];
       P.g_bary[3 * (base + k) + 2] = gb[2];
@@ -276,11 +276,13 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
       float sp_, sq_;  // prob and 1 - prob, each accurate (sigmoid2): the derivative's factor
       sigmoid2((-d) * isig, sp_, sq_);
       const float gd = -((g_prob * (sp_ * sq_)) * isig);
-      P.g_zbuf[base + k] = gz;
+      if (P.g_zbuf) P.g_zbuf[base + k] = gz;
       P.g_dists[base + k] = gd;
-      P.g_bary[3 * (base + k)] = gb[0];
-      P.g_bary[3 * (base + k) + 1] = gb[1];
-      P.g_bary[3 * (base + k) + 2] = gb[2];
+      if (P.g_bary) {
+        P.g_bary[3 * (base + k)] = gb[0];
+        P.g_bary[3 * (base + k) + 1] = gb[1];
+        P.g_bary[3 * (base + k) + 2] = gb[2];
+      }
     }
     // (empty slots: their zero gradients were written by coalesced fills before the launch; written
     // here one lane per pixel they were K-strided 4-B stores, most of this kernel's time at large K)

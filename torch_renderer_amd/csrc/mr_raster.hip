@@ -852,7 +852,9 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
                                     float* g_tex_rgba, float* g_verts_uvs, int64_t num_verts_uvs, void* stream) {
   int rc = check_frags(m, sp, p2f, zbuf, bary, dists, N, H, W, K);
   if (rc) return rc;
-  if (!grad_rgba || !fwd_ws || !bws || !g_zbuf || !g_bary || !g_dists || !g_verts)
+  const bool sil = (sp->out_flags & MR_OUT_SIL) != 0, hard = !sil && (sp->out_flags & MR_OUT_HARD);
+  if (!grad_rgba || !fwd_ws || !bws || !g_verts || (!g_zbuf && !sil && !hard) || (!g_bary && !sil) ||
+      (!g_dists && !hard))
     return set_err(MR_EINVAL, "NULL argument");
   if (bws_bytes < mr_shade_fragments_backward_workspace(m->V, m->F)) return set_err(MR_EWORKSPACE, "backward workspace too small");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
@@ -877,9 +879,9 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   const int grid = ceil_div(N * (int64_t)H * W, 256);
   {  // the fragment gradients of empty slots are zero: cleared here with coalesced fills
     const size_t slots = (size_t)N * H * W * K;
-    if (hipMemsetAsync(g_zbuf, 0, sizeof(float) * slots, st) != hipSuccess ||
-        hipMemsetAsync(g_dists, 0, sizeof(float) * slots, st) != hipSuccess ||
-        hipMemsetAsync(g_bary, 0, sizeof(float) * 3 * slots, st) != hipSuccess)
+    if ((g_zbuf && hipMemsetAsync(g_zbuf, 0, sizeof(float) * slots, st) != hipSuccess) ||
+        (g_dists && hipMemsetAsync(g_dists, 0, sizeof(float) * slots, st) != hipSuccess) ||
+        (g_bary && hipMemsetAsync(g_bary, 0, sizeof(float) * 3 * slots, st) != hipSuccess))
       return set_err(MR_ELAUNCH, "memset failed");
   }
   if (vcol) MR_TIMED(KID_FRAG_SHADE_BWD, st, (k_frag_shade_bwd<27><<<grid, 256, 0, st>>>(P)));

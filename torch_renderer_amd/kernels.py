@@ -630,8 +630,12 @@ class ShadeFragments(torch.autograd.Function):
             sp.light_kind = 1
         bwb = L.mr_shade_fragments_backward_workspace(v.shape[0], f.shape[0])
         bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
-        gz, gd = torch.empty_like(zbuf), torch.empty_like(dists)
-        gb = torch.empty_like(bary)
+        # gradients that are zero by construction stay None (NULL): the silhouette blend reads only the
+        # distances, hard_rgb_blend neither depths nor distances (no GB-sized zero tensors at K = 50)
+        sil, hard = not cfg.want_rgb, cfg.want_rgb and cfg.hard
+        gz = None if (sil or hard) else torch.empty_like(zbuf)
+        gd = None if hard else torch.empty_like(dists)
+        gb = None if sil else torch.empty_like(bary)
         gv = torch.empty_like(v)
         gc = torch.empty_like(vcol) if vcol.numel() else None
         need_map = ctx.tex_kind == 2 and ctx.needs_input_grad[5]

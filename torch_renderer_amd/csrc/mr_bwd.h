@@ -218,8 +218,35 @@ MR_DEV int seg_stage(int key, float (&v)[ACC], float* lrow, int* lkey) {
   const int prev = dpp_wave_shr1(key, -2);  // lane 0: no predecessor
   const bool head = lane == 0 || key != prev;
   const int d = lane - wave_incl_max(head ? lane : 0);  // distance to the run's first lane
+  // seg_incl_sum's six steps, each only when some lane's run reaches that far back (uniform
+  // branches; a skipped step would have kept every lane's value): runs are mostly shorter than a
+  // tile row, so the two cross-row steps and the 8-lane step usually drop out (same sums, bitwise)
+  const int r = lane & 15;
+  float sh;
+  if (__ballot(d >= 1)) {
 #pragma unroll
-  for (int i = 0; i < ACC; ++i) v[i] = seg_incl_sum(v[i], d, lane);
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x111, 0xf>(v[i]); v[i] = d >= 1 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 2)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x112, 0xf>(v[i]); v[i] = d >= 2 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 4)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x114, 0xf>(v[i]); v[i] = d >= 4 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 8)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x118, 0xf>(v[i]); v[i] = d >= 8 ? sh : v[i]; }
+  }
+  if (__ballot(d > r)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x142, 0xa>(v[i]); v[i] = d > r ? sh : v[i]; }
+  }
+  if (__ballot(d > lane - 32)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x143, 0xc>(v[i]); v[i] = d > lane - 32 ? sh : v[i]; }
+  }
   const int next = dpp_wave_shl1(key, -2);  // lane 63: no successor
   const bool emit = (lane == 63 || key != next) && key >= 0;
   const unsigned long long m = __ballot(emit);
@@ -241,16 +268,24 @@ MR_DEV void seg_flush(int nt, float* __restrict__ dst, const float* lrow, const 
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int tot = nt * ACC;  // <= 64 * ACC
+  // element j = 64 i + lane of the flattened rows: row r = j / ACC, column c = j % ACC, advanced by
+  // 64 = q ACC + m per block instead of divided out; 32-bit element offsets (F * ACC < 2^30, checked
+  // on the host) keep the atomics' address in the scalar base + 32-bit vector offset form
+  constexpr int q = 64 / ACC, m = 64 - q * ACC;
+  int r = lane / ACC, c = lane - r * ACC;
 #pragma unroll
   for (int i = 0; i < ACC; ++i) {
     if (64 * i < tot) {
       const int j = 64 * i + lane;
       if (j < tot) {
-        const int r = j / ACC;
         const float x = lrow[j];
-        if (x != 0.0f) atomicAdd(&dst[(int64_t)lkey[r] * ACC + (j - r * ACC)], x);
+        if (x != 0.0f) atomicAdd(dst + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
       }
     }
+    c += m;
+    const bool wrap = c >= ACC;
+    c = wrap ? c - ACC : c;
+    r += wrap ? q + 1 : q;
     __builtin_amdgcn_sched_barrier(0);  // one row block at a time (no hoisting: register peak)
   }
   wave_lds_sync();

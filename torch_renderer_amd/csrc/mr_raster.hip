@@ -709,6 +709,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1 (faces_per_pixel=%d)", s->faces_per_pixel);
   if (sp->out_flags & MR_OUT_HARD) return set_err(MR_EUNSUPPORTED, "hard_rgb_blend runs on the fragment-shader path (mr_shade_fragments_*)");
   if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
+  if (m->F * 27 >= (1ll << 30)) return set_err(MR_EUNSUPPORTED, "F >= 2^30 / 27 faces");  // 32-bit row offsets
   if (!fws || !bws || !gverts || (!gviews && !(gRcv && gtcv))) return set_err(MR_EINVAL, "NULL argument");
   if (sp->light_kind == 0 && !vraw) return set_err(MR_EINVAL, "raw vertex normals required");
   const size_t need = mr_render_backward_workspace(N, m->V, m->F, s->H, s->W);

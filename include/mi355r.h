@@ -303,6 +303,25 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* mesh, const float* vnormals
                                     float* grad_tex_rgba, float* grad_verts_uvs, int64_t num_verts_uvs,
                                     void* stream);
 
+/* MeshRenderer(MeshRasterizer(faces_per_pixel = K, 2 <= K <= 64), SoftSilhouetteShader(sigma)) for ONE
+ * mesh shared by N views (deform_mesh_with_color.py:153-165) in one pass: the K-deep fragments are blended
+ * as they are produced and never written. rgba (N,H,W,4) must hold the background (1, 1, 1, 0) on entry
+ * (tiles no face reaches are not written); it gets (1, 1, 1, 1 - prod_k (1 - sigmoid(-d_k / sigma))),
+ * bitwise mr_rasterize_meshes_world + mr_shade_fragments_forward(MR_OUT_SIL). views_out / face_verts as
+ * mr_rasterize_meshes_world. The workspace keeps each tile's fragments compactly for the backward, which
+ * writes grad_face_verts (N*F,3,3) for mr_project_faces_backward: the chain of
+ * mr_shade_fragments_backward(MR_OUT_SIL) and mr_rasterize_meshes_backward without fragment-gradient
+ * tensors. MR_EUNSUPPORTED for grids the per-view binning does not take (the caller then runs the
+ * two-step path). */
+size_t mr_soft_silhouette_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t K, int32_t max_faces_per_bin);
+int32_t mr_soft_silhouette_forward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                   const mr_poses_t* poses, int64_t N, const mr_raster_settings_t* s, float sigma,
+                                   mr_view_t* views_out, float* face_verts, float* rgba, void* workspace,
+                                   size_t workspace_bytes, void* stream);
+int32_t mr_soft_silhouette_backward(const float* face_verts, int64_t N, int64_t F, const mr_raster_settings_t* s,
+                                    float sigma, const float* grad_rgba, const void* workspace, float* grad_face_verts,
+                                    void* stream);
+
 /* ---------------- instrumentation ---------------- */
 
 /* camera_pose_optimizer.py:257-276 Model.calc_loss fused: sil_loss =

@@ -66,3 +66,27 @@ def test_mesh_rasterizer_of_an_empty_scene(K):
     for x in (frag.zbuf, frag.dists, frag.bary_coords):
         assert bool((x.detach() == -1).all())
     assert torch.equal(vg.grad.cpu(), torch.zeros_like(verts))
+
+
+def test_fused_soft_silhouette_of_an_empty_scene():
+    """MeshRenderer(MeshRasterizer(K = 8), SoftSilhouetteShader): no occupied tile, so the fused raster emits
+    no slot and k_sil_bwd's grid exits on the slot counter; every pixel keeps the prefilled (1, 1, 1, 0)."""
+    from torch_renderer_amd.mesh_renderer import MeshRenderer, SoftSilhouetteShader
+    verts, faces, _ = mesh_arrays("cow")
+    H, W = 48, 56
+    R, T, _, _ = canonical_views(verts, 2, H, W)
+    T = T.clone()
+    T[:, 2] -= 50.0
+    cams = PerspectiveCameras(device=DEV)
+    vg = verts.to(DEV).requires_grad_(True)
+    meshes = Meshes([vg], [faces.to(DEV)]).extend(2)
+    rs = RasterizationSettings(image_size=(H, W), faces_per_pixel=8, blur_radius=1e-4)
+    renderer = MeshRenderer(MeshRasterizer(cams, rs), SoftSilhouetteShader())
+    _dirty_allocator()
+    img = renderer(meshes, R=R.to(DEV), T=T.to(DEV))
+    img.sum().backward()
+    torch.cuda.synchronize()
+    bg = torch.zeros(2, H, W, 4)
+    bg[..., :3] = 1.0
+    assert torch.equal(img.detach().cpu(), bg)
+    assert torch.equal(vg.grad.cpu(), torch.zeros_like(verts))

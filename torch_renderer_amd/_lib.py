@@ -93,6 +93,12 @@ _SIGS = [
                                          ctypes.POINTER(MrRasterSettings), _VP, _VP, _VP, _VP, _VP, _VP, _VP, _SZ,
                                          _VP]),
     ("mr_binning_background_pixels", _I64, [_I64, _I64, _I32, _I32, _I32]),
+    ("mr_soft_silhouette_workspace", _SZ, [_I64, _I64, _I32, _I32, _I32, _I32]),
+    ("mr_soft_silhouette_forward", _I32, [_VP, _I64, _VP, _I64, ctypes.POINTER(MrPoses), _I64,
+                                          ctypes.POINTER(MrRasterSettings), ctypes.c_float, _VP, _VP, _VP, _VP, _SZ,
+                                          _VP]),
+    ("mr_soft_silhouette_backward", _I32, [_VP, _I64, _I64, ctypes.POINTER(MrRasterSettings), ctypes.c_float, _VP,
+                                           _VP, _VP, _VP]),
     ("mr_project_faces", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_project_faces_meshes", _I32, [_VP, _I64, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_project_faces_meshes_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP,

@@ -74,16 +74,23 @@ struct RasterBwdParams {
 
 // One stored fragment (pixel px, py; slot pix; packed face f) of the modular raster backward:
 // the 9 face_verts gradients of face f in g.
+MR_DEV void raster_bwd_fragment_v(const RasterBwdParams& P, int px, int py, int64_t f, float gzp, const float (&gb)[3],
+                                  float gdp, float (&g)[3][3]);
 MR_DEV void raster_bwd_fragment(const RasterBwdParams& P, int px, int py, int64_t pix, int64_t f, float (&g)[3][3]) {
+  // an upstream gradient PyTorch passed as None arrives as NULL: zero
+  const float gb[3] = {P.gb ? P.gb[3 * pix] : 0.0f, P.gb ? P.gb[3 * pix + 1] : 0.0f, P.gb ? P.gb[3 * pix + 2] : 0.0f};
+  const float gzp = P.gz ? P.gz[pix] : 0.0f, gdp = P.gd ? P.gd[pix] : 0.0f;
+  raster_bwd_fragment_v(P, px, py, f, gzp, gb, gdp, g);
+}
+// The same from the fragment's upstream gradients given as values (gz, gb, gd).
+MR_DEV void raster_bwd_fragment_v(const RasterBwdParams& P, int px, int py, int64_t f, float gzp, const float (&gb)[3],
+                                  float gdp, float (&g)[3][3]) {
   FaceRec r;
   const float* v = P.fv + 9 * f;
   r.x0 = v[0]; r.y0 = v[1]; r.z0 = v[2];
   r.x1 = v[3]; r.y1 = v[4]; r.z1 = v[5];
   r.x2 = v[6]; r.y2 = v[7]; r.z2 = v[8];
   r.area = (float)((double)edge_fn(r.x2, r.y2, r.x0, r.y0, r.x1, r.y1) + MR_KEPS_D);
-  // an upstream gradient PyTorch passed as None arrives as NULL: zero
-  const float gb[3] = {P.gb ? P.gb[3 * pix] : 0.0f, P.gb ? P.gb[3 * pix + 1] : 0.0f, P.gb ? P.gb[3 * pix + 2] : 0.0f};
-  const float gzp = P.gz ? P.gz[pix] : 0.0f, gdp = P.gd ? P.gd[pix] : 0.0f;
   const float xf = col_ndc(px, P.H, P.W), yf = row_ndc(py, P.H, P.W);
   int ci = 0;
   const float vv[3][3] = {{r.x0, r.y0, r.z0}, {r.x1, r.y1, r.z1}, {r.x2, r.y2, r.z2}};

@@ -48,7 +48,6 @@ struct FragSums {
   float numw[3], denw;   // sum_k w_k c_k, sum_k w_k
 };
 
-MR_DEV float frag_prob(float d, float inv_sigma) { return sigmoidf_((-d) * inv_sigma); }
 
 MR_DEV void frag_sums(const FragShadeParams& P, int64_t pix, int n, FragSums& R, bool colours) {
   const ShadeParams& S = P.S;
@@ -289,4 +288,60 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
     if (!P.sil && S.light_kind == 0) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
     else if (ACC == 27 && !P.sil) seg_scatter<ACC>(key, row, P.gface, lrow[wave], lkey[wave]);
   }
+}
+
+// Backward of the fused soft silhouette: one wave per slot over its compact fragments (coalesced), the
+// blend's derivative (k_frag_shade_bwd's silhouette branch: the distance gradient) chained straight into
+// the rasterizer's backward (raster_bwd_fragment with zero depth / barycentric gradients) — no fragment
+// gradient tensors; face_verts gradients summed per workgroup in an LDS hash (as k_raster_bwd_slots).
+struct SilBwdParams {
+  RasterBwdParams R;
+  int T, TX;
+  float isig;
+  const int* ctr;
+  const int* stile;
+  const int* scount;
+  const int4* sent;
+  const float4* spix;
+  const float* grad_rgba;
+};
+__global__ void __launch_bounds__(256) k_sil_bwd(SilBwdParams P) {
+  __shared__ LdsAcc<9> L;
+  const int nslots = P.ctr[CTR_SLOTS];
+  if ((int)blockIdx.x * 4 >= nslots) return;  // uniform over the workgroup
+  acc_init(L);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (s < nslots) {
+    const int gt = P.stile[s];
+    const int n = gt / P.T, t = gt - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int64_t HW = (int64_t)P.R.H * P.R.W;
+    const int ne = P.scount[s];
+    const int4* ent = P.sent + (int64_t)s * 64 * P.R.K;
+    for (int e = lane; e < ne; e += 64) {
+      const int4 en = ent[e];
+      const int pl = en.z & 255, k = en.z >> 8;
+      const int px = tx * MR_TS + (pl & 7), py = ty * MR_TS + (pl >> 3);
+      const float4 inf = P.spix[(int64_t)s * 64 + pl];
+      const float alpha_nz = inf.x;
+      const int nzero = __float_as_int(inf.y), kzero = __float_as_int(inf.z);
+      const float d = __int_as_float(en.y);
+      const float g_alpha = -P.grad_rgba[4 * (n * HW + (int64_t)py * P.R.W + px) + 3];  // A = 1 - alpha
+      const float prob = frag_prob(d, P.isig);
+      const float one_m = 1.0f - prob;
+      const float others = nzero == 0 ? alpha_nz * frcp(one_m) : (nzero == 1 && kzero == k ? alpha_nz : 0.0f);
+      const float g_prob = g_alpha * (-others);
+      float sp_, sq_;
+      sigmoid2((-d) * P.isig, sp_, sq_);
+      const float gd = -((g_prob * (sp_ * sq_)) * P.isig);
+      const float gb0[3] = {0.0f, 0.0f, 0.0f};
+      float g[3][3];
+      raster_bwd_fragment_v(P.R, px, py, en.x, 0.0f, gb0, gd, g);
+      acc_add<9>(L, P.R.gfv, en.x, &g[0][0]);
+    }
+  }
+  __syncthreads();
+  acc_flush(L, P.R.gfv);
 }

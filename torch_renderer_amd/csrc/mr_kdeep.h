@@ -155,7 +155,13 @@ struct KpStage {
   unsigned long long cmask[64];
   unsigned long long bucket[MR_KP_BC][64];
 };
-template <int KP>
+// SIL: the fused soft silhouette (mr_soft_silhouette_forward): instead of writing the K fragment
+// slots, each pixel's sorted list is blended (sigmoid_alpha_blend, as k_frag_shade_fwd over the stored
+// fragments, same operations in the same order) into rgba, and the tile's fragments are kept compactly
+// for the backward: {packed face, signed distance, lane | k << 8} per fragment, lane-major (a pixel's
+// fragments consecutive) from the slot's region, their count per slot, and per tile pixel the blend's
+// {product of the non-zero (1 - p) factors, number of zero factors, index of the last zero factor}.
+template <int KP, bool SIL = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_raster_kp(FwdParams P) {
   __shared__ KpStage S;
   const int lane = threadIdx.x;
@@ -305,6 +311,44 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     wave_lds_sync();  // the stage is rewritten by the next batch
   }
   drain();
+  if (SIL) {
+    const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
+    const int cnt = in_img ? min(lc, K) : 0;
+    const int incl = wave_incl_sum(cnt);
+    if (lane == 63) P.scount[s] = incl;
+    int4* ent = P.sent + (int64_t)s * 64 * K + (incl - cnt);
+    float alpha_nz = 1.0f;
+    int nzero = 0, kzero = -1;
+#pragma unroll 1
+    for (int k = 0; k < K; ++k) {
+      if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
+      const unsigned long long key = q[0];
+#pragma unroll
+      for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
+      q[KP - 1] = MR_KEY_EMPTY;
+      if (!in_img || !(key < MR_KEY_EMPTY)) continue;
+      const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
+      const FaceRec r = P.recs[id];
+      FragEval ev;
+      eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
+      const float prob = frag_prob(ev.sdist, P.isig);
+      const float one_m = 1.0f - prob;
+      if (one_m == 0.0f) {
+        ++nzero;
+        kzero = k;
+      } else {
+        alpha_nz *= one_m;
+      }
+      ent[k] = make_int4(rec_orig(id, P.NF), __float_as_int(ev.sdist), lane | (k << 8), 0);
+    }
+    if (in_img) {
+      const int64_t q4 = n * HW + (int64_t)py * W + px;
+      const float alpha = nzero ? 0.0f : alpha_nz;
+      ((float4*)P.sil)[q4] = make_float4(1.0f, 1.0f, 1.0f, 1.0f - alpha);
+    }
+    P.spix[(int64_t)s * 64 + lane] = make_float4(alpha_nz, __int_as_float(nzero), __int_as_float(kzero), 0.0f);
+    return;
+  }
   if (!in_img) return;
   const int64_t pix = (n * HW + (int64_t)py * W + px) * K;
   const float xf = col_ndc(px, H, W), yf = row_ndc(py, H, W);
@@ -332,11 +376,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
-template <int KP>
+template <int KP, bool SIL = false>
 static void launch_raster_kr(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
   if (slots_cap >= (1ll << 31)) return;
-  MR_TIMED(KID_RASTER_K, st, (k_raster_kp<KP><<<(unsigned)slots_cap, 64, 0, st>>>(P)));  // one wave per tile
+  MR_TIMED(KID_RASTER_K, st, (k_raster_kp<KP, SIL><<<(unsigned)slots_cap, 64, 0, st>>>(P)));  // one wave per tile
 }
+// The fused soft silhouette's raster (K <= 64, register lists).
+static void launch_raster_sil(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+  const int K = P.K;
+  const int64_t sc = N * (int64_t)g.T;
+  if (K <= 4) launch_raster_kr<4, true>(P, sc, st);
+  else if (K <= 8) launch_raster_kr<8, true>(P, sc, st);
+  else if (K <= 16) launch_raster_kr<16, true>(P, sc, st);
+  else if (K <= 32) launch_raster_kr<32, true>(P, sc, st);
+  else if (K <= 50) launch_raster_kr<50, true>(P, sc, st);
+  else launch_raster_kr<64, true>(P, sc, st);
+}
+
 
 static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
   static int fgrid = 0;

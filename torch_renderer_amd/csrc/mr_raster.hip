@@ -335,6 +335,110 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
   return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
 }
 
+// ---------------- fused soft silhouette (MeshRenderer(MeshRasterizer(K > 1), SoftSilhouetteShader)) --------
+struct SilWS {
+  int* scount;
+  float4* spix;
+  int4* sent;
+  size_t bytes;
+};
+static SilWS carve_sil(void* base, size_t raster_bytes, int64_t NT, int K) {
+  SilWS w;
+  char* b = (char*)base;
+  size_t off = align_up(raster_bytes, 256);
+  w.scount = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)NT, 256);
+  w.spix = (float4*)(b + off);
+  off = align_up(off + sizeof(float4) * 64 * (size_t)NT, 256);
+  w.sent = (int4*)(b + off);
+  off = align_up(off + sizeof(int4) * 64 * (size_t)K * (size_t)NT, 256);
+  w.bytes = off;
+  return w;
+}
+size_t mr_soft_silhouette_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t K, int32_t max_faces_per_bin) {
+  const int64_t Fb = N * F > 0 ? N * F : 1;
+  BinGeom g = bin_geom(H, W, N, Fb, max_faces_per_bin);
+  const size_t rb = carve_raster_ws(nullptr, N, Fb, H, W, g).bytes;
+  return carve_sil(nullptr, rb, N * (int64_t)g.T, K > 0 ? K : 1).bytes;
+}
+
+int32_t mr_soft_silhouette_forward(const float* verts, int64_t V, const int32_t* faces, int64_t F,
+                                   const mr_poses_t* poses, int64_t N, const mr_raster_settings_t* s, float sigma,
+                                   mr_view_t* views_out, float* face_verts, float* rgba, void* ws, size_t ws_bytes,
+                                   void* stream) {
+  int rc = check_settings(s);
+  if (rc) return rc;
+  const int K = s->faces_per_pixel;
+  if (K < 2 || K > 64) return set_err(MR_EUNSUPPORTED, "fused soft silhouette: 2 <= faces_per_pixel <= 64 (got %d)", K);
+  if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N must be in [1, 65535] (got %lld)", (long long)N);
+  if (F <= 0 || V <= 0 || N * F >= (1ll << 30)) return set_err(MR_EINVAL, "F / V out of range");
+  if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
+  if (!(sigma > 0.0f)) return set_err(MR_EINVAL, "sigma must be > 0");
+  if (!poses || !poses->R || !poses->T || !poses->intr || !views_out || !verts || !faces || !face_verts || !rgba)
+    return set_err(MR_EINVAL, "NULL argument");
+  if (poses->R_stride < 0 || poses->T_stride < 0 || poses->intr_stride < 0) return set_err(MR_EINVAL, "negative stride");
+  const int64_t Fb = N * F;
+  BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
+  if (!view_binning(g, N, Fb)) return set_err(MR_EUNSUPPORTED, "fused soft silhouette: per-view binning sizes only");
+  if ((int64_t)N * g.T * 64 * K >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*T*64*K >= 2^31");
+  RasterWS w = carve_raster_ws(ws, N, Fb, s->H, s->W, g);
+  SilWS sw = carve_sil(ws, w.bytes, N * (int64_t)g.T, K);
+  if (ws_bytes < sw.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, sw.bytes);
+  hipStream_t st = (hipStream_t)stream;
+  CvPoses C;
+  C.R = poses->R; C.sR = poses->R_stride; C.t = poses->T; C.sT = poses->T_stride;
+  C.intr = poses->intr; C.sI = poses->intr_stride; C.out = (float*)views_out; C.opencv = 0;
+  SetupParams SP = make_setup(s, g, w);
+  SP.NF = Fb;
+  SP.fv_out = face_verts;
+  FwdParams P = make_fwd(s, g, w, N, nullptr, F, Fb);
+  P.sil = rgba;
+  P.isig = 1.0f / sigma;  // = mr_shade_params_t.sigma_sil's reciprocal in make_shade
+  P.scount = sw.scount; P.spix = sw.spix; P.sent = sw.sent;
+  NormalsArgs NA;
+  memset(&NA, 0, sizeof(NA));
+  dim3 rgrid((unsigned)ceil_div(F, 256), (unsigned)N + 1);  // row 0: counter clear
+  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  MR_CHECK_LAUNCH("k_bin_rect_world");
+  if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, F, true, st))) return rc;
+  launch_raster_sil(P, g, N, st);
+  MR_CHECK_LAUNCH("k_raster_kp (silhouette)");
+  return MR_OK;
+}
+
+int32_t mr_soft_silhouette_backward(const float* face_verts, int64_t N, int64_t F, const mr_raster_settings_t* s,
+                                    float sigma, const float* grad_rgba, const void* ws, float* grad_face_verts,
+                                    void* stream) {
+  int rc = check_settings(s);
+  if (rc) return rc;
+  if (N <= 0 || N > 65535 || F <= 0) return set_err(MR_EINVAL, "bad sizes");
+  if (!face_verts || !grad_rgba || !ws || !grad_face_verts) return set_err(MR_EINVAL, "NULL argument");
+  const int K = s->faces_per_pixel;
+  if (K < 2 || K > 64 || !(sigma > 0.0f)) return set_err(MR_EINVAL, "bad faces_per_pixel / sigma");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t Fb = N * F;
+  if (hipMemsetAsync(grad_face_verts, 0, sizeof(float) * 9 * (size_t)Fb, st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "memset failed");
+  BinGeom g = bin_geom(s->H, s->W, N, Fb, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws((void*)ws, N, Fb, s->H, s->W, g);
+  SilWS sw = carve_sil((void*)ws, w.bytes, N * (int64_t)g.T, K);
+  SilBwdParams P;
+  memset(&P, 0, sizeof(P));
+  P.R.N = (int)N; P.R.H = s->H; P.R.W = s->W; P.R.NBX = ceil_div(s->W, MR_BT); P.R.K = K;
+  P.R.persp = s->perspective_correct; P.R.clipb = s->clip_barycentric_coords;
+  P.R.cull = s->cull_backfaces; P.R.clipz = s->clip_z != 0; P.R.zc = s->z_clip_value;
+  P.R.blur = s->blur_radius; P.R.bbox_pad = sqrtf(s->blur_radius);
+  P.R.fv = face_verts; P.R.gfv = grad_face_verts;
+  P.T = g.T; P.TX = g.TX; P.isig = 1.0f / sigma;
+  P.ctr = w.ctr; P.stile = w.stile; P.scount = sw.scount; P.sent = sw.sent; P.spix = sw.spix;
+  P.grad_rgba = grad_rgba;
+  const int64_t NT = N * (int64_t)g.T;
+  MR_TIMED(KID_RASTER_BWD, st, (k_sil_bwd<<<(unsigned)((NT + 3) / 4), 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_sil_bwd");
+  return MR_OK;
+}
+
 int32_t mr_rasterize_meshes_backward(const float* fv, const int64_t* p2f, const float* gz, const float* gb,
                                      const float* gd, int64_t N, int64_t Ftot, const mr_raster_settings_t* s,
                                      float* gfv, void* stream) {

@@ -74,6 +74,8 @@ MR_DEV float dot3(const float a[3], const float b[3]) {
   return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
 }
 MR_DEV float sigmoidf_(float x) { return frcp(1.0f + fexp(-x)); }
+// sigmoid_alpha_blend's per-fragment probability sigmoid(-d / sigma)
+MR_DEV float frag_prob(float d, float inv_sigma) { return sigmoidf_((-d) * inv_sigma); }
 // sigmoid(x) and 1 - sigmoid(x), each to a few ulp of ITS OWN value. 1 - p is not formed as a
 // difference: near saturation (p -> 1, i.e. a pixel a few sigma inside a face) that cancels every
 // significant bit, and the blends' derivative p (1 - p) / sigma (x 1e4) carries the loss straight into

@@ -234,6 +234,11 @@ struct FwdParams {
   float* rgb;
   int32_t* p2f32;  // optional
   float4* frec;    // MODE 1: the winners' fragments for the backward (slot-major, 64 per slot)
+  // fused soft silhouette (k_raster_kp<KP, true>): sil = rgba (N,H,W,4); the compact fragments per slot
+  float isig;
+  int* scount;
+  int4* sent;
+  float4* spix;
 };
 
 // One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).

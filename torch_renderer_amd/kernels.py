@@ -287,6 +287,54 @@ class RasterizeMeshesWorld(torch.autograd.Function):
         return (gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12]) + (None,) * 12
 
 
+class SoftSilhouetteWorld(torch.autograd.Function):
+    """MeshRenderer(MeshRasterizer(faces_per_pixel = K > 1), SoftSilhouetteShader) for one mesh shared by N
+    views in one native pass (mr_soft_silhouette_forward / _backward; deform_mesh_with_color.py:153-165):
+    the K-deep fragments are blended as the raster produces them and never written. Bitwise
+    RasterizeMeshesWorld + ShadeFragments(silhouette) in the forward; the backward chains the blend's
+    distance gradients straight into the rasterizer's backward (no fragment-gradient tensors), then
+    mr_project_faces_backward as RasterizeMeshesWorld does. Returns rgba (N,H,W,4)."""
+
+    @staticmethod
+    def forward(ctx, verts, R, T, faces, intr, N, H, W, K, blur, persp, clip, cull, mfpb, z_clip, sigma):
+        _require_cuda(verts, R, T, faces, intr)
+        L = _lib.load()
+        v = verts.detach().float().contiguous()
+        f, vptr, vadj = mesh_topology(faces, v.shape[0])
+        N, Fn, dev = int(N), f.shape[0], v.device
+        ps, keep = _poses_struct(R, T, intr)
+        s = raster_settings_struct(H, W, K, blur, persp, clip, cull, mfpb, z_clip)
+        views = torch.empty((N, 16), device=dev)
+        fv = torch.empty((N * Fn, 3, 3), device=dev)
+        rgba = torch.tensor([1.0, 1.0, 1.0, 0.0], device=dev).expand(N, H, W, 4).contiguous()  # background
+        wsb = L.mr_soft_silhouette_workspace(N, Fn, H, W, K, s.max_faces_per_bin)
+        ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
+        check(L.mr_soft_silhouette_forward(ptr(v), v.shape[0], ptr(f), Fn, ctypes.byref(ps), N, ctypes.byref(s),
+                                           float(sigma), ptr(views), ptr(fv), ptr(rgba), ptr(ws), wsb,
+                                           _lib.stream_handle(dev)))
+        del keep
+        ctx.save_for_backward(v, f, views, vptr, vadj, fv, ws)
+        ctx.cfg = (H, W, K, persp, clip, blur, cull, mfpb, z_clip, float(sigma))
+        return rgba
+
+    @staticmethod
+    def backward(ctx, g):
+        v, f, views, vptr, vadj, fv, ws = ctx.saved_tensors
+        H, W, K, persp, clip, blur, cull, mfpb, z_clip, sigma = ctx.cfg
+        L = _lib.load()
+        N = views.shape[0]
+        dev = v.device
+        s = raster_settings_struct(H, W, K, blur, persp, clip, cull, mfpb, z_clip)
+        gfv = torch.empty_like(fv)
+        check(L.mr_soft_silhouette_backward(ptr(fv), N, f.shape[0], ctypes.byref(s), sigma,
+                                            ptr(g.float().contiguous()), ptr(ws), ptr(gfv), _lib.stream_handle(dev)))
+        gv = torch.empty_like(v)
+        gviews = torch.empty((N, 12), device=dev)
+        check(L.mr_project_faces_backward(ptr(v), v.shape[0], ptr(f), f.shape[0], ptr(vptr), ptr(vadj), ptr(views),
+                                          N, ptr(gfv), ptr(gv), ptr(gviews), _lib.stream_handle(dev)))
+        return (gv, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12]) + (None,) * 13
+
+
 def vertex_normals(verts, faces):
     """(normals, raw sums) — Meshes.verts_normals_packed on the GPU (no autograd)."""
     _require_cuda(verts, faces)

@@ -460,6 +460,27 @@ class MeshRenderer(torch.nn.Module):
         cfg.z_clip = _z_clip_value(cameras, rs)
         return cfg
 
+    def _soft_silhouette(self, meshes, cameras, rs, kwargs):
+        """SoftSilhouetteWorld for a shared mesh, or None when the grid is one the per-view binning does not
+        take (the caller then runs rasterizer + shader)."""
+        from .kernels import SoftSilhouetteWorld
+
+        H, W = rs.hw()
+        persp = cameras.is_perspective() if rs.perspective_correct is None else bool(rs.perspective_correct)
+        clip = rs.blur_radius > 0.0 if rs.clip_barycentric_coords is None else bool(rs.clip_barycentric_coords)
+        cfg = _shade_config(self.shader, cameras, H, W, kwargs)
+        R, T, intr = _views(meshes, cameras, (H, W), kwargs)
+        N, Fn = R.shape[0], meshes.shared_faces().shape[0]
+        # the fused pass needs the per-view binning (mr_rasterize_meshes_world's common case: <= 16,384
+        # 8x8 tiles, <= 256 per side, <= 65,536 faces per view)
+        tx, ty = (W + 7) // 8, (H + 7) // 8
+        if tx * ty > 16384 or tx > 256 or ty > 256 or Fn > 65536:
+            return None
+        return SoftSilhouetteWorld.apply(meshes.shared_verts(), R, T, meshes.shared_faces(), intr, N, H, W,
+                                         int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip,
+                                         bool(rs.cull_backfaces), rs.max_faces_per_bin, _z_clip_value(cameras, rs),
+                                         cfg.sigma_sil)
+
     def forward(self, meshes_world: Meshes, **kwargs) -> torch.Tensor:
         """upstream signature: forward(meshes_world, **kwargs) (camera_pose_optimizer.py:177)."""
         from .torch_renderer import render_mesh_batch
@@ -471,6 +492,13 @@ class MeshRenderer(torch.nn.Module):
         rs = kwargs.get("raster_settings", self.rasterizer.raster_settings)
         from .torch_renderer import textures_need_modular
 
+        if (type(self.shader) is SoftSilhouetteShader and type(self.rasterizer) is MeshRasterizer and
+                1 < int(rs.faces_per_pixel) <= 64 and meshes.is_shared() and not rs.cull_to_frustum):
+            # the soft silhouette of deform_mesh_with_color.py: raster + sigmoid_alpha_blend in one pass,
+            # the fragments never written (bitwise the two-step result; SoftSilhouetteWorld)
+            out = self._soft_silhouette(meshes, cameras, rs, kwargs)
+            if out is not None:
+                return out
         if int(rs.faces_per_pixel) != 1 or float(rs.blur_radius) != 0.0 or isinstance(self.shader, HardPhongShader) or (
                 isinstance(self.shader, SoftPhongShader) and textures_need_modular(meshes)):
             # soft rasterization, or a texture map that needs gradients: the HIP

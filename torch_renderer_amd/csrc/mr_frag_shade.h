@@ -290,38 +290,39 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
   }
 }
 
-// Backward of the fused soft silhouette: one wave per slot over its compact fragments (coalesced), the
-// blend's derivative (k_frag_shade_bwd's silhouette branch: the distance gradient) chained straight into
-// the rasterizer's backward (raster_bwd_fragment with zero depth / barycentric gradients) — no fragment
-// gradient tensors; face_verts gradients summed per workgroup in an LDS hash (as k_raster_bwd_slots).
+// Backward of the fused soft silhouette over the flat fragment array (coalesced, balanced: a chunk of
+// MR_SIL_CHUNK fragments per workgroup iteration whatever the tile it came from; one wave per slot ran each
+// heavy tile's ~3k fragments serially), the blend's derivative (k_frag_shade_bwd's silhouette branch: the
+// distance gradient) chained straight into the rasterizer's backward (raster_bwd_fragment with zero depth /
+// barycentric gradients) — no fragment gradient tensors; face_verts gradients summed per chunk in an LDS
+// hash (a chunk's fragments come from one or two tiles), flushed with one global atomic per face component.
+#define MR_SIL_CHUNK 1024
 struct SilBwdParams {
   RasterBwdParams R;
   int T, TX;
   float isig;
   const int* ctr;
   const int* stile;
-  const int* scount;
   const int4* sent;
   const float4* spix;
   const float* grad_rgba;
 };
 __global__ void __launch_bounds__(256) k_sil_bwd(SilBwdParams P) {
   __shared__ LdsAcc<9> L;
-  const int nslots = P.ctr[CTR_SLOTS];
-  if ((int)blockIdx.x * 4 >= nslots) return;  // uniform over the workgroup
-  acc_init(L);
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int s = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (s < nslots) {
-    const int gt = P.stile[s];
-    const int n = gt / P.T, t = gt - n * P.T;
-    const int ty = t / P.TX, tx = t - ty * P.TX;
-    const int64_t HW = (int64_t)P.R.H * P.R.W;
-    const int ne = P.scount[s];
-    const int4* ent = P.sent + (int64_t)s * 64 * P.R.K;
-    for (int e = lane; e < ne; e += 64) {
-      const int4 en = ent[e];
+  const int ne = P.ctr[CTR_SENT];
+  const int64_t HW = (int64_t)P.R.H * P.R.W;
+#pragma unroll 1
+  for (int c0 = blockIdx.x * MR_SIL_CHUNK; c0 < ne; c0 += gridDim.x * MR_SIL_CHUNK) {  // uniform
+    acc_init(L);
+    __syncthreads();
+    const int c1 = min(c0 + MR_SIL_CHUNK, ne);
+#pragma unroll 1
+    for (int e = c0 + (int)threadIdx.x; e < c1; e += 256) {
+      const int4 en = P.sent[e];
+      const int s = en.w;
+      const int gt = P.stile[s];
+      const int n = gt / P.T, t = gt - n * P.T;
+      const int ty = t / P.TX, tx = t - ty * P.TX;
       const int pl = en.z & 255, k = en.z >> 8;
       const int px = tx * MR_TS + (pl & 7), py = ty * MR_TS + (pl >> 3);
       const float4 inf = P.spix[(int64_t)s * 64 + pl];
@@ -341,7 +342,8 @@ __global__ void __launch_bounds__(256) k_sil_bwd(SilBwdParams P) {
       raster_bwd_fragment_v(P.R, px, py, en.x, 0.0f, gb0, gd, g);
       acc_add<9>(L, P.R.gfv, en.x, &g[0][0]);
     }
+    __syncthreads();
+    acc_flush(L, P.R.gfv);
+    __syncthreads();
   }
-  __syncthreads();
-  acc_flush(L, P.R.gfv);
 }

@@ -153,13 +153,16 @@ struct KpStage {
   int mark[64];
   int bcnt[64];
   unsigned long long cmask[64];
+  unsigned long long thr[64];  // per pixel: its list's last key once full (else EMPTY), set at each drain
   unsigned long long bucket[MR_KP_BC][64];
 };
+
 // SIL: the fused soft silhouette (mr_soft_silhouette_forward): instead of writing the K fragment
 // slots, each pixel's sorted list is blended (sigmoid_alpha_blend, as k_frag_shade_fwd over the stored
 // fragments, same operations in the same order) into rgba, and the tile's fragments are kept compactly
-// for the backward: {packed face, signed distance, lane | k << 8} per fragment, lane-major (a pixel's
-// fragments consecutive) from the slot's region, their count per slot, and per tile pixel the blend's
+// for the backward: {packed face, signed distance, lane | k << 8, slot} per fragment in one flat array (each
+// slot's run lane-major, a pixel's fragments consecutive, at an offset from one atomic per wave; the total in
+// ctr[CTR_SENT]), and per tile pixel the blend's
 // {product of the non-zero (1 - p) factors, number of zero factors, index of the last zero factor}.
 template <int KP, bool SIL = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_raster_kp(FwdParams P) {
@@ -203,6 +206,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   };
   S.bcnt[lane] = 0;
   S.mark[lane] = -1;
+  S.thr[lane] = MR_KEY_EMPTY;
   int mb = 0;  // the fullest bucket's fill (uniform)
   int lc = 0;  // keys in this lane's list
   // Drain: every bucket's keys into its lane's list. The lists' fill after the drain is known before
@@ -229,6 +233,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       for (int i = 0; i < mc; ++i) insert(i < c ? S.bucket[i][lane] : MR_KEY_EMPTY);
     }
     S.bcnt[lane] = 0;
+    S.thr[lane] = lc >= KP ? q[KP - 1] : MR_KEY_EMPTY;  // a full list rejects every key above its last
     wave_lds_sync();
     mb = 0;
   };
@@ -290,7 +295,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         const FaceRec r = stage_rec_get(S.rec, m);
         const int id = S.id[m];
         const float xf = col_ndc(x0 + (p & 7), H, W), yf = row_ndc(y0 + (p >> 3), H, W);
-        float pz;
+        float pz = 0.0f;
         int cid = id;
         bool keep = false;
         if (r.flags & FR_PAIR) {  // the split face's two triangles as one candidate (pair rule)
@@ -299,9 +304,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         } else if (r.flags & FR_VALID) {
           keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
         }
-        if (keep) {
+        const unsigned long long key = frag_key(pz, (int)rec_code(cid, P.NF));
+        if (keep && key < S.thr[p]) {  // (keys a full list would reject do not enter the buckets)
           const int pos = atomicAdd(&S.bcnt[p], 1);
-          S.bucket[pos][p] = frag_key(pz, (int)rec_code(cid, P.NF));
+          S.bucket[pos][p] = key;
         }
       }
       pb = pend;
@@ -315,8 +321,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const float xf = col_ndc(in_img ? px : 0, H, W), yf = row_ndc(in_img ? py : 0, H, W);
     const int cnt = in_img ? min(lc, K) : 0;
     const int incl = wave_incl_sum(cnt);
-    if (lane == 63) P.scount[s] = incl;
-    int4* ent = P.sent + (int64_t)s * 64 * K + (incl - cnt);
+    int base = 0;
+    if (lane == 63) base = atomicAdd(&P.ctr[CTR_SENT], incl);  // the slot's run of the flat fragment array
+    base = __builtin_amdgcn_readlane(base, 63);
+    int4* ent = P.sent + base + (incl - cnt);
     float alpha_nz = 1.0f;
     int nzero = 0, kzero = -1;
 #pragma unroll 1
@@ -339,7 +347,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       } else {
         alpha_nz *= one_m;
       }
-      ent[k] = make_int4(rec_orig(id, P.NF), __float_as_int(ev.sdist), lane | (k << 8), 0);
+      ent[k] = make_int4(rec_orig(id, P.NF), __float_as_int(ev.sdist), lane | (k << 8), s);
     }
     if (in_img) {
       const int64_t q4 = n * HW + (int64_t)py * W + px;

@@ -337,7 +337,6 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
 
 // ---------------- fused soft silhouette (MeshRenderer(MeshRasterizer(K > 1), SoftSilhouetteShader)) --------
 struct SilWS {
-  int* scount;
   float4* spix;
   int4* sent;
   size_t bytes;
@@ -346,8 +345,6 @@ static SilWS carve_sil(void* base, size_t raster_bytes, int64_t NT, int K) {
   SilWS w;
   char* b = (char*)base;
   size_t off = align_up(raster_bytes, 256);
-  w.scount = (int*)(b + off);
-  off = align_up(off + sizeof(int) * (size_t)NT, 256);
   w.spix = (float4*)(b + off);
   off = align_up(off + sizeof(float4) * 64 * (size_t)NT, 256);
   w.sent = (int4*)(b + off);
@@ -394,7 +391,7 @@ int32_t mr_soft_silhouette_forward(const float* verts, int64_t V, const int32_t*
   FwdParams P = make_fwd(s, g, w, N, nullptr, F, Fb);
   P.sil = rgba;
   P.isig = 1.0f / sigma;  // = mr_shade_params_t.sigma_sil's reciprocal in make_shade
-  P.scount = sw.scount; P.spix = sw.spix; P.sent = sw.sent;
+  P.spix = sw.spix; P.sent = sw.sent;
   NormalsArgs NA;
   memset(&NA, 0, sizeof(NA));
   dim3 rgrid((unsigned)ceil_div(F, 256), (unsigned)N + 1);  // row 0: counter clear
@@ -431,10 +428,11 @@ int32_t mr_soft_silhouette_backward(const float* face_verts, int64_t N, int64_t 
   P.R.blur = s->blur_radius; P.R.bbox_pad = sqrtf(s->blur_radius);
   P.R.fv = face_verts; P.R.gfv = grad_face_verts;
   P.T = g.T; P.TX = g.TX; P.isig = 1.0f / sigma;
-  P.ctr = w.ctr; P.stile = w.stile; P.scount = sw.scount; P.sent = sw.sent; P.spix = sw.spix;
+  P.ctr = w.ctr; P.stile = w.stile; P.sent = sw.sent; P.spix = sw.spix;
   P.grad_rgba = grad_rgba;
-  const int64_t NT = N * (int64_t)g.T;
-  MR_TIMED(KID_RASTER_BWD, st, (k_sil_bwd<<<(unsigned)((NT + 3) / 4), 256, 0, st>>>(P)));
+  static int grid = 0;
+  if (!grid) grid = resident_grid(k_sil_bwd, 256, 8);
+  MR_TIMED(KID_RASTER_BWD, st, (k_sil_bwd<<<grid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_sil_bwd");
   return MR_OK;
 }

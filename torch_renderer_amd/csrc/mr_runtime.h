@@ -80,7 +80,8 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // ---------------------------------------------------------------------------
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
-enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_ENTRIES64 = 4, CTR_COUNT = 8 };
+// ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_COUNT = 8 };
 
 struct BinGeom {
   int TX, TY, T;

@@ -236,7 +236,6 @@ struct FwdParams {
   float4* frec;    // MODE 1: the winners' fragments for the backward (slot-major, 64 per slot)
   // fused soft silhouette (k_raster_kp<KP, true>): sil = rgba (N,H,W,4); the compact fragments per slot
   float isig;
-  int* scount;
   int4* sent;
   float4* spix;
 };

@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
 // order: the fragments are bitwise those of the face-at-a-time kernel (deform workload: 2.22 ms
 // (two waves per tile, every face at every pixel) -> see DESIGN.md for this kernel's numbers).
 #ifndef MR_KP_BC
-#define MR_KP_BC 32
+#define MR_KP_BC 24
 #endif
 // Shift-insert of key into the first NS positions of the ascending list q (positions >= NS are
 // empty for every lane of the wave and stay so: no lane holds more than NS keys).
@@ -144,8 +144,12 @@ MR_DEV void insert_ns(unsigned long long (&q)[KP], unsigned long long key) {
 }
 
 #ifndef MR_KP_ROOM
-#define MR_KP_ROOM 16  // drain the buckets once the fullest one has less room than this
+#define MR_KP_ROOM 12  // drain the buckets once the fullest one has less room than this
 #endif
+#ifndef MR_KP_SORT
+#define MR_KP_SORT 2048  // tiles of 65 .. MR_KP_SORT listed faces are walked in depth order (0: never)
+#endif
+#define MR_KP_ZBINS 256
 struct KpStage {
   float rec[16][64];
   int id[64];
@@ -156,6 +160,65 @@ struct KpStage {
   unsigned long long thr[64];  // per pixel: its list's last key once full (else EMPTY), set at each drain
   unsigned long long bucket[MR_KP_BC][64];
 };
+static_assert(MR_KP_SORT <= 65536 && sizeof(KpStage::bucket) >= sizeof(int) * (MR_KP_SORT + MR_KP_ZBINS),
+              "the depth sort's scratch lives in the bucket array");
+
+// Depth order of a tile's list (entries list[base .. base + count)): perm[i] = the entry to walk i-th,
+// by a counting sort of the faces' nearest vertex depth into MR_KP_ZBINS bins over the tile's range
+// (order inside a bin: arbitrary). The K nearest keys do not depend on the walk order, so this only
+// changes how much work they take: walked near-to-far, each pixel's list holds its final keys after
+// its first few dozen candidates and the full list's last key (S.thr) then keeps the farther
+// candidates out of the buckets — the drains' shift-inserts, ~40 % of the kernel on the deform
+// workload, run about once per kept key instead of once per candidate. The bucket array is the
+// sort's scratch (the bins' counts and each entry's (bin, rank)); only perm (u16) persists.
+MR_DEV void kp_depth_order(const FwdParams& P, KpStage& S, unsigned short* perm, int64_t base, int count, int lane) {
+  float* zs = (float*)&S.bucket[0][0];  // count floats, then the bins
+  int* zb = (int*)zs;
+  int* bins = (int*)zs + MR_KP_SORT;
+  float lo = INFINITY, hi = -INFINITY;
+#pragma unroll 1
+  for (int e = lane; e < count; e += 64) {
+    const float* f = (const float*)(P.recs + P.list[base + e]);
+    const float z = fminf(fminf(f[2], f[5]), f[8]);  // z0, z1, z2
+    zs[e] = z;
+    lo = fminf(lo, z);
+    hi = fmaxf(hi, z);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = fminf(lo, __shfl_xor(lo, o, 64));
+    hi = fmaxf(hi, __shfl_xor(hi, o, 64));
+  }
+  const float span = hi - lo;
+  const float scale = span > 0.0f && span < INFINITY ? (float)MR_KP_ZBINS / span : 0.0f;
+#pragma unroll
+  for (int k = 0; k < MR_KP_ZBINS / 64; ++k) bins[k * 64 + lane] = 0;
+  wave_lds_sync();
+#pragma unroll 1
+  for (int e = lane; e < count; e += 64) {
+    const float t = (zs[e] - lo) * scale;
+    const int b = t >= 0.0f ? min((int)t, MR_KP_ZBINS - 1) : 0;  // (NaN: bin 0)
+    zb[e] = (b << 16) | atomicAdd(&bins[b], 1);
+  }
+  wave_lds_sync();
+  int c[MR_KP_ZBINS / 64], run = 0;  // lane owns bins [4 lane, 4 lane + 4): exclusive prefix
+#pragma unroll
+  for (int k = 0; k < MR_KP_ZBINS / 64; ++k) {
+    c[k] = run;
+    run += bins[lane * (MR_KP_ZBINS / 64) + k];
+  }
+  const int off = wave_incl_sum(run) - run;
+  wave_lds_sync();
+#pragma unroll
+  for (int k = 0; k < MR_KP_ZBINS / 64; ++k) bins[lane * (MR_KP_ZBINS / 64) + k] = off + c[k];
+  wave_lds_sync();
+#pragma unroll 1
+  for (int e = lane; e < count; e += 64) {
+    const int v = zb[e];
+    perm[bins[v >> 16] + (v & 0xffff)] = (unsigned short)e;
+  }
+  wave_lds_sync();
+}
 
 // SIL: the fused soft silhouette (mr_soft_silhouette_forward): instead of writing the K fragment
 // slots, each pixel's sorted list is blended (sigmoid_alpha_blend, as k_frag_shade_fwd over the stored
@@ -167,6 +230,7 @@ struct KpStage {
 template <int KP, bool SIL = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_raster_kp(FwdParams P) {
   __shared__ KpStage S;
+  __shared__ unsigned short perm[MR_KP_SORT > 0 ? MR_KP_SORT : 1];
   const int lane = threadIdx.x;
   const int s = blockIdx.x;
   if (s >= P.ctr[CTR_SLOTS]) return;
@@ -176,6 +240,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const bool fast_ok = !(blur > 0.0f);
   const int H = P.H, W = P.W;
   const int64_t HW = (int64_t)H * W;
+#ifdef MR_XP_STAMP  // per-tile timing for tools/kp_stamps.py (experiment builds only)
+  const unsigned long long t_start = wall_clock64();
+  int xp_passes = 0, xp_drains = 0;
+#endif
   const int gt = P.stile[s];
   const int n = gt / P.T, t = gt - n * P.T;
   const int ty = t / P.TX, tx = t - ty * P.TX;
@@ -189,6 +257,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const int64_t vcnt = P.view_count ? P.view_count[n] : P.F;
   const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
   const int xe = min(x0 + MR_TS, W) - 1, ye = min(y0 + MR_TS, H) - 1;  // the tile's last pixels inside the image
+  const bool zsorted = MR_KP_SORT > 0 && !ovf && count > 64 && count <= MR_KP_SORT;
+  if (zsorted) kp_depth_order(P, S, perm, vb + ex, count, lane);
   unsigned long long q[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
@@ -214,6 +284,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   // than NS keys, only the first NS positions can change and the shift runs NS steps, not KP
   // (most lists hold a few keys: the full KP-step shift was ~half of the kernel).
   auto drain = [&]() {
+#ifdef MR_XP_STAMP
+    ++xp_drains;
+#endif
     wave_lds_sync();
     const int c = S.bcnt[lane];
     const int mc = __builtin_amdgcn_readlane(wave_incl_max(c), 63);
@@ -242,7 +315,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const int e = eb + lane;
     unsigned long long cmask = 0;
     if (e < count) {
-      const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + e];
+      const int id = ovf ? (int)(vfirst + e) : P.list[vb + ex + (zsorted ? (int)perm[e] : e)];
       const FaceRec r = load_rec(P.recs, id);
       // candidate pixels: the record's padded bbox; an overflow unit scans only first triangles of
       // split faces, so there it covers both triangles of the pair (as k_tile_raster)
@@ -278,6 +351,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 #pragma unroll 1
     for (int pb = 0; pb < NP;) {
       if (mb > MR_KP_BC - MR_KP_ROOM) drain();
+#ifdef MR_XP_STAMP
+      ++xp_passes;
+#endif
       // the entry straddling pb, and the first entry past what the buckets can still take
       const int first = 63 - __builtin_clzll(__ballot(np > 0 && pexcl <= pb));
       const int lim = first + (MR_KP_BC - mb);
@@ -355,6 +431,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       ((float4*)P.sil)[q4] = make_float4(1.0f, 1.0f, 1.0f, 1.0f - alpha);
     }
     P.spix[(int64_t)s * 64 + lane] = make_float4(alpha_nz, __int_as_float(nzero), __int_as_float(kzero), 0.0f);
+#ifdef MR_XP_STAMP
+    const unsigned long long t_end = wall_clock64();
+    if (lane < 4) {
+      const int v = lane == 0 ? (int)(unsigned)t_start : lane == 1 ? (int)(unsigned)t_end : lane == 2 ? xp_passes : xp_drains;
+      P.sil[(n * HW + (int64_t)y0 * W + x0 + lane) * 4] = __int_as_float(v);
+    }
+#endif
     return;
   }
   if (!in_img) return;

@@ -277,13 +277,38 @@ MR_DEV Bg background(const FwdParams& P) {
   return b;
 }
 
+// m 16-B words per pixel quad of a chunk of nq quads, all of the same value, written
+// lane-contiguously: store k of the wave covers the chunk's words [64 k, 64 k + 64) (one 1-KB
+// burst per store instruction; a lane writing its quad's m consecutive words strides every store
+// by 16 m bytes: fragment pass 164 -> 161 us, tools/micro/store_bw.hip 103 -> 89 us for the whole
+// fragment background). The fused render's background keeps the per-lane layout: its
+// lane-contiguous version measured 221 -> 244 us per step (profiles/r3s_fill_ab.txt).
+template <int M, typename T4>
+MR_DEV void fill_words(T4* __restrict__ base, int nq, int lane, const T4& v) {
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+    if (k * 64 + lane < M * nq) base[k * 64 + lane] = v;
+}
+
 // Background of one 64-lane chunk of view n: 4 pixels per lane and 16-B vector stores when
-// W % 4 == 0 (every row then starts 16-B aligned), else one pixel per lane.
+// W % 4 == 0 (every row then starts 16-B aligned; PyTorch3D fragments lane-contiguous), else one
+// pixel per lane.
 template <int MODE, int CH>
 MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) {
   const int lane = threadIdx.x & 63;
   const int64_t HW = (int64_t)P.H * P.W * (MODE == 0 ? P.K : 1);  // MODE 0: every entry is -1
-  if (vec) {
+  if (MODE == 0 && vec) {
+    const int64_t q0 = (int64_t)c * 64;  // first quad of the chunk inside the view
+    const int nq = (int)min((int64_t)64, HW / 4 - q0);
+    if (nq <= 0) return;
+    const int64_t pix = (int64_t)n * HW + 4 * q0;
+    const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+    const longlong2 l1 = make_longlong2(-1ll, -1ll);
+    fill_words<2>((longlong2*)(P.p2f + pix), nq, lane, l1);
+    fill_words<1>((float4*)(P.zbuf + pix), nq, lane, m1);
+    fill_words<1>((float4*)(P.dists + pix), nq, lane, m1);
+    fill_words<3>((float4*)(P.bary + pix * 3), nq, lane, m1);
+  } else if (vec) {
     const int64_t g = (int64_t)c * 64 + lane;
     if (g >= HW / 4) return;
     const int64_t pix = (int64_t)n * HW + 4 * g;

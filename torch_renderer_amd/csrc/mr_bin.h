@@ -696,12 +696,60 @@ MR_DEV float cv_view_elem(const CvPoses& C, int64_t n, int k) {
   }
   return v;
 }
+// m 16-B words per pixel quad of a chunk of nq quads, all of the same value, written
+// lane-contiguously: store k of the wave covers the chunk's words [64 k, 64 k + 64) (one 1-KB
+// burst per store instruction; a lane writing its quad's m consecutive words strides every store
+// by 16 m bytes: fragment pass 164 -> 161 us, tools/micro/store_bw.hip 103 -> 89 us for the whole
+// fragment background). The fused render's background keeps the per-lane layout: its
+// lane-contiguous version measured 221 -> 244 us per step (profiles/r3s_fill_ab.txt).
+template <int M, typename T4>
+MR_DEV void fill_words(T4* __restrict__ base, int nq, int lane, const T4& v) {
+#pragma unroll
+  for (int k = 0; k < M; ++k)
+    if (k * 64 + lane < M * nq) base[k * 64 + lane] = v;
+}
+
+// PyTorch3D fragment background chunks (64 pixel quads each, view-major, W % 4 == 0) that a
+// k_bin_rect_world launch writes from grid rows past the views: the record pass stores ~100 B per
+// face at ~2.6 TB/s, so its launch has store bandwidth to spare for part of the 470-MB background
+// the binning and raster launches otherwise stream (count 0: none).
+struct FragBg {
+  int64_t* p2f;
+  float *zbuf, *dists, *bary;
+  int H, W, nviews;
+  int first, count;  // chunks [first, first + count)
+};
+MR_DEV void frag_bg_rows(const FragBg& B, int row) {
+  const int lane = threadIdx.x & 63;
+  const int w = (row * (int)gridDim.x + (int)blockIdx.x) * 4 + (int)(threadIdx.x >> 6);
+  const int G = ((int)gridDim.y - 1 - B.nviews) * (int)gridDim.x * 4;
+  const int64_t HW = (int64_t)B.H * B.W;
+  const int cpv = (int)((HW / 4 + 63) / 64);
+  const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+  const longlong2 l1 = make_longlong2(-1ll, -1ll);
+#pragma unroll 1
+  for (int c = B.first + w; c < B.first + B.count; c += G) {
+    const int n = c / cpv;
+    const int64_t q0 = (int64_t)(c - n * cpv) * 64;
+    const int nq = (int)min((int64_t)64, HW / 4 - q0);
+    const int64_t pix = (int64_t)n * HW + 4 * q0;
+    fill_words<2>((longlong2*)(B.p2f + pix), nq, lane, l1);
+    fill_words<1>((float4*)(B.zbuf + pix), nq, lane, m1);
+    fill_words<1>((float4*)(B.dists + pix), nq, lane, m1);
+    fill_words<3>((float4*)(B.bary + pix * 3), nq, lane, m1);
+  }
+}
+
 template <bool CLIP>
 __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const float* __restrict__ verts,
                                                         const int32_t* __restrict__ faces, int64_t F,
                                                         const ViewRec* __restrict__ views, NormalsArgs NA,
-                                                        int* __restrict__ ctr, CvPoses C) {
+                                                        int* __restrict__ ctr, CvPoses C, FragBg B) {
   const int n = (int)blockIdx.y - 1;
+  if (B.count > 0 && n >= B.nviews) {
+    frag_bg_rows(B, n - B.nviews);
+    return;
+  }
   if (n >= 0 && C.R && blockIdx.x == 0 && threadIdx.x < 16) C.out[(int64_t)n * 16 + threadIdx.x] = cv_view_elem(C, n, threadIdx.x);
   if (n < 0) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -128,6 +128,12 @@ extern "C++" {
 #ifndef MR_BG_CPW_FRAG
 #define MR_BG_CPW_FRAG 8    // 7 KB chunks (PyTorch3D fragments; 4 -> 8: fragment pass 166 -> 162 us)
 #endif
+#ifndef MR_BG_RECT_ROWS
+#define MR_BG_RECT_ROWS 16  // fragment background rows of the record launch (each ceil(F / 256) workgroups)
+#endif
+#ifndef MR_BG_RECT_CPW
+#define MR_BG_RECT_CPW 4    // chunks per wave of those rows
+#endif
 #ifndef MR_VIEW_LDS
 #define MR_VIEW_LDS 98304  // k_bin_view's LDS: the tile histogram + the list stage
 #endif
@@ -245,7 +251,8 @@ int32_t mr_rasterize_meshes(const float* face_verts, const int64_t* first, const
       if ((rc = launch_bin_view(SP, w, g, N, first, count, 0, true, st))) return rc;
       return launch_raster_k(P, g, N, st);
     }
-    if ((rc = launch_bin_view<0, 3>(SP, w, g, N, first, count, 0, false, st, nullptr, &P))) return rc;
+    P.emit_frag = (s->W & 3) == 0;  // per-tile counts (ranges) for the raster's background skip
+    if ((rc = launch_bin_view<0, 3>(SP, w, g, N, first, count, 0, P.emit_frag != 0, st, nullptr, &P))) return rc;
     return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
   }
   const int fvb = ceil_div(Ftot, 256 * MR_FV_FPT);
@@ -324,14 +331,30 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
   NormalsArgs NA;
   memset(&NA, 0, sizeof(NA));
   dim3 rgrid((unsigned)ceil_div(F, 256), (unsigned)N + 1);  // row 0: counter clear
-  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
-  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  // K = 1, W % 4 == 0: background chunks past k_bin_view's share go to extra rows of the record
+  // launch (up to MR_BG_RECT_ROWS rows of MR_BG_RECT_CPW chunks per wave), the rest to the raster
+  FragBg FB{};
+  int64_t rect_bg0 = 0, rect_bgn = 0;
+  if (s->faces_per_pixel == 1 && (s->W & 3) == 0 && MR_BG_RECT_ROWS > 0) {
+    const int64_t total = N * (((int64_t)s->H * s->W / 4 + 63) / 64);
+    rect_bg0 = bg_chunks(N, 0, s->H, s->W, 0);  // = the k_bin_view share launch_bin_view takes
+    rect_bgn = std::min<int64_t>(total - rect_bg0, (int64_t)MR_BG_RECT_ROWS * rgrid.x * 4 * MR_BG_RECT_CPW);
+    if (rect_bgn > 0) {
+      FB.p2f = p2f; FB.zbuf = zbuf; FB.dists = dists; FB.bary = bary;
+      FB.H = s->H; FB.W = s->W; FB.nviews = (int)N; FB.first = (int)rect_bg0; FB.count = (int)rect_bgn;
+      rgrid.y += MR_BG_RECT_ROWS;
+    }
+  }
+  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C, FB)));
+  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C, FB)));
   MR_CHECK_LAUNCH("k_bin_rect_world");
   if (s->faces_per_pixel > 1) {
     if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, F, true, st))) return rc;
     return launch_raster_k(P, g, N, st);
   }
-  if ((rc = launch_bin_view<0, 3>(SP, w, g, N, nullptr, nullptr, F, false, st, nullptr, &P))) return rc;
+  P.emit_frag = (s->W & 3) == 0;  // per-tile counts (ranges) for the raster's background skip
+  if ((rc = launch_bin_view<0, 3>(SP, w, g, N, nullptr, nullptr, F, P.emit_frag != 0, st, nullptr, &P))) return rc;
+  if (rect_bgn > 0) P.fill_first = (int)(rect_bg0 + rect_bgn);  // the raster writes the chunks after the record launch's
   return launch_raster_and_shade<0, 3>(P, g, N, st, s->clip_z != 0);
 }
 
@@ -395,8 +418,8 @@ int32_t mr_soft_silhouette_forward(const float* verts, int64_t V, const int32_t*
   NormalsArgs NA;
   memset(&NA, 0, sizeof(NA));
   dim3 rgrid((unsigned)ceil_div(F, 256), (unsigned)N + 1);  // row 0: counter clear
-  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
-  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C)));
+  if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C, FragBg{})));
+  else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, verts, faces, F, (const ViewRec*)views_out, NA, w.ctr, C, FragBg{})));
   MR_CHECK_LAUNCH("k_bin_rect_world");
   if ((rc = launch_bin_view(SP, w, g, N, nullptr, nullptr, F, true, st))) return rc;
   launch_raster_sil(P, g, N, st);
@@ -728,8 +751,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     NA.nzero4 = (27 * m->F + 3) / 4;
     const int64_t bx = std::max<int64_t>(ceil_div(maxvf, 256), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
-    if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
-    else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C)));
+    if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C, FragBg{})));
+    else MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<false><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C, FragBg{})));
     MR_CHECK_LAUNCH("k_bin_rect_world");
     if (sp->rgb_channels == 4) {
       if ((rc = launch_bin_view<1, 4>(SP, w, g, N, m->view_face_first, m->view_face_count, m->F, false, st, &P.S, &P))) return rc;

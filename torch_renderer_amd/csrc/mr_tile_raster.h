@@ -214,6 +214,8 @@ struct FwdParams {
   int64_t list_cap;
   int mfpb;
   int fill;  // k_tile_raster also writes the background
+  int emit_frag;  // MODE 0, W % 4 == 0, cnt per tile: k_tile_raster writes each listed tile's 64 fragments
+                  // itself and its background chunks skip the listed tiles (no k_shade<0> launch)
   int fill_first;  // ... from this chunk on: the chunks before it were written by k_bin_view<MODE, CH>
   int* ctr;
   unsigned long long* tkey;
@@ -275,19 +277,6 @@ MR_DEV Bg background(const FwdParams& P) {
     b.c[0] = o.rgb[0]; b.c[1] = o.rgb[1]; b.c[2] = o.rgb[2]; b.c[3] = o.alpha;
   }
   return b;
-}
-
-// m 16-B words per pixel quad of a chunk of nq quads, all of the same value, written
-// lane-contiguously: store k of the wave covers the chunk's words [64 k, 64 k + 64) (one 1-KB
-// burst per store instruction; a lane writing its quad's m consecutive words strides every store
-// by 16 m bytes: fragment pass 164 -> 161 us, tools/micro/store_bw.hip 103 -> 89 us for the whole
-// fragment background). The fused render's background keeps the per-lane layout: its
-// lane-contiguous version measured 221 -> 244 us per step (profiles/r3s_fill_ab.txt).
-template <int M, typename T4>
-MR_DEV void fill_words(T4* __restrict__ base, int nq, int lane, const T4& v) {
-#pragma unroll
-  for (int k = 0; k < M; ++k)
-    if (k * 64 + lane < M * nq) base[k * 64 + lane] = v;
 }
 
 // Background of one 64-lane chunk of view n: 4 pixels per lane and 16-B vector stores when
@@ -371,6 +360,50 @@ MR_DEV void fill_chunk(const FwdParams& P, const Bg& b, int n, int c, bool vec) 
   }
 }
 
+// PyTorch3D fragment background of one chunk (view n, 64 pixel quads, W % 4 == 0) outside the
+// listed tiles (emit_frag: k_tile_raster writes every pixel of a listed tile when it resolves the
+// tile, so neither write can land after the other on the same pixel). A quad never straddles a
+// tile (quads start at multiples of 4 pixels, tiles at multiples of 8), and each 16-B word of
+// every array belongs to one quad (p2f: 2 words per quad, zbuf / dists: 1, bary: 3).
+MR_DEV void fill_frag_unlisted(const FwdParams& P, int n, int c) {
+  const int lane = threadIdx.x & 63;
+  const int64_t HW = (int64_t)P.H * P.W;
+  const int64_t q0 = (int64_t)c * 64;
+  const int nq = (int)min((int64_t)64, HW / 4 - q0);
+  if (nq <= 0) return;
+  bool listed = false;
+  if (lane < nq) {
+    const int p0 = (int)(4 * q0);  // the chunk's first pixel (uniform: one division per chunk)
+    int y = p0 / P.W, x = p0 - y * P.W + 4 * lane;
+    while (x >= P.W) {  // (one step at most when W >= 256)
+      x -= P.W;
+      ++y;
+    }
+    listed = P.cnt[(int64_t)n * P.T + (y >> 3) * P.TX + (x >> 3)] > 0;
+  }
+  const unsigned long long lm = __ballot(listed);
+  const int64_t pix = (int64_t)n * HW + 4 * q0;
+  const float4 m1 = make_float4(-1.f, -1.f, -1.f, -1.f);
+  longlong2* p2 = (longlong2*)(P.p2f + pix);
+  float4* pz = (float4*)(P.zbuf + pix);
+  float4* pd = (float4*)(P.dists + pix);
+  float4* pb = (float4*)(P.bary + pix * 3);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int j = k * 64 + lane;
+    if (j < 2 * nq && !((lm >> (j >> 1)) & 1ull)) p2[j] = make_longlong2(-1ll, -1ll);
+  }
+  if (lane < nq && !((lm >> lane) & 1ull)) {
+    pz[lane] = m1;
+    pd[lane] = m1;
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int j = k * 64 + lane;
+    if (j < 3 * nq && !((lm >> (j / 3)) & 1ull)) pb[j] = m1;
+  }
+}
+
 // Persistent grid of independent waves (4 per workgroup, no workgroup barriers): wave g
 // takes units g, g + G, ... of the list k_bin_scan emitted (G = resident waves). Per unit:
 //  (1) one entry per lane: load its face record, clip the face's padded pixel bbox to the
@@ -419,9 +452,16 @@ __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P, FwdParams F)
   const int64_t HW = (int64_t)F.H * F.W * (MODE == 0 ? F.K : 1);
   const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
   const Bg bg = background<MODE>(F);
+  const int c0 = b * 16 + (int)(threadIdx.x >> 6);
+  const int gn = nbw / cpv, gc = nbw - gn * cpv;
+  int cn = c0 / cpv, cc = c0 - cn * cpv;
 #pragma unroll 1
-  for (int c = b * 16 + (int)(threadIdx.x >> 6); c < F.fill_first; c += nbw)
-    fill_chunk<MODE, CH>(F, bg, c / cpv, c - (c / cpv) * cpv, vec);
+  for (int c = c0; c < F.fill_first; c += nbw) {
+    fill_chunk<MODE, CH>(F, bg, cn, cc, vec);
+    cn += gn;
+    cc += gc;
+    if (cc >= cpv) { cc -= cpv; ++cn; }
+  }
 }
 
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
@@ -623,12 +663,53 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
       const unsigned code = (unsigned)(k & 0xffffffffull);
       const int px = x0 + (lane & 7), py = y0 + (lane >> 3);
       const bool hit = code != MR_NONE && px < W && py < H;
-      P.sface[(int64_t)slot * 64 + lane] = hit ? (CLIP ? code_rec(code, P.NF) : (int)(code >> 1)) : -1;
+      const int rid = hit ? (CLIP ? code_rec(code, P.NF) : (int)(code >> 1)) : -1;
+      if (MODE == 0 && P.emit_frag) {
+        // the tile's fragments (k_shade<0>'s work): the winner's exact evaluation, or the background
+        if (px < W && py < H) {
+          const int64_t q = (int64_t)n * H * W + (int64_t)py * W + px;
+          int64_t f = -1;
+          float z = -1.0f, d = -1.0f, b0 = -1.0f, b1 = -1.0f, b2 = -1.0f;
+          if (hit) {
+            const FaceRec r = load_rec(P.recs, rid);
+            FragEval ev;
+            eval_face(r, S.xs[lane & 7], S.ys[lane >> 3], pad, blur, persp, clipb, ev);  // kept by construction
+            if (r.flags & FR_CLIP) clip_unconvert(P.crec[rid], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+            f = rec_orig(rid, P.NF); z = ev.pz; d = ev.sdist; b0 = ev.b0; b1 = ev.b1; b2 = ev.b2;
+          }
+          P.p2f[q] = f;
+          P.zbuf[q] = z;
+          P.dists[q] = d;
+          P.bary[3 * q + 0] = b0;
+          P.bary[3 * q + 1] = b1;
+          P.bary[3 * q + 2] = b2;
+        }
+      } else {
+        P.sface[(int64_t)slot * 64 + lane] = rid;
+      }
     }
     wave_lds_sync();
   }
+  // (view, chunk) stepped incrementally: no integer division per chunk
+  const int gn = G / cpv, gc = G - gn * cpv;
+  int cn = chunk / cpv, cc = chunk - cn * cpv;
+  if (MODE == 0 && P.emit_frag) {
 #pragma unroll 1
-  for (; chunk < nchunks; chunk += G) fill_chunk<MODE, CH>(P, bg, chunk / cpv, chunk - (chunk / cpv) * cpv, vec);
+    for (; chunk < nchunks; chunk += G) {
+      fill_frag_unlisted(P, cn, cc);
+      cn += gn;
+      cc += gc;
+      if (cc >= cpv) { cc -= cpv; ++cn; }
+    }
+  } else {
+#pragma unroll 1
+    for (; chunk < nchunks; chunk += G) {
+      fill_chunk<MODE, CH>(P, bg, cn, cc, vec);
+      cn += gn;
+      cc += gc;
+      if (cc >= cpv) { cc -= cpv; ++cn; }
+    }
+  }
 }
 
 // Per-face shading records of the shared mesh (one thread per face).
@@ -802,6 +883,7 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   if (clip) MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, true><<<rgrid_c, 256, 0, st>>>(P)));
   else MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, false><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");
+  if (MODE == 0 && P.emit_frag) return MR_OK;  // the raster wrote the listed tiles' fragments
   const int64_t slots_cap = N * (int64_t)g.T;
   int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
   sg = (sg + 7) / 8 * 8;  // XCD-partitioned slot ranges

@@ -377,11 +377,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (r.flags & FR_PAIR) {  // the split face's two triangles as one candidate (pair rule)
           keep = pair_keep(P.recs, P.NF, id, r, xf, yf, pad, blur, persp, clipb, cid, pz) &&
                  (cid == id || (ovf && id < P.NF));
+          keep = keep && frag_key(pz, (int)rec_code(cid, P.NF)) < S.thr[p];
         } else if (r.flags & FR_VALID) {
-          keep = frag_keep(r, xf, yf, pad, blur, persp, clipb, fast_ok && (r.flags & FR_FAST), pz);
+          // the depth key first: a key the pixel's full list rejects skips the point-triangle distance
+          // (most of the late candidates of a near-to-far walk)
+          bool inside = false;
+          keep = frag_depth(r, xf, yf, pad, persp, clipb, fast_ok && (r.flags & FR_FAST), pz, inside) &&
+                 frag_key(pz, (int)rec_code(cid, P.NF)) < S.thr[p] &&
+                 (inside || (blur > 0.0f && !(pt_tri_dist(xf, yf, r) >= blur)));
         }
         const unsigned long long key = frag_key(pz, (int)rec_code(cid, P.NF));
-        if (keep && key < S.thr[p]) {  // (keys a full list would reject do not enter the buckets)
+        if (keep) {  // (keys a full list would reject do not enter the buckets)
           const int pos = atomicAdd(&S.bcnt[p], 1);
           S.bucket[pos][p] = key;
         }

@@ -124,6 +124,32 @@ MR_DEV bool frag_keep(const FaceRec& r, float x, float y, float pad, float blur,
   return true;
 }
 
+// frag_keep split in two for callers that can reject on the depth key first (k_raster_kp): the part
+// up to the depth (bbox, edge signs, divisions, pz >= 0), with the inside flag; the caller then keeps
+// the fragment iff inside || (blur > 0 && !(pt_tri_dist >= blur)) — frag_keep's decision exactly.
+MR_DEV bool frag_depth(const FaceRec& r, float x, float y, float pad, bool persp, bool clipb, bool fast, float& pz,
+                       bool& inside) {
+  if (x > r.xmax + pad || x < r.xmin - pad || y > r.ymax + pad || y < r.ymin - pad) return false;
+  const float e0 = edge_fn(x, y, r.x1, r.y1, r.x2, r.y2);
+  const float e1 = edge_fn(x, y, r.x2, r.y2, r.x0, r.y0);
+  const float e2 = edge_fn(x, y, r.x0, r.y0, r.x1, r.y1);
+  if (fast) {
+    const bool inp = (e0 > 0.0f) & (e1 > 0.0f) & (e2 > 0.0f);
+    const bool inn = (e0 < 0.0f) & (e1 < 0.0f) & (e2 < 0.0f);
+    if (!(r.area > 0.0f ? inp : inn)) return false;
+  }
+  const float w0 = e0 / r.area, w1 = e1 / r.area, w2 = e2 / r.area;
+  float c0, c1, c2, b0, b1, b2;
+  if (persp) persp_fwd(w0, w1, w2, r.z0, r.z1, r.z2, c0, c1, c2);
+  else { c0 = w0; c1 = w1; c2 = w2; }
+  if (clipb) clip_fwd(c0, c1, c2, b0, b1, b2);
+  else { b0 = c0; b1 = c1; b2 = c2; }
+  pz = b0 * r.z0 + b1 * r.z1 + b2 * r.z2;
+  if (pz < 0.0f) return false;
+  inside = c0 > 0.0f && c1 > 0.0f && c2 > 0.0f;
+  return true;
+}
+
 #define MR_NONE 0x7fffffff  // "no face" sentinel, larger than any face code
 
 // Sort code of a record id: upstream's clipped packed order puts the two triangles of a split

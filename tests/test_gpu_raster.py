@@ -16,6 +16,8 @@ CASES = [
     ("cow", 96, 128, 3, True),
     ("teapot", 80, 80, 2, False),
     ("dolphin", 64, 96, 1, True),
+    # W % 8 == 4: the last tile column is half outside the image, 256-pixel background chunks span rows
+    ("cow", 60, 100, 2, True),
 ]
 
 

@@ -87,6 +87,10 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
         * RGBA as SoftSilhouetteShader returns it, (1, 1, 1, alpha) per pixel, written by the
         * kernels; its gradient is the (N,H,W,4) gradient of that tensor (channel 3 is read) */
        MR_OUT_SIL_RGBA = 32,
+       /* with MR_OUT_DEPTH, mr_render_forward/_backward[_opencv]: the depth buffer is MeshRasterizer's
+        * zbuf[..., 0] of K = 1 fragments (the nearest face's depth, -1 where no face) instead of
+        * DepthRender's relu of it (camera_pose_optimizer.py:244-246 reads rasterizer(...).zbuf). */
+       MR_OUT_ZBUF = 64,
        /* mr_shade_fragments_* only: every pixel's empty slots (pix_to_face = -1) follow its filled
         * ones, as mr_rasterize_meshes[_world] (and PyTorch3D's rasterizer) write them; the kernels
         * then stop at a pixel's first empty slot instead of reading all K (same results) */
@@ -332,13 +336,28 @@ int32_t mr_soft_silhouette_backward(const float* face_verts, int64_t N, int64_t 
  * backward writes dL/d{depth, sil, rgb (npix,3)} given the device scalar dL/dtotal and the
  * forward's workspace. */
 size_t mr_pose_loss_workspace(int64_t npix);
-int32_t mr_pose_loss_forward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
-                             const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
-                             float delta, float w_color, float* out, void* ws, size_t ws_bytes, void* stream);
-int32_t mr_pose_loss_backward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
-                              const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
-                              float delta, float w_color, const float* g_total, const void* fwd_ws,
+int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                             int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                             int64_t npix, float delta, float w_color, float* out, void* ws, size_t ws_bytes,
+                             void* stream);
+/* sil_stride 1: sil is (npix); 4: sil is channel 3 of an (npix, 4) RGBA tensor (the SoftSilhouetteShader
+ * image the reference slices with [..., 3]), read in place. rgb_stride 3 or 4 likewise. The gradients
+ * come back in the same layouts, for the whole tensors the views were taken from: g_sil (npix) or
+ * (npix, 4) RGBA with zero RGB, g_rgb (npix, 3) or (npix, 4) with zero alpha — what the slices'
+ * backward would produce, without its zero-filled buffer and strided copy. */
+int32_t mr_pose_loss_backward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                              int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                              int64_t npix, float delta, float w_color, const float* g_total, const void* fwd_ws,
                               float* g_depth, float* g_sil, float* g_rgb, void* stream);
+
+/* upstream pytorch3d.transforms.quaternion_to_matrix (camera_pose_optimizer.py:241: the 7-vector
+ * pose's real-first quaternion, not renormalised: two_s = 2 / |q|^2) for N quaternions q (rows
+ * q_stride floats apart) -> R (N,3,3), torch's operation order (bitwise the elementwise torch
+ * formula); the backward writes dL/dq (N,4) from dL/dR. One launch each instead of ~90 tiny torch
+ * kernels per optimiser step. */
+int32_t mr_quaternion_to_matrix(const float* q, int64_t q_stride, int64_t N, float* R, void* stream);
+int32_t mr_quaternion_to_matrix_backward(const float* q, int64_t q_stride, const float* grad_R, int64_t N,
+                                         float* grad_q, void* stream);
 
 /* Work counters left in `workspace` by the last mr_render_forward / mr_rasterize_meshes that used it
  * (same N, total faces, H, W, max_faces_per_bin). Synchronises `stream`; for benchmarks and tools.
@@ -346,6 +365,13 @@ int32_t mr_pose_loss_backward(const float* depth, const float* sil, const float*
  * out[3] = covered pixels. */
 int32_t mr_workspace_stats(const void* workspace, int64_t N, int64_t total_faces, int32_t H, int32_t W,
                            int32_t max_faces_per_bin, int64_t* out, void* stream);
+
+/* The 8 raw work counters at the head of a forward workspace (same sizes as the forward that used
+ * it): [0] work units, [1] non-empty tiles, [3] kept soft-silhouette fragments, [4..5] list entries
+ * (u64), [6] tiles the K-deep raster walked near-to-far (its depth-ordered list walk). Synchronises
+ * `stream`; for tests and tools. */
+int32_t mr_workspace_counters(const void* workspace, int64_t N, int64_t total_faces, int32_t H, int32_t W,
+                              int32_t max_faces_per_bin, int32_t* out8, void* stream);
 
 /* Per-kernel timing with HIP events recorded on each launch's stream (bench.py).
  * enable=1 clears and starts collection; mr_timing_read synchronizes on the

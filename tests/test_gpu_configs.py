@@ -411,9 +411,10 @@ def test_c5_subdivided_sphere_1024_vertex_grads():
 
 
 def test_determinism_metric_config():
-    """Rendering the benchmarked batch twice gives bitwise-identical images, pix_to_face and
-    per-view pose gradients. The shared vertex gradient sums face rows with float atomics (one
-    per run of equal faces per tile), so it may differ run to run in the last bits: reported."""
+    """Rendering the benchmarked batch twice gives bitwise-identical images, pix_to_face, per-view
+    pose gradients AND shared vertex gradients: the backward writes one gradient row per (record,
+    tile) with plain stores and k_face_reduce sums each face's rows in a fixed order (no float
+    atomics on the per-view binning path)."""
     H = W = 512
     N = 16
     verts, faces, d = mesh_arrays("cow")
@@ -428,7 +429,7 @@ def test_determinism_metric_config():
     assert torch.equal(ga[1], gb[1]) and torch.equal(ga[2], gb[2])
     dv = (ga[0] - gb[0]).abs().max().item()
     print(f"[determinism] vertex grad run-to-run max |diff| = {dv:.3e} (scale {ga[0].abs().max().item():.3e})")
-    assert dv <= 1e-5 * max(1.0, ga[0].abs().max().item())
+    assert torch.equal(ga[0], gb[0]), "vertex gradients differ between two identical runs"
 
 
 def test_large_image_count_scan_fill_path():

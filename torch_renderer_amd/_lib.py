@@ -25,6 +25,7 @@ MR_OUT_SIL = 2
 MR_OUT_RGB = 4
 MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
 MR_OUT_SIL_RGBA = 32  # silhouette as (N,H,W,4) RGBA (1, 1, 1, alpha), fused render path
+MR_OUT_ZBUF = 64  # depth output = MeshRasterizer's zbuf[..., 0] (background -1), fused render path
 MR_FRAG_SORTED = 64  # mr_shade_fragments_*: empty slots follow the filled ones (this library's rasterizer)
 MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
 
@@ -129,11 +130,14 @@ _SIGS = [
                                            _VP, _I64, ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _SZ, _VP, _VP,
                                            _VP, _VP, _VP, _VP, _VP, _I64, _VP]),
     ("mr_pose_loss_workspace", _SZ, [_I64]),
-    ("mr_pose_loss_forward", _I32, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float, _VP,
-                                    _VP, _SZ, _VP]),
-    ("mr_pose_loss_backward", _I32, [_VP, _VP, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float, _VP,
-                                     _VP, _VP, _VP, _VP, _VP]),
+    ("mr_pose_loss_forward", _I32, [_VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float,
+                                    _VP, _VP, _SZ, _VP]),
+    ("mr_pose_loss_backward", _I32, [_VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float,
+                                     _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("mr_quaternion_to_matrix", _I32, [_VP, _I64, _I64, _VP, _VP]),
+    ("mr_quaternion_to_matrix_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
+    ("mr_workspace_counters", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_timing_enable", _I32, [_I32]),
     ("mr_timing_read", _I32, [_VP, _VP, _I32]),
     ("mr_timing_kernel_name", ctypes.c_char_p, [_I32]),

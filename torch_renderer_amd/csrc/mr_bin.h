@@ -844,8 +844,9 @@ __global__ void __launch_bounds__(256) k_bin_rect_fv(SetupParams P, const float*
 }
 
 struct ViewBinParams {
-  int T, TX, mfpb, clipz;
+  int T, TX, TY, mfpb, clipz;
   int nviews;
+  int bands;   // workgroups per view: band b bins tile rows [b TY / bands, (b + 1) TY / bands)
   int ranges;  // write cnt / start per tile (read by k_raster_k, K > 1)
   int64_t list_cap, NF;
   const uint32_t* rects;
@@ -868,24 +869,42 @@ struct ViewBinParams {
   int64_t Fs;
   int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
   int stage_cap;  // list entries of a view staged in LDS (after the histogram)
+  // fused path: per-(record, tile) gradient rows for the deterministic backward (rbase NULL: none)
+  int* rbase;
+  uint8_t* rtag;
+  int64_t rows_cap;
 };
 
-template <typename Fn>
-MR_DEV void rect_tiles(uint32_t r, int TX, Fn&& fn) {
+// Tiles of a rectangle (0 for MR_RECT_NONE).
+MR_DEV int rect_size(uint32_t r) {
   const int tx0 = r & 255, tx1 = (r >> 8) & 255, ty0 = (r >> 16) & 255, ty1 = r >> 24;
-  for (int ty = ty0; ty <= ty1; ++ty)
-    for (int tx = tx0; tx <= tx1; ++tx) fn(ty * TX + tx);
+  return tx1 < tx0 ? 0 : (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
 }
 
+// The band-local tiles (ty - by0) * TX + tx of rectangle r inside tile rows [by0, by1).
+template <typename Fn>
+MR_DEV void rect_tiles(uint32_t r, int TX, int by0, int by1, Fn&& fn) {
+  const int tx0 = r & 255, tx1 = (r >> 8) & 255;
+  const int ty0 = max((int)((r >> 16) & 255), by0), ty1 = min((int)(r >> 24), by1 - 1);
+  for (int ty = ty0; ty <= ty1; ++ty)
+    for (int tx = tx0; tx <= tx1; ++tx) fn((ty - by0) * TX + tx);
+}
+
+// One 1024-thread workgroup per (view, band of tile rows): every band reads all of the view's
+// rectangles (4 B each, L2-resident after the first band) and bins the part of each inside its rows.
+// Bands share nothing, so a view's binning runs on `bands` CUs at once instead of one (a single
+// workgroup per view was the fragment pass's 26-us critical path with 64 views on 256 CUs).
 MR_DEV void bin_view_body(const ViewBinParams& P) {
-  extern __shared__ __attribute__((aligned(16))) int hist[];  // T (+ T/64 pad): counts, then fill cursors
+  extern __shared__ __attribute__((aligned(16))) int hist[];  // Tb (+ Tb/64 pad): counts, then fill cursors
   __shared__ int part[16];
   __shared__ long long base[3];
+  __shared__ int rows_base;
   __shared__ int nmulti;
   __shared__ int multi_slot[MR_SCAN_MULTI];
-  const int n = blockIdx.x, t = threadIdx.x;
-  if (n >= (int)P.nviews) {  // ShadeRec workgroups (they run on the CUs the views leave idle)
-    const int64_t f = (int64_t)(n - P.nviews) * 1024 + t;
+  const int blk = blockIdx.x, t = threadIdx.x;
+  const int B = P.bands;
+  if (blk >= P.nviews * B) {  // ShadeRec workgroups (they run on the CUs the views leave idle)
+    const int64_t f = (int64_t)(blk - P.nviews * B) * 1024 + t;
     if (f < P.Fs) {
       ShadeRec R;
       make_shade_rec(P.S, (uint32_t)f, R);
@@ -893,13 +912,16 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     }
     return;
   }
-  // tile tt lives at hist[tt + tt / 64] (the scan's per-thread runs of C tiles spread over the
+  const int n = blk / B, b = blk - n * B;
+  const int by0 = b * P.TY / B, by1 = (b + 1) * P.TY / B;  // this band's tile rows
+  const int T0 = by0 * P.TX, Tb = (by1 - by0) * P.TX;      // its first tile and tile count
+  // band tile lt lives at hist[lt + lt / 64] (the scan's per-thread runs of C tiles spread over the
   // banks); a view's rectangles are read in chunks of MR_VIEW_RPT per thread, all loads of a
   // chunk in flight together, and a view of one chunk keeps them in registers for the fill.
   const int j = t;
   const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
-  for (int i = t; i < P.T + (P.T >> 6); i += 1024) hist[i] = 0;
+  for (int i = t; i < Tb + (Tb >> 6); i += 1024) hist[i] = 0;
   if (t == 0) nmulti = 0;
   lds_barrier();
   const int nq = P.clipz ? 2 : 1;
@@ -920,12 +942,13 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
+      for (int q = 0; q < 2; ++q)
+        rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
   }
   lds_barrier();
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
-  const int C = (P.T + 1023) / 1024;
-  const int t0 = min(t * C, P.T), t1 = min(t0 + C, P.T);
+  const int C = (Tb + 1023) / 1024;
+  const int t0 = min(t * C, Tb), t1 = min(t0 + C, Tb);
   int le = 0, my_u = 0, my_s = 0;
   for (int tt = t0; tt < t1; ++tt) {
     const int cc = hist[tt + (tt >> 6)];
@@ -942,23 +965,27 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
   } else if (t == 64) {
+    // slot range of (view, band): the R/T reduction walks a view's bands in order
     const int b1 = atomicAdd(&P.ctr[CTR_SLOTS], as);
     base[1] = b1;
-    P.vslot[n] = b1;
-    P.vslot[P.nviews + n] = as;
+    P.vslot[blk] = b1;
+    P.vslot[P.nviews * B + blk] = as;
   } else if (t == 128) {
     base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
   }
   lds_barrier();
   const long long vb = base[2];
-  if (t == 0) P.vbase[n] = (int)(vb < 0x7fffffffll ? vb : 0x7fffffffll);
+  // tile list starts are absolute pool positions here (view base 0): a view's bands take separate
+  // ranges of the pool. (Readers use vbase[n] + start[tile], as on the count -> scan path.)
+  if (t == 0 && b == 0) P.vbase[n] = 0;
   int u0 = (int)base[0] + iu - my_u, slot = (int)base[1] + is - my_s;
   for (int tt = t0, ex = ex0; tt < t1; ++tt) {
     const int cc = hist[tt + (tt >> 6)];
-    const int gt = n * P.T + tt;
+    const int gt = n * P.T + T0 + tt;
     if (P.ranges) {
       P.cnt[gt] = cc;
-      P.start[gt] = ex;
+      // clamped: a list past the pool's end keeps start + cnt > list_cap (its overflow test)
+      P.start[gt] = (int)min(vb + ex, (long long)P.list_cap);
     }
     const bool mo = P.mfpb > 0 && cc > P.mfpb;
     const int nu = cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
@@ -990,10 +1017,48 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
-  // fill: the view's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
+  if (P.rbase) {
+    // Gradient rows (fused render path): each record's tile rectangle gets consecutive rows, its k-th
+    // tile (row-major inside the rectangle) at rbase[rid] + k; the backward writes the row of every
+    // (record, tile) it shades and k_face_reduce sums a face's rows in a fixed order (deterministic
+    // vertex gradients, no float atomics). The records of chunk slot k belong to band k % bands; one
+    // row allocation per workgroup and chunk; the rows' tags are cleared here.
+#pragma unroll 1
+    for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+      if (vcount > 1024 * MR_VIEW_RPT) load_chunk(i0);  // a view of one chunk: still in registers
+      int mine = 0;
+#pragma unroll
+      for (int k = 0; k < MR_VIEW_RPT; ++k)
+        if (k % B == b)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) mine += rect_size(rr[k][q]);
+      int tot;
+      const int incl = block_incl_sum<true>(mine, part, tot);
+      if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
+      lds_barrier();
+      const long long wb = rows_base;
+      long long rb = wb + incl - mine;
+#pragma unroll
+      for (int k = 0; k < MR_VIEW_RPT; ++k)
+        if (k % B == b)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            const int i = i0 + k * 1024 + j;
+            if (q < nq && i < vcount) {
+              const int sz = rect_size(rr[k][q]);
+              P.rbase[(q ? P.NF : 0) + f0 + i] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: rows full (atomics)
+              rb += sz;
+            }
+          }
+      for (int i = t; i < tot; i += 1024)
+        if (wb + i < P.rows_cap) P.rtag[wb + i] = 0;
+      lds_barrier();  // rows_base is rewritten by the next chunk
+    }
+  }
+  // fill: the band's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
   // staged in LDS and stored as consecutive lines afterwards (scattered 4-B stores issue one
-  // lane per cycle), the rest (a view larger than the stage) go straight to the pool
-  int* stage = hist + ((P.T + (P.T >> 6) + 3) & ~3);
+  // lane per cycle), the rest (a band larger than the stage) go straight to the pool
+  int* stage = hist + ((Tb + (Tb >> 6) + 3) & ~3);
   const int lst = min(te, P.stage_cap);
   const bool one = vcount <= 1024 * MR_VIEW_RPT;  // the rectangles are still in registers
 #pragma unroll 1
@@ -1004,7 +1069,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int rid = (int)((q ? P.NF : 0) + f0 + i0 + k * 1024 + j);
-        rect_tiles(rr[k][q], P.TX, [&](int tt) {
+        rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) {
           // an overflowing tile's cursor starts at MR_CURSOR_OFF >= list_cap: no store, and no
           // read of the cursor before the atomic
           const int pos = atomicAdd(&hist[tt + (tt >> 6)], 1);

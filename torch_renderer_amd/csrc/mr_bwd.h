@@ -347,10 +347,122 @@ struct RenderBwdParams {
   const ClipRec* crec;
   float zc;      // z_clip_value (clipped records only)
   const ViewRec* views;
-  float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows]
+  float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows] (float atomics: the
+                 // count -> scan path, and records whose rows did not fit)
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
   const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
+  // deterministic face gradients (k_bin_view's rows; rbase NULL: float atomics into gface)
+  const int* rbase;
+  const uint32_t* rects;
+  uint8_t* rtag;
+  float* rrows;
 };
+
+// Order the 64 pixels of a slot by winning record (groups in order of first appearance, pixels of a
+// group in tile order): each (tile, record) then forms ONE run of consecutive lanes, so the per-face
+// rows of a tile come out of one segmented scan, one row per (tile, record) — 13.5 instead of 28.7
+// runs per tile on the bench workload — and can be written with plain stores. The loop runs once
+// per distinct record of the tile (uniform, scalar bookkeeping). Returns the tile pixel this lane
+// takes; f becomes that pixel's record.
+MR_DEV int sort_slot_pixels(int& f, int lane, int* lperm) {
+  unsigned long long rem = ~0ull;
+  int pos = 0, base = 0;
+  while (rem) {
+    const int l = (int)__builtin_ctzll(rem);
+    const int key = __builtin_amdgcn_readlane(f, l);
+    const unsigned long long m = __ballot(f == key);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    pos = f == key ? base + below : pos;
+    base += __popcll(m);
+    rem &= ~m;
+  }
+  lperm[pos] = lane;
+  wave_lds_sync();
+  const int src = lperm[lane];
+  f = __builtin_amdgcn_ds_bpermute(src << 2, f);
+  wave_lds_sync();  // lperm is rewritten for the next slot
+  return src;
+}
+
+// seg_stage for the row path: key = record id (runs are whole (tile, record) groups after
+// sort_slot_pixels), q = the run's gradient row (-1: float atomics into gface row `face`). The run
+// totals are staged in LDS with their row / face; the row's tag is set by the emitting lane.
+template <int ACC>
+MR_DEV int seg_stage_rows(int key, int face, int q, float (&v)[ACC], float* lrow, int* lkey, int* lq,
+                          uint8_t* __restrict__ rtag) {
+  const int lane = threadIdx.x & 63;
+  const int prev = dpp_wave_shr1(key, -2);
+  const bool head = lane == 0 || key != prev;
+  const int d = lane - wave_incl_max(head ? lane : 0);
+  const int r = lane & 15;
+  float sh;
+  if (__ballot(d >= 1)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x111, 0xf>(v[i]); v[i] = d >= 1 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 2)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x112, 0xf>(v[i]); v[i] = d >= 2 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 4)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x114, 0xf>(v[i]); v[i] = d >= 4 ? sh : v[i]; }
+  }
+  if (__ballot(d >= 8)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x118, 0xf>(v[i]); v[i] = d >= 8 ? sh : v[i]; }
+  }
+  if (__ballot(d > r)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x142, 0xa>(v[i]); v[i] = d > r ? sh : v[i]; }
+  }
+  if (__ballot(d > lane - 32)) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) { sh = v[i] + dppf<0x143, 0xc>(v[i]); v[i] = d > lane - 32 ? sh : v[i]; }
+  }
+  const int next = dpp_wave_shl1(key, -2);
+  const bool emit = (lane == 63 || key != next) && key >= 0;
+  const unsigned long long m = __ballot(emit);
+  if (emit) {
+    const int slot = __popcll(m & ((1ull << lane) - 1ull));
+    lkey[slot] = face;
+    lq[slot] = q;
+    if (q >= 0) rtag[q] = 1;
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
+  }
+  wave_lds_sync();
+  return __popcll(m);
+}
+// seg_flush for the row path: plain stores of whole rows (every component: the rows are not
+// cleared), float atomics for the runs without a row. Straight-line, as seg_flush.
+template <int ACC>
+MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__ gface, const float* lrow,
+                           const int* lkey, const int* lq) {
+  int lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  const int tot = nt * ACC;
+  constexpr int qd = 64 / ACC, m = 64 - qd * ACC;
+  int r = lane / ACC, c = lane - r * ACC;
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) {
+    if (64 * i < tot) {
+      const int j = 64 * i + lane;
+      if (j < tot) {
+        const float x = lrow[j];
+        const int q = lq[r];
+        if (q >= 0) rows[(int64_t)q * ACC + c] = x;
+        else if (x != 0.0f) atomicAdd(gface + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
+      }
+    }
+    c += m;
+    const bool wrap = c >= ACC;
+    c = wrap ? c - ACC : c;
+    r += wrap ? qd + 1 : qd;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  wave_lds_sync();
+}
 
 MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& px, int& py) {
   n = gt / P.T;
@@ -370,12 +482,16 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // phi copies wait on the load right away, which defeats the prefetch.
 __device__ float g_zero4[4];
 MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
-                             float4& fr) {
+                             float4& fr, int& rb, uint32_t& rect) {
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
   r = load_rec(P.recs, f < 0 ? 0 : f);
   fr = P.frec[(int64_t)slot * 64 + lane];
+  const int* pr = P.rbase ? P.rbase + (f < 0 ? 0 : f) : (const int*)g_zero4;
+  const uint32_t* pt = P.rbase ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
+  rb = *pr;
+  rect = *pt;
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
   const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
@@ -440,6 +556,8 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   const RenderBwdParams& P = P0;
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
+  __shared__ int lq[4][64];
+  __shared__ int lperm[4][64];
   __shared__ float4 lrec[4][MR_BWD_REC][64];
   const bool lut = stage_tex_lut(P.S);  // the u8 texture table in LDS
   const int lane = threadIdx.x & 63;
@@ -464,34 +582,41 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   FaceRec r_c;
   float g_c[5];
   float4 fr_c;
-  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
+  int rb_c;
+  uint32_t rect_c;
+  // lane -> tile pixel p_c of the slot in flight (pixels grouped by record, sort_slot_pixels)
+  int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
+  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rb_c, rect_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
   for (; s < send; s += G) {
     const RenderBwdParams& P = kernarg_params<RenderBwdParams>();  // see kernarg_params
-    const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c;
+    const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c, p = p_c;
     const FaceRec r = r_c;
     const float4 frag = fr_c;
+    const int rb = rb_c;
+    const uint32_t rect = rect_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
     gt_c = gt_n;
     f_c = f_n;
     sl_c = sl_n;
-    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, lane, r_c, g_c, fr_c);
+    p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
+    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rb_c, rect_c);
     sc = min(s + 2 * G, slast);
     sl_n = sc;
     gt_n = P.stile[sc + lz];
     f_n = P.sface[(int64_t)sc * 64 + lane];
     int n, px, py;
-    slot_pixel(P, gt, lane, n, px, py);
+    slot_pixel(P, gt, p, n, px, py);
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (f >= 0) {
       PixGeom Gm;
       load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
       const float gD = gin[0], gS = gin[1];
       float gC[3] = {gin[2], gin[3], gin[4]};
-      const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, lane) : 0.0f;
+      const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, p) : 0.0f;
       FragEval e;
       float4 o[MR_BWD_REC];
       // the forward's fragment (k_shade<1> wrote the winner's barycentrics, original-face ones for a
@@ -538,7 +663,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
-      seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+      seg_flush_rows<ACC>(nt_prev, P.rrows, P.gface, lrow[wave], lkey[wave], lq[wave]);
       if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -581,35 +706,89 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         }
       }
     }
-    nt_prev = seg_stage<ACC>(key, row, lrow[wave], lkey[wave]);
+    // the run's gradient row: tile (tx, ty) is the k-th of the record's rectangle (row-major), its row
+    // rbase + k; -1 (float atomics) without rows, when the record's rows did not fit, or for a tile
+    // outside the rectangle (not expected: a winning pixel lies inside the record's padded bbox)
+    int q = -1;
+    if (P.rbase && f >= 0 && rb >= 0) {
+      const int t = gt - n * P.T;
+      const int ty = t / P.TX, tx = t - ty * P.TX;
+      const int rx0 = rect & 255, rx1 = (rect >> 8) & 255, ry0 = (rect >> 16) & 255, ry1 = rect >> 24;
+      if (tx >= rx0 && tx <= rx1 && ty >= ry0 && ty <= ry1) q = rb + (ty - ry0) * (rx1 - rx0 + 1) + (tx - rx0);
+    }
+    nt_prev = seg_stage_rows<ACC>(f >= 0 ? f : -1, key, q, row, lrow[wave], lkey[wave], lq[wave], P.rtag);
     rt_prev = rt_partial(gR, gT, lane);
     s_prev = s;
   }
   if (nt_prev >= 0) {
-    seg_flush<ACC>(nt_prev, P.gface, lrow[wave], lkey[wave]);
+    seg_flush_rows<ACC>(nt_prev, P.rrows, P.gface, lrow[wave], lkey[wave], lq[wave]);
     if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
   }
+}
+
+// Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of its records'
+// (tile) rows over the views — one wave per face, lane = view (views 64 apart summed in order per
+// lane, then a fixed DPP tree), each lane walking its record's rectangle row by row and adding the
+// rows the backward tagged — plus whatever the backward had to add with float atomics (gface rows of
+// records without rows, zero otherwise). Shared mesh: records n F + f (and NF + n F + f for a split
+// face's second triangle); distinct meshes (F_shared = 0): record f (and NF + f).
+template <int ACC>
+__global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip,
+                                                     const int* __restrict__ rbase, const uint32_t* __restrict__ rects,
+                                                     const uint8_t* __restrict__ rtag, const float* __restrict__ rows,
+                                                     const float* __restrict__ gatom, float* __restrict__ gout) {
+  __shared__ float red[4][ACC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t f = (int64_t)blockIdx.x * 4 + wave;
+  if (f >= F) return;  // uniform over the wave (no workgroup barrier below)
+  float acc[ACC];
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
+  const int nv = F_shared ? N : 1;
+  for (int n = lane; n < nv; n += 64) {
+    for (int q = 0; q <= clip; ++q) {
+      const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
+      const int rb = rbase[rid];
+      const int sz = rb >= 0 ? rect_size(rects[rid]) : 0;
+      for (int k = 0; k < sz; ++k) {
+        if (!rtag[rb + k]) continue;
+        const float* x = rows + (int64_t)(rb + k) * ACC;
+#pragma unroll
+        for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < ACC; ++i) {
+    const float t = wave_sum_f_dpp(acc[i]);
+    if (lane == 63) red[wave][i] = t;
+  }
+  wave_lds_sync();
+  if (lane < ACC) gout[f * ACC + lane] = red[wave][lane] + gatom[f * ACC + lane];
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
 // out (N,12) PyTorch3D-frame R/T grads, or (gRcv, gtcv) non-null: the same grads written
 // straight in the OpenCV frame (k_view_grads_to_opencv's chain rule, saving its launch).
-MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N,
+// vslot holds (first slot, count) of each (view, band) range: N * bands firsts, then the counts.
+MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N, int bands,
                            float* __restrict__ out, float* __restrict__ gRcv, float* __restrict__ gtcv, int n) {
   __shared__ float sm[12][4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int s0 = vslot[n], ns = vslot[N + n];
   // each thread sums whole 48-B partial rows (three 16-B loads in flight together instead of 12
   // dependent passes over the rows); per component the order is the same as a per-component loop
   float acc[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
-  for (int t = threadIdx.x; t < ns; t += 256) {
-    const float4* q = (const float4*)(part + ((int64_t)s0 + t) * 12);
-    const float4 a = q[0], b = q[1], c = q[2];
-    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-    acc[4] += b.x; acc[5] += b.y; acc[6] += b.z; acc[7] += b.w;
-    acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+  for (int b = 0; b < bands; ++b) {
+    const int s0 = vslot[n * bands + b], ns = vslot[N * bands + n * bands + b];
+    for (int t = threadIdx.x; t < ns; t += 256) {
+      const float4* q = (const float4*)(part + ((int64_t)s0 + t) * 12);
+      const float4 a = q[0], c4 = q[1], c = q[2];
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
+      acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 12; ++i) {
@@ -631,7 +810,7 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
 }
 
 __global__ void __launch_bounds__(256) k_rt_reduce(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                   int N, float* __restrict__ out, float* __restrict__ gRcv,
+                                                   int N, int bands, float* __restrict__ out, float* __restrict__ gRcv,
                                                    float* __restrict__ gtcv) {
-  rt_reduce_view(part, vslot, N, out, gRcv, gtcv, blockIdx.x);
+  rt_reduce_view(part, vslot, N, bands, out, gRcv, gtcv, blockIdx.x);
 }

@@ -240,10 +240,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const bool fast_ok = !(blur > 0.0f);
   const int H = P.H, W = P.W;
   const int64_t HW = (int64_t)H * W;
-#ifdef MR_XP_STAMP  // per-tile timing for tools/kp_stamps.py (experiment builds only)
-  const unsigned long long t_start = wall_clock64();
-  int xp_passes = 0, xp_drains = 0;
-#endif
   const int gt = P.stile[s];
   const int n = gt / P.T, t = gt - n * P.T;
   const int ty = t / P.TX, tx = t - ty * P.TX;
@@ -258,7 +254,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const int count = ovf ? (int)(vcnt < 0x7fffffffll ? vcnt : 0x7fffffffll) : cc;
   const int xe = min(x0 + MR_TS, W) - 1, ye = min(y0 + MR_TS, H) - 1;  // the tile's last pixels inside the image
   const bool zsorted = MR_KP_SORT > 0 && !ovf && count > 64 && count <= MR_KP_SORT;
-  if (zsorted) kp_depth_order(P, S, perm, vb + ex, count, lane);
+  if (zsorted) {
+    kp_depth_order(P, S, perm, vb + ex, count, lane);
+    if (lane == 0) atomicAdd(&P.ctr[CTR_ZWALK], 1);  // tiles walked near-to-far (mr_workspace_stats out[4])
+  }
   unsigned long long q[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) q[k] = MR_KEY_EMPTY;
@@ -284,9 +283,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   // than NS keys, only the first NS positions can change and the shift runs NS steps, not KP
   // (most lists hold a few keys: the full KP-step shift was ~half of the kernel).
   auto drain = [&]() {
-#ifdef MR_XP_STAMP
-    ++xp_drains;
-#endif
     wave_lds_sync();
     const int c = S.bcnt[lane];
     const int mc = __builtin_amdgcn_readlane(wave_incl_max(c), 63);
@@ -351,9 +347,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 #pragma unroll 1
     for (int pb = 0; pb < NP;) {
       if (mb > MR_KP_BC - MR_KP_ROOM) drain();
-#ifdef MR_XP_STAMP
-      ++xp_passes;
-#endif
       // the entry straddling pb, and the first entry past what the buckets can still take
       const int first = 63 - __builtin_clzll(__ballot(np > 0 && pexcl <= pb));
       const int lim = first + (MR_KP_BC - mb);
@@ -437,13 +430,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       ((float4*)P.sil)[q4] = make_float4(1.0f, 1.0f, 1.0f, 1.0f - alpha);
     }
     P.spix[(int64_t)s * 64 + lane] = make_float4(alpha_nz, __int_as_float(nzero), __int_as_float(kzero), 0.0f);
-#ifdef MR_XP_STAMP
-    const unsigned long long t_end = wall_clock64();
-    if (lane < 4) {
-      const int v = lane == 0 ? (int)(unsigned)t_start : lane == 1 ? (int)(unsigned)t_end : lane == 2 ? xp_passes : xp_drains;
-      P.sil[(n * HW + (int64_t)y0 * W + x0 + lane) * 4] = __int_as_float(v);
-    }
-#endif
     return;
   }
   if (!in_img) return;

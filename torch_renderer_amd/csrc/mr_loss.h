@@ -15,6 +15,7 @@
 struct PoseLossParams {
   const float* depth;
   const float* sil;
+  int64_t sil_stride;  // 1, or 4: channel 3 of an RGBA image (sil points at element 3)
   const float* rgb;
   int64_t rgb_stride;  // floats between consecutive pixels' colours (3, or 4 for an RGBA view)
   const uint8_t* mask;
@@ -48,7 +49,7 @@ __global__ void __launch_bounds__(256) k_pose_loss_partial(PoseLossParams P, flo
   int cnt = 0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
     const bool m = P.mask[i] != 0;
-    s_l1 += fabsf(P.sil[i] - (m ? 1.0f : 0.0f));
+    s_l1 += fabsf(P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f));
     if (m) {
       s_h += huber_val(P.depth[i] - P.depth_ref[i], P.delta);
       ++cnt;
@@ -108,13 +109,69 @@ __global__ void __launch_bounds__(256) k_pose_loss_bwd(PoseLossParams P, const f
   if (i >= P.npix) return;
   const float g = *g_total;
   const bool m = P.mask[i] != 0;
-  const float e = P.sil[i] - (m ? 1.0f : 0.0f);
-  g_sil[i] = g * ((e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f)) / (float)P.npix);
+  const float e = P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f);
+  const float gs = g * ((e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f)) / (float)P.npix);
+  // an RGBA silhouette's gradient is the whole (npix, 4) image's: zero RGB, one 16-B store per pixel
+  if (P.sil_stride == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
+  else g_sil[i] = gs;
   g_depth[i] = m ? g * (huber_grad(P.depth[i] - P.depth_ref[i], P.delta) / (float)*count) : 0.0f;
   const float s = g * P.w_color * (2.0f / (float)(3 * P.npix));
   const float* c = P.rgb + i * P.rgb_stride;
   const float* r = P.rgb_ref + 3 * i;
-  g_rgb[3 * i] = s * (c[0] - r[0]);
-  g_rgb[3 * i + 1] = s * (c[1] - r[1]);
-  g_rgb[3 * i + 2] = s * (c[2] - r[2]);
+  const float g0 = s * (c[0] - r[0]), g1 = s * (c[1] - r[1]), g2 = s * (c[2] - r[2]);
+  if (P.rgb_stride == 4) {
+    ((float4*)g_rgb)[i] = make_float4(g0, g1, g2, 0.0f);
+  } else {
+    g_rgb[3 * i] = g0;
+    g_rgb[3 * i + 1] = g1;
+    g_rgb[3 * i + 2] = g2;
+  }
+}
+
+// upstream quaternion_to_matrix, one thread per quaternion (torch's elementwise operation order, no
+// contraction: bitwise the torch formula of transforms.quaternion_to_matrix).
+__global__ void __launch_bounds__(256) k_quat_to_matrix(const float* __restrict__ q, int64_t qs, int64_t N,
+                                                        float* __restrict__ R) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const float r = q[n * qs], i = q[n * qs + 1], j = q[n * qs + 2], k = q[n * qs + 3];
+  const float two_s = 2.0f / (((r * r + i * i) + j * j) + k * k);
+  float* o = R + 9 * n;
+  o[0] = 1.0f - two_s * (j * j + k * k);
+  o[1] = two_s * (i * j - k * r);
+  o[2] = two_s * (i * k + j * r);
+  o[3] = two_s * (i * j + k * r);
+  o[4] = 1.0f - two_s * (i * i + k * k);
+  o[5] = two_s * (j * k - i * r);
+  o[6] = two_s * (i * k - j * r);
+  o[7] = two_s * (j * k + i * r);
+  o[8] = 1.0f - two_s * (i * i + j * j);
+}
+
+// Its backward: R_ab = [a == b] + two_s * M_ab(q) with M quadratic in q and two_s = 2 / |q|^2, so
+// dL/dq = two_s * sum_ab G_ab dM_ab/dq - (two_s^2 (sum_ab G_ab M_ab)) q.
+__global__ void __launch_bounds__(256) k_quat_to_matrix_bwd(const float* __restrict__ q, int64_t qs,
+                                                            const float* __restrict__ gR, int64_t N,
+                                                            float* __restrict__ gq) {
+  const int64_t n = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  const float r = q[n * qs], i = q[n * qs + 1], j = q[n * qs + 2], k = q[n * qs + 3];
+  const float two_s = 2.0f / (((r * r + i * i) + j * j) + k * k);
+  const float* G = gR + 9 * n;
+  // M (R = I + two_s M): diagonal -(..), off-diagonal products
+  const float M[9] = {-(j * j + k * k), i * j - k * r, i * k + j * r,
+                      i * j + k * r, -(i * i + k * k), j * k - i * r,
+                      i * k - j * r, j * k + i * r, -(i * i + j * j)};
+  float gm = 0.0f;
+  for (int a = 0; a < 9; ++a) gm += G[a] * M[a];
+  // sum_ab G_ab dM_ab / d(r, i, j, k)
+  const float dr = (-k * G[1] + j * G[2] + k * G[3] - i * G[5] - j * G[6] + i * G[7]);
+  const float di = (j * G[1] + k * G[2] + j * G[3] - 2.0f * i * G[4] - r * G[5] + k * G[6] + r * G[7] - 2.0f * i * G[8]);
+  const float dj = (-2.0f * j * G[0] + i * G[1] + r * G[2] + i * G[3] + k * G[5] - r * G[6] + k * G[7] - 2.0f * j * G[8]);
+  const float dk = (-2.0f * k * G[0] - r * G[1] + i * G[2] + r * G[3] - 2.0f * k * G[4] + j * G[5] + i * G[6] + j * G[7]);
+  const float c = two_s * two_s * gm;  // d two_s / dq = -two_s^2 q
+  gq[4 * n] = two_s * dr - c * r;
+  gq[4 * n + 1] = two_s * di - c * i;
+  gq[4 * n + 2] = two_s * dj - c * j;
+  gq[4 * n + 3] = two_s * dk - c * k;
 }

@@ -137,6 +137,9 @@ extern "C++" {
 #ifndef MR_VIEW_LDS
 #define MR_VIEW_LDS 98304  // k_bin_view's LDS: the tile histogram + the list stage
 #endif
+#ifndef MR_VIEW_LDS_BANDED
+#define MR_VIEW_LDS_BANDED 65536  // ... with several bands per view: two workgroups per CU
+#endif
 static size_t view_lds_bytes() {
   static size_t b = 0;
   if (!b) {
@@ -156,10 +159,19 @@ static int num_cus() {
   }
   return cus;
 }
+// Workgroups (bands of tile rows) per view of the per-view binning: enough for the views to cover
+// the CUs (64 views -> 4 bands on 256 CUs), at most MR_BANDS_MAX and one tile row per band. A pure
+// function of the batch geometry: the backward's R/T reduction walks the same (view, band) ranges.
+static int bin_bands(int64_t N, const BinGeom& g) {
+  int64_t b = (int64_t)num_cus() / (N > 0 ? N : 1);
+  if (b > MR_BANDS_MAX) b = MR_BANDS_MAX;
+  if (b > g.TY) b = g.TY;
+  return b < 1 ? 1 : (int)b;
+}
 // Background chunks the k_bin_view launch takes over (chunks of 64 lanes x 4 pixels when W % 4 == 0,
-// else 64 pixels); 0 when the views leave no CU idle.
-static int64_t bg_chunks(int64_t N, int64_t sb, int H, int W, int mode) {
-  const int64_t nbg = (int64_t)num_cus() - N - sb;
+// else 64 pixels); 0 when the binning workgroups (nbin = views x bands) leave no CU idle.
+static int64_t bg_chunks(int64_t N, int64_t nbin, int64_t sb, int H, int W, int mode) {
+  const int64_t nbg = (int64_t)num_cus() - nbin - sb;
   if (nbg <= 0) return 0;
   const int64_t HW = (int64_t)H * W;
   const int64_t nchunks = N * ((W & 3) == 0 ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
@@ -181,26 +193,34 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.srec = w.srec;
     V.Fs = F;
     sb = ceil_div(F, 1024);
+    // the fused render path: per-(record, tile) gradient rows for the deterministic backward
+    V.rbase = w.rbase;
+    V.rtag = w.rtag;
+    V.rows_cap = rows_cap(g, S->tex_kind == 1 ? 27 : 18);
   }
   V.nsrec_wg = (int)sb;
-  V.T = g.T; V.TX = g.TX; V.mfpb = g.mfpb; V.clipz = SP.clipz;
+  V.T = g.T; V.TX = g.TX; V.TY = g.TY; V.mfpb = g.mfpb; V.clipz = SP.clipz;
+  const int B = bin_bands(N, g);
+  V.bands = B;
+  const int64_t nbin = N * B;
   V.list_cap = g.list_cap; V.NF = SP.NF;
   V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
   V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
   V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
-  const size_t hist_b = sizeof(int) * (size_t)((g.T + (g.T >> 6) + 3) & ~3);
-  const size_t shm = std::max(hist_b, view_lds_bytes());
+  const int Tb = ((g.TY + B - 1) / B) * g.TX;  // tiles of the largest band
+  const size_t hist_b = sizeof(int) * (size_t)((Tb + (Tb >> 6) + 3) & ~3);
+  const size_t shm = std::max(hist_b, B > 1 ? (size_t)MR_VIEW_LDS_BANDED : view_lds_bytes());
   V.stage_cap = (int)((shm - hist_b) / sizeof(int));
   if constexpr (MODE >= 0) {
-    const int64_t nbg = (int64_t)num_cus() - N - sb;
+    const int64_t nbg = (int64_t)num_cus() - nbin - sb;
     if (Pf && nbg > 0 && (MODE != 0 || Pf->K == 1)) {
-      Pf->fill_first = (int)bg_chunks(N, sb, Pf->H, Pf->W, MODE);
-      MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<MODE, CH><<<(unsigned)(N + sb + nbg), 1024, shm, st>>>(V, *Pf)));
+      Pf->fill_first = (int)bg_chunks(N, nbin, sb, Pf->H, Pf->W, MODE);
+      MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<MODE, CH><<<(unsigned)(nbin + sb + nbg), 1024, shm, st>>>(V, *Pf)));
       MR_CHECK_LAUNCH("k_bin_view");
       return MR_OK;
     }
   }
-  MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<<<(unsigned)(N + sb), 1024, shm, st>>>(V)));
+  MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<<<(unsigned)(nbin + sb), 1024, shm, st>>>(V)));
   MR_CHECK_LAUNCH("k_bin_view");
   return MR_OK;
 }
@@ -211,7 +231,7 @@ int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W,
   BinGeom g = bin_geom(H, W, N, N * (F > 0 ? F : 1), 0);
   if (!view_binning(g, N, N * (F > 0 ? F : 1))) return 0;
   const int64_t sb = mode == 1 ? ceil_div(F, 1024) : 0;
-  const int64_t px = bg_chunks(N, sb, H, W, mode) * ((W & 3) == 0 ? 256 : 64);
+  const int64_t px = bg_chunks(N, N * bin_bands(N, g), sb, H, W, mode) * ((W & 3) == 0 ? 256 : 64);
   return std::min<int64_t>(px, N * (int64_t)H * W);
 }
 
@@ -337,7 +357,7 @@ int32_t mr_rasterize_meshes_world(const float* verts, int64_t V, const int32_t* 
   int64_t rect_bg0 = 0, rect_bgn = 0;
   if (s->faces_per_pixel == 1 && (s->W & 3) == 0 && MR_BG_RECT_ROWS > 0) {
     const int64_t total = N * (((int64_t)s->H * s->W / 4 + 63) / 64);
-    rect_bg0 = bg_chunks(N, 0, s->H, s->W, 0);  // = the k_bin_view share launch_bin_view takes
+    rect_bg0 = bg_chunks(N, N * bin_bands(N, g), 0, s->H, s->W, 0);  // = the k_bin_view share launch_bin_view takes
     rect_bgn = std::min<int64_t>(total - rect_bg0, (int64_t)MR_BG_RECT_ROWS * rgrid.x * 4 * MR_BG_RECT_CPW);
     if (rect_bgn > 0) {
       FB.p2f = p2f; FB.zbuf = zbuf; FB.dists = dists; FB.bary = bary;
@@ -650,6 +670,7 @@ static ShadeParams make_shade(const mr_mesh_t* m, const mr_shade_params_t* sp, c
   S.inv_gamma = 1.0f / sp->gamma;
   S.inv_zrange = 1.0f / (sp->zfar - sp->znear);
   S.inv_sigma_sil = 1.0f / sp->sigma_sil;
+  S.zbuf_mode = (sp->out_flags & MR_OUT_ZBUF) ? 1 : 0;
   return S;
 }
 
@@ -791,9 +812,9 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
   const int64_t NT = N * (int64_t)ceil_div(W, MR_TS) * ceil_div(H, MR_TS);
-  (void)F;  // the face-gradient rows are in the forward's workspace
   size_t off = align_up(sizeof(float) * 3 * (size_t)V, 256);                   // gnu
   off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);                  // rt_part
+  off = align_up(off + sizeof(float) * 27 * (size_t)(F > 0 ? F : 1), 256);     // per-face gradient totals
   return off;
 }
 
@@ -852,8 +873,11 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   float* gnu = (float*)(b + off);
   off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
   float* rt_part = (float*)(b + off);
-  // the per-face gradient rows live in the forward's workspace, which the forward cleared; a
-  // second backward over the same forward (MR_GRAD_ROWS_CLEARED not set) clears them again
+  off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);
+  float* gtot = (float*)(b + off);  // per-face totals (k_face_reduce) read by the vertex gathers
+  // float-atomic face rows (records without gradient rows) live in the forward's workspace, which
+  // the forward cleared; a second backward over the same forward (MR_GRAD_ROWS_CLEARED not set)
+  // clears them again
   float* gface = w.grows;
   if (!(sp->out_flags & MR_GRAD_ROWS_CLEARED) &&
       hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
@@ -883,6 +907,15 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.gface = gface;
   P.rt_part = rt_part;
   P.frec = w.frec;
+  // per-(record, tile) gradient rows: allocated by the per-view binning (k_bin_view) of the fused
+  // forward; the count -> scan path has none (float atomics into gface)
+  const bool vpath = view_binning(g, N, NF);
+  if (vpath) {
+    P.rbase = w.rbase;
+    P.rects = w.rects;
+    P.rtag = w.rtag;
+    P.rrows = w.rrows;
+  }
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
@@ -900,11 +933,24 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false><<<cap(f18), 256, 0, st>>>(P)));
   }
   MR_CHECK_LAUNCH("k_bwd_fused");
+  {
+    const int nb = ceil_div(m->F, 4);
+    const int clip = s->clip_z ? 1 : 0;
+    const int64_t Fs = multi ? 0 : m->F;
+    if (vpath) {
+      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      MR_CHECK_LAUNCH("k_face_reduce");
+      gface = gtot;
+    }
+  }
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V * MR_VL, 256);
-  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv)));
-  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
-  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  // the forward's slot ranges: one per (view, band) on the per-view binning, one per view otherwise
+  const int bands = view_binning(g, N, NF) ? bin_bands(N, g) : 1;
+  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv)));
+  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
@@ -1017,8 +1063,8 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   const int use_n = sp->light_kind == 0 && !P.sil;
   const int vb = ceil_div(m->V * MR_VL, 256);
   if (use_n) {
-    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
-    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
+    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
+    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
     MR_CHECK_LAUNCH("k_rt_vgrad_a");
   }
   if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, g_verts, g_vcolors);
@@ -1069,6 +1115,18 @@ int32_t mr_workspace_stats(const void* ws, int64_t N, int64_t Ftot, int32_t H, i
   return MR_OK;
 }
 
+int32_t mr_workspace_counters(const void* ws, int64_t N, int64_t Ftot, int32_t H, int32_t W, int32_t mfpb, int32_t* out8,
+                              void* stream) {
+  if (!ws || !out8 || N <= 0 || N > 65535) return set_err(MR_EINVAL, "bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  BinGeom g = bin_geom(H, W, N, Ftot > 0 ? Ftot : 1, mfpb);
+  RasterWS w = carve_raster_ws((void*)ws, N, Ftot > 0 ? Ftot : 1, H, W, g);
+  if (hipMemcpyAsync(out8, w.ctr, sizeof(int) * CTR_COUNT, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return set_err(MR_ELAUNCH, "counter copy failed");
+  return MR_OK;
+}
+
 int32_t mr_timing_enable(int32_t enable) {
   if (enable && !g_t.created) {
     for (int i = 0; i < 2 * MR_TPOOL; ++i)
@@ -1107,14 +1165,15 @@ int32_t mr_timing_read(int32_t* launches, double* total_ms, int32_t n) {
 const char* mr_timing_kernel_name(int32_t k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : ""; }
 int32_t mr_timing_kernel_count(void) { return KID_COUNT; }
 
-static int pose_loss_params(PoseLossParams& P, const float* depth, const float* sil, const float* rgb,
-                            int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
-                            int64_t npix, float delta, float w_color) {
+static int pose_loss_params(PoseLossParams& P, const float* depth, const float* sil, int64_t sil_stride,
+                            const float* rgb, int64_t rgb_stride, const uint8_t* mask, const float* depth_ref,
+                            const float* rgb_ref, int64_t npix, float delta, float w_color) {
   if (npix <= 0) return set_err(MR_EINVAL, "npix must be > 0");
   if (!depth || !sil || !rgb || !mask || !depth_ref || !rgb_ref) return set_err(MR_EINVAL, "NULL loss input");
-  if (rgb_stride < 3) return set_err(MR_EINVAL, "rgb_stride must be >= 3");
+  if (rgb_stride != 3 && rgb_stride != 4) return set_err(MR_EINVAL, "rgb_stride must be 3 or 4");
+  if (sil_stride != 1 && sil_stride != 4) return set_err(MR_EINVAL, "sil_stride must be 1 or 4");
   if (!(delta > 0.0f)) return set_err(MR_EINVAL, "huber delta must be > 0");
-  P.depth = depth; P.sil = sil; P.rgb = rgb; P.rgb_stride = rgb_stride; P.mask = mask;
+  P.depth = depth; P.sil = sil; P.sil_stride = sil_stride; P.rgb = rgb; P.rgb_stride = rgb_stride; P.mask = mask;
   P.depth_ref = depth_ref; P.rgb_ref = rgb_ref; P.npix = npix; P.delta = delta; P.w_color = w_color;
   return MR_OK;
 }
@@ -1124,11 +1183,12 @@ size_t mr_pose_loss_workspace(int64_t npix) {
   return align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256) + 256;
 }
 
-int32_t mr_pose_loss_forward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
-                             const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
-                             float delta, float w_color, float* out, void* ws, size_t ws_bytes, void* stream) {
+int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                             int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                             int64_t npix, float delta, float w_color, float* out, void* ws, size_t ws_bytes,
+                             void* stream) {
   PoseLossParams P;
-  int rc = pose_loss_params(P, depth, sil, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
+  int rc = pose_loss_params(P, depth, sil, sil_stride, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
   if (rc) return rc;
   if (!out || !ws) return set_err(MR_EINVAL, "NULL output / workspace");
   if (ws_bytes < mr_pose_loss_workspace(npix)) return set_err(MR_EWORKSPACE, "loss workspace too small");
@@ -1145,19 +1205,40 @@ int32_t mr_pose_loss_forward(const float* depth, const float* sil, const float* 
   return MR_OK;
 }
 
-int32_t mr_pose_loss_backward(const float* depth, const float* sil, const float* rgb, int64_t rgb_stride,
-                              const uint8_t* mask, const float* depth_ref, const float* rgb_ref, int64_t npix,
-                              float delta, float w_color, const float* g_total, const void* fwd_ws,
+int32_t mr_pose_loss_backward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                              int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                              int64_t npix, float delta, float w_color, const float* g_total, const void* fwd_ws,
                               float* g_depth, float* g_sil, float* g_rgb, void* stream) {
   PoseLossParams P;
-  int rc = pose_loss_params(P, depth, sil, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
+  int rc = pose_loss_params(P, depth, sil, sil_stride, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
   if (rc) return rc;
   if (!g_total || !fwd_ws || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL gradient argument");
   const char* w = (const char*)fwd_ws;
   const int64_t* count = (const int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) +
                                           align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
+  if ((sil_stride == 4 && ((uintptr_t)g_sil & 15)) || (rgb_stride == 4 && ((uintptr_t)g_rgb & 15)))
+    return set_err(MR_EINVAL, "RGBA gradient buffers must be 16-byte aligned");
   k_pose_loss_bwd<<<(unsigned)ceil_div(npix, 256), 256, 0, (hipStream_t)stream>>>(P, g_total, count, g_depth, g_sil, g_rgb);
   MR_CHECK_LAUNCH("k_pose_loss_bwd");
+  return MR_OK;
+}
+
+int32_t mr_quaternion_to_matrix(const float* q, int64_t q_stride, int64_t N, float* R, void* stream) {
+  if (N < 0 || q_stride < 4) return set_err(MR_EINVAL, "bad quaternion batch");
+  if (N == 0) return MR_OK;
+  if (!q || !R) return set_err(MR_EINVAL, "NULL argument");
+  k_quat_to_matrix<<<ceil_div(N, 256), 256, 0, (hipStream_t)stream>>>(q, q_stride, N, R);
+  MR_CHECK_LAUNCH("k_quat_to_matrix");
+  return MR_OK;
+}
+
+int32_t mr_quaternion_to_matrix_backward(const float* q, int64_t q_stride, const float* gR, int64_t N, float* gq,
+                                         void* stream) {
+  if (N < 0 || q_stride < 4) return set_err(MR_EINVAL, "bad quaternion batch");
+  if (N == 0) return MR_OK;
+  if (!q || !gR || !gq) return set_err(MR_EINVAL, "NULL argument");
+  k_quat_to_matrix_bwd<<<ceil_div(N, 256), 256, 0, (hipStream_t)stream>>>(q, q_stride, gR, N, gq);
+  MR_CHECK_LAUNCH("k_quat_to_matrix_bwd");
   return MR_OK;
 }
 

@@ -30,7 +30,8 @@ static int set_err(int code, const char* fmt, ...) {
 enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_SHADE_FRAG, KID_SHADE_RENDER, KID_RASTER_BWD, KID_BWD_SHADE, KID_BWD_GEOM, KID_RT_REDUCE,
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
-                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_BIN_RECT, KID_BIN_VIEW, KID_COUNT };
+                KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_BIN_RECT, KID_BIN_VIEW,
+                KID_FACE_REDUCE, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_bwd_shade(unused)", "k_bwd_geom(unused)", "k_rt_reduce",
@@ -38,7 +39,7 @@ static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bi
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
                                               "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero",
-                                              "k_bin_rect", "k_bin_view"};
+                                              "k_bin_rect", "k_bin_view", "k_face_reduce"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -78,10 +79,14 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // fill), work units, compact per-tile depth keys, and (fused path) the compact
 // per-view list of covered (pixel, face) pairs.
 // ---------------------------------------------------------------------------
+#define MR_BANDS_MAX 8  // per-view binning: workgroups (bands of tile rows) per view
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
 // ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)
-enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_COUNT = 8 };
+// ctr[CTR_ZWALK]: tiles the K-deep raster walked near-to-far (its depth-ordered list walk)
+// ctr[CTR_ROWS]: per-(record, tile) gradient rows allocated by the per-view binning (fused path)
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_ZWALK = 6, CTR_ROWS = 7,
+       CTR_COUNT = 8 };
 
 struct BinGeom {
   int TX, TY, T;
@@ -115,7 +120,7 @@ struct RasterWS {
   int* cur;    // (N*T) fill cursors
   int* vbase;  // (N) first list entry of each view (saturating)
   int* tdone;  // (N*T) per slot: units of a shared slot still to finish (count-down; the last writes)
-  int* vslot;  // (2N) first slot and number of slots of each view
+  int* vslot;  // (2 N B) first slot and number of slots of each (view, band); B = 1 on the count -> scan path
   int* stile;  // (N*T) per slot: view * T + tile
   int4* units; // (unit_cap) {view*T + tile, first list entry (-1: every face of the view), entries, slot | multi<<31}
   int* list;   // list_cap
@@ -125,8 +130,15 @@ struct RasterWS {
   float* grows;    // (F, 27) the fused backward's per-face gradient rows, cleared by the forward
   float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
+  // fused path, deterministic face gradients: the backward writes one gradient row per (record, tile)
+  // it shades (plain stores, no float atomics), k_face_reduce sums each face's rows in a fixed order
+  int* rbase;      // (2 * Ftot) first row of each record's tile rectangle (k_bin_view; -1: rows full)
+  uint8_t* rtag;   // (rows_cap) 1 = the backward wrote the row, cleared by k_bin_view
+  float* rrows;    // (list_cap * 18 floats) rows of 18 or 27 floats
   size_t bytes;
 };
+// Gradient rows of `acc` floats that fit the forward's row space (one per list entry of 18-float rows).
+static int64_t rows_cap(const BinGeom& g, int acc) { return g.list_cap * 18 / acc; }
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
                                 int64_t Fshade = 0) {
   (void)H; (void)W;
@@ -153,7 +165,7 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   w.tdone = (int*)(b + off);
   off = align_up(off + sizeof(int) * NT, 256);
   w.vslot = (int*)(b + off);
-  off = align_up(off + sizeof(int) * 2 * (size_t)N, 256);
+  off = align_up(off + sizeof(int) * 2 * MR_BANDS_MAX * (size_t)N, 256);
   w.stile = (int*)(b + off);
   off = align_up(off + sizeof(int) * NT, 256);
   w.units = (int4*)(b + off);
@@ -172,6 +184,12 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(float4) * (Fshade > 0 ? 64 * NT : 0), 256);
   w.crec = (ClipRec*)(b + off);
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
+  w.rbase = (int*)(b + off);
+  off = align_up(off + (Fshade > 0 ? sizeof(int) * 2 * (size_t)(Ftot > 0 ? Ftot : 1) : 0), 256);
+  w.rtag = (uint8_t*)(b + off);
+  off = align_up(off + (Fshade > 0 ? (size_t)g.list_cap : 0), 256);
+  w.rrows = (float*)(b + off);
+  off = align_up(off + (Fshade > 0 ? sizeof(float) * 18 * (size_t)g.list_cap : 0), 256);
   w.bytes = off;
   return w;
 }

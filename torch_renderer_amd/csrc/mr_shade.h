@@ -40,6 +40,7 @@ struct ShadeParams {
   float sigma_sil;
   // reciprocals precomputed on the host (multiplications in the per-pixel code)
   float inv_sigma_rgb, inv_gamma, inv_zrange, inv_sigma_sil;
+  int zbuf_mode;  // MR_OUT_ZBUF: the depth output is zbuf[..., 0] (background -1), not relu(zbuf)
 };
 
 struct ViewRec {  // 16 floats, matches mr_view_t
@@ -311,8 +312,8 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
   const float m = hit ? 1.0f : 0.0f;
   const float zb = hit ? z : -1.0f;    // zbuf background = -1
   const float dd = hit ? sd : -1.0f;   // dists background = -1
-  // DepthRender: relu(zbuf[..., 0])
-  o.depth = zb > 0.0f ? zb : 0.0f;
+  // DepthRender: relu(zbuf[..., 0]); MeshRasterizer's zbuf[..., 0] itself in zbuf mode
+  o.depth = (S.zbuf_mode || zb > 0.0f) ? zb : 0.0f;
   // SoftSilhouetteShader / sigmoid_alpha_blend
   sigmoid2((-dd) * S.inv_sigma_sil, C.ps, C.qs);
   C.ps *= m;
@@ -393,8 +394,8 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
     R.gb[c] = 0.0f;
     for (int k = 0; k < 3; ++k) R.gX[c][k] = R.gN[c][k] = R.gC[c][k] = 0.0f;
   }
-  // depth = relu(z)
-  if (z > 0.0f) R.gz += gD;
+  // depth = relu(z) (zbuf mode: z)
+  if (S.zbuf_mode || z > 0.0f) R.gz += gD;
   // silhouette: sil = 1 - (1 - ps), ps = sigmoid(-sd / sigma_sil)
   {
     const float gx = gS * (C.ps * C.qs);

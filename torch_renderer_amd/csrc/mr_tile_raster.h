@@ -468,12 +468,12 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
 // The background does not depend on the raster (k_shade overwrites the covered pixels later).
 template <int MODE, int CH>
 __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P, FwdParams F) {
-  const int b = (int)blockIdx.x - P.nviews - P.nsrec_wg;
+  const int b = (int)blockIdx.x - P.nviews * P.bands - P.nsrec_wg;
   if (b < 0) {
     bin_view_body(P);
     return;
   }
-  const int nbw = ((int)gridDim.x - P.nviews - P.nsrec_wg) * 16;  // background waves
+  const int nbw = ((int)gridDim.x - P.nviews * P.bands - P.nsrec_wg) * 16;  // background waves
   const bool vec = (F.W & 3) == 0;
   const int64_t HW = (int64_t)F.H * F.W * (MODE == 0 ? F.K : 1);
   const int cpv = (int)(vec ? (HW / 4 + 63) / 64 : (HW + 63) / 64);

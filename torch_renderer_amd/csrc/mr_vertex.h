@@ -80,12 +80,12 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
 // (saves a dependent launch of two tiny kernels per step).
 template <int ACC>
 __global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                    int N, float* __restrict__ gviews, float* __restrict__ gRcv,
+                                                    int N, int bands, float* __restrict__ gviews, float* __restrict__ gRcv,
                                                     float* __restrict__ gtcv, int64_t V,
                                                     const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                                                     const float* __restrict__ gface, const float* __restrict__ vraw,
                                                     float* __restrict__ gnu) {
-  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, gviews, gRcv, gtcv, blockIdx.x);
+  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, bands, gviews, gRcv, gtcv, blockIdx.x);
   else vgrad_a_block<ACC>(V, ptr, adj, gface, vraw, gnu, (int64_t)blockIdx.x - N);
 }
 

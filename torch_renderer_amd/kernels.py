@@ -387,6 +387,7 @@ class ShadeConfig:
     sil_rgba: bool = False  # silhouette as SoftSilhouetteShader's (N,H,W,4) RGBA, written by the kernels
     z_clip: float | None = None  # near clip plane (view z) of FoVPerspectiveCameras: znear / 2
     frag_sorted: bool = False  # fragment shading: empty slots follow the filled ones (MR_FRAG_SORTED)
+    zbuf: bool = False  # depth output = zbuf[..., 0] of K = 1 fragments (background -1), not relu of it
 
     def raster_struct(self):
         return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,
@@ -406,7 +407,8 @@ class ShadeConfig:
         sp.sigma_sil = float(self.sigma_sil)
         sp.out_flags = ((_lib.MR_OUT_DEPTH if self.want_depth else 0) | (_lib.MR_OUT_SIL if self.want_sil else 0) |
                         (_lib.MR_OUT_RGB if self.want_rgb else 0) | (_lib.MR_OUT_HARD if self.hard else 0) |
-                        (_lib.MR_OUT_SIL_RGBA if self.want_sil and self.sil_rgba else 0))
+                        (_lib.MR_OUT_SIL_RGBA if self.want_sil and self.sil_rgba else 0) |
+                        (_lib.MR_OUT_ZBUF if self.want_depth and self.zbuf else 0))
         sp.rgb_channels = int(self.rgb_channels)
         return sp
 

@@ -8,9 +8,13 @@ and one backward (``mr_pose_loss_*``), instead of ~15 torch elementwise / reduct
 * ``color_loss = torch.nn.MSELoss()(color, rgb_ref)``
 * ``total      = sil_loss + hloss + 0.01 * color_loss``
 
-``color`` may be the RGBA view ``image[..., :3]`` the reference passes (read in place, no copy).
-The reductions run in a fixed order (deterministic); the values agree with torch's to float32
-rounding of a different summation order. An empty mask gives NaN, like torch's mean of nothing.
+``color`` may be the RGBA view ``image[..., :3]`` and ``silhouette`` the view ``sil_image[..., 3]``
+the reference passes (camera_pose_optimizer.py:248,250): both are read in place, and their gradients
+are written by the loss's backward straight in the RGBA images' layout (zero in the channels the
+views leave out) and handed to autograd for the images themselves — what the slices' backward
+would produce, without its zero-filled (N,H,W,4) buffer and strided copy per image. The reductions
+run in a fixed order (deterministic); the values agree with torch's to float32 rounding of a
+different summation order. An empty mask gives NaN, like torch's mean of nothing.
 """
 from __future__ import annotations
 
@@ -27,40 +31,49 @@ def _vp(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
-def _color_arg(color: torch.Tensor):
-    """(tensor to read, floats between consecutive pixels): an RGBA view ``x[..., :3]`` of a dense
-    (..., C) tensor is read in place with stride C; anything else is made contiguous (stride 3)."""
-    c = color.detach()
-    if c.dtype == torch.float32 and c.dim() >= 2 and c.stride(-1) == 1 and c.stride(-2) >= 3:
-        st = c.stride(-2)
-        expect = st
-        ok = True
-        for i in range(c.dim() - 2, -1, -1):
-            if c.size(i) > 1 and c.stride(i) != expect:
-                ok = False
-                break
-            expect *= c.size(i)
-        if ok:
-            return c, st
-    return c.float().contiguous(), 3
+def _rgba_base(t: torch.Tensor, channels):
+    """The dense float32 (..., 4) tensor `t` is the slice ``base[..., channels]`` of (a slice object
+    or an int channel), or None."""
+    b = t._base
+    if b is None or b.dtype != torch.float32 or t.dtype != torch.float32 or b.dim() < 2 or b.shape[-1] != 4 \
+            or not b.is_contiguous() or t.device != b.device:
+        return None
+    if isinstance(channels, int):
+        ok = (tuple(t.shape) == tuple(b.shape[:-1]) and tuple(t.stride()) == tuple(b.stride()[:-1]) and
+              t.storage_offset() == b.storage_offset() + channels)
+    else:
+        ok = (tuple(t.shape) == tuple(b.shape[:-1]) + (3,) and tuple(t.stride()) == tuple(b.stride()) and
+              t.storage_offset() == b.storage_offset())
+    return b if ok else None
 
 
 class PoseLoss(torch.autograd.Function):
+    """sil_in / color_in: the silhouette (npix) and colour (npix, 3) tensors, or (sil_rgba / col_rgba
+    set) the RGBA images they are the [..., 3] / [..., :3] slices of, whose gradients are returned."""
+
     @staticmethod
-    def forward(ctx, depth, silhouette, color, mask, depth_ref, rgb_ref, delta, w_color):
-        _require_cuda(depth, silhouette, color, mask, depth_ref, rgb_ref)
-        if color.shape[-1] != 3 or rgb_ref.shape[-1] != 3:
+    def forward(ctx, depth, sil_in, color_in, mask, depth_ref, rgb_ref, delta, w_color, sil_rgba, col_rgba):
+        _require_cuda(depth, sil_in, color_in, mask, depth_ref, rgb_ref)
+        if rgb_ref.shape[-1] != 3 or color_in.shape[-1] != (4 if col_rgba else 3):
             raise ValueError("color and rgb_ref must end in 3 channels")
         npix = depth.numel()
-        for name, t, k in (("silhouette", silhouette, npix), ("mask", mask, npix), ("depth_ref", depth_ref, npix),
-                           ("color", color, 3 * npix), ("rgb_ref", rgb_ref, 3 * npix)):
+        for name, t, k in (("silhouette", sil_in, 4 * npix if sil_rgba else npix), ("mask", mask, npix),
+                           ("depth_ref", depth_ref, npix), ("color", color_in, (4 if col_rgba else 3) * npix),
+                           ("rgb_ref", rgb_ref, 3 * npix)):
             if t.numel() != k:
                 raise ValueError(f"pose_loss: {name} has {t.numel()} elements, expected {k} (no broadcasting)")
         L = _lib.load()
         dev = depth.device
         d = depth.detach().float().contiguous()
-        s = silhouette.detach().float().contiguous()
-        c, stride = _color_arg(color)
+        if sil_rgba:  # channel 3 of the RGBA image, read in place
+            s, s_stride, s_ptr = sil_in.detach(), 4, ctypes.c_void_p(sil_in.data_ptr() + 12)
+        else:
+            s = sil_in.detach().float().contiguous()
+            s_stride, s_ptr = 1, _vp(s)
+        if col_rgba:
+            c, stride = color_in.detach(), 4
+        else:  # (an RGBA slice pose_loss recognised comes as its image instead)
+            c, stride = color_in.detach().float().contiguous(), 3
         m = mask.detach().to(torch.bool).contiguous().view(torch.uint8)
         dr = depth_ref.detach().float().contiguous()
         rr = rgb_ref.detach().float().contiguous()
@@ -68,11 +81,11 @@ class PoseLoss(torch.autograd.Function):
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
         out = torch.empty(4, device=dev)
         stream = _lib.stream_handle(dev)
-        check(L.mr_pose_loss_forward(_vp(d), _vp(s), _vp(c), stride, _vp(m), _vp(dr), _vp(rr), npix,
+        check(L.mr_pose_loss_forward(_vp(d), s_ptr, s_stride, _vp(c), stride, _vp(m), _vp(dr), _vp(rr), npix,
                                      float(delta), float(w_color), _vp(out), _vp(ws), wsb, stream))
         ctx.save_for_backward(d, s, c, m, dr, rr, ws)
-        ctx.stride, ctx.npix, ctx.delta, ctx.w_color = stride, npix, float(delta), float(w_color)
-        ctx.shapes = (depth.shape, silhouette.shape, color.shape)
+        ctx.stride, ctx.s_stride, ctx.npix, ctx.delta, ctx.w_color = stride, s_stride, npix, float(delta), float(w_color)
+        ctx.shapes = (depth.shape, sil_in.shape, color_in.shape)
         terms = out[1:].clone()
         ctx.mark_non_differentiable(terms)
         return out[0].clone(), terms
@@ -84,13 +97,14 @@ class PoseLoss(torch.autograd.Function):
         dev = d.device
         g = (g_total if g_total is not None else torch.zeros((), device=dev)).float().contiguous().reshape(1)
         gd = torch.empty_like(d)
-        gs = torch.empty_like(s)
-        gc = torch.empty((ctx.npix, 3), device=dev)
-        check(L.mr_pose_loss_backward(_vp(d), _vp(s), _vp(c), ctx.stride, _vp(m), _vp(dr), _vp(rr), ctx.npix,
-                                      ctx.delta, ctx.w_color, _vp(g), _vp(ws), _vp(gd), _vp(gs), _vp(gc),
+        gs = torch.empty((ctx.npix, ctx.s_stride), device=dev)  # (npix, 4): the RGBA image's gradient
+        gc = torch.empty((ctx.npix, ctx.stride), device=dev)
+        s_ptr = ctypes.c_void_p(s.data_ptr() + 12) if ctx.s_stride == 4 else _vp(s)
+        check(L.mr_pose_loss_backward(_vp(d), s_ptr, ctx.s_stride, _vp(c), ctx.stride, _vp(m), _vp(dr), _vp(rr),
+                                      ctx.npix, ctx.delta, ctx.w_color, _vp(g), _vp(ws), _vp(gd), _vp(gs), _vp(gc),
                                       _lib.stream_handle(dev)))
         sd, ss, sc = ctx.shapes
-        return gd.reshape(sd), gs.reshape(ss), gc.reshape(sc), None, None, None, None, None
+        return gd.reshape(sd), gs.reshape(ss), gc.reshape(sc), None, None, None, None, None, None, None
 
 
 def pose_loss(depth, silhouette, color, mask, depth_ref, rgb_ref, delta: float = 0.05, w_color: float = 0.01,
@@ -98,7 +112,10 @@ def pose_loss(depth, silhouette, color, mask, depth_ref, rgb_ref, delta: float =
     """camera_pose_optimizer.py:257-276 calc_loss on the GPU. Returns the total loss (0-dim,
     differentiable w.r.t. depth, silhouette and color), or (total, (sil_loss, hloss, color_loss))
     with ``return_terms`` (the terms the reference logs; not differentiable)."""
-    total, terms = PoseLoss.apply(depth, silhouette, color, mask, depth_ref, rgb_ref, delta, w_color)
+    sb = _rgba_base(silhouette, 3)
+    cb = _rgba_base(color, slice(0, 3))
+    total, terms = PoseLoss.apply(depth, silhouette if sb is None else sb, color if cb is None else cb, mask,
+                                  depth_ref, rgb_ref, delta, w_color, sb is not None, cb is not None)
     if return_terms:
         return total, (terms[0], terms[1], terms[2])
     return total

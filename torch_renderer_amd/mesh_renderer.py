@@ -101,18 +101,34 @@ def _triple(x, default, what="lights/materials"):
     return tuple(float(v) for v in t.cpu())
 
 
+def _tensor_sig(v):
+    return (v.data_ptr(), v._version, tuple(v.shape), str(v.device)) if torch.is_tensor(v) else None
+
+
 def _triple_property(name, what):
     """A light / material field that re-converts on assignment (upstream reads the tensors on every
-    call, so e.g. renderer.py:82-83 ``lights.location = ...`` takes effect on the next render). The
-    getter returns what was assigned; ``_name`` holds the float triple the kernels take."""
+    call, so e.g. renderer.py:82-83 ``lights.location = ...`` takes effect on the next render) and,
+    for a tensor value, again whenever the tensor is edited in place (``lights.location[0, 2] = -5.``:
+    its storage or version changes), as _bg_triple does. The getter returns what was assigned;
+    _field_triple(obj, name) is the float triple the kernels take."""
     def get(self):
         return self.__dict__["_raw_" + name]
 
     def set_(self, v):
-        self.__dict__["_" + name] = _triple(v, None, what)  # validates (grad, shape) on assignment
+        self.__dict__["_" + name] = (_tensor_sig(v), _triple(v, None, what))  # validates (grad, shape)
         self.__dict__["_raw_" + name] = v
+        self.__dict__["_what_" + name] = what
 
     return property(get, set_)
+
+
+def _field_triple(obj, name):
+    sig, trip = obj.__dict__["_" + name]
+    raw = obj.__dict__["_raw_" + name]
+    if sig is not None and _tensor_sig(raw) != sig:  # edited in place since the last conversion
+        sig, trip = _tensor_sig(raw), _triple(raw, None, obj.__dict__["_what_" + name])
+        obj.__dict__["_" + name] = (sig, trip)
+    return trip
 
 
 class PointLights:
@@ -132,11 +148,11 @@ class PointLights:
         self.location = location
 
     def location_tuple(self):
-        return self.__dict__["_location"]
+        return _field_triple(self, "location")
 
     def color_tuples(self):
         """(ambient, diffuse, specular) as float triples."""
-        return self.__dict__["_ambient"], self.__dict__["_diffuse"], self.__dict__["_specular"]
+        return _field_triple(self, "ambient"), _field_triple(self, "diffuse"), _field_triple(self, "specular")
 
 
 class AmbientLights:
@@ -149,7 +165,7 @@ class AmbientLights:
         self.ambient_color = ambient_color
 
     def ambient_tuple(self):
-        return self.__dict__["_ambient"]
+        return _field_triple(self, "ambient")
 
 
 class Materials:
@@ -179,7 +195,7 @@ class Materials:
         self.__dict__["_raw_shininess"] = v
 
     def color_tuples(self):
-        return self.__dict__["_ambient"], self.__dict__["_diffuse"], self.__dict__["_specular"]
+        return _field_triple(self, "ambient"), _field_triple(self, "diffuse"), _field_triple(self, "specular")
 
     def shininess_value(self):
         return self.__dict__["_shininess"]
@@ -195,6 +211,56 @@ class Fragments:
     bary_coords: torch.Tensor
     dists: torch.Tensor
     sorted_slots: bool = field(default=False, repr=False, compare=False)
+    _p2f_sig: tuple | None = field(default=None, repr=False, compare=False)
+
+    def __post_init__(self):
+        # the slot order holds for pix_to_face as the rasterizer wrote it: an in-place edit (e.g.
+        # masking faces with -1) or a replaced tensor turns the early stop off (shade every slot)
+        if self.sorted_slots and self._p2f_sig is None:
+            self._p2f_sig = _tensor_sig(self.pix_to_face)
+
+    def slots_sorted(self) -> bool:
+        if not self.sorted_slots:
+            return False
+        p2f = self.pix_to_face
+        return self._p2f_sig is not None and _tensor_sig(p2f) == self._p2f_sig
+
+    def materialize(self) -> "Fragments":
+        """Every field computed now (a no-op here; see _LazyFragments)."""
+        return self
+
+
+class _LazyFragments(Fragments):
+    """MeshRasterizer's K = 1 Fragments of one mesh shared by the views, computed on first access.
+    ``zbuf`` alone — what camera_pose_optimizer.py:244-246 and batch_rendering_test.py:274 read —
+    comes from the fused render in zbuf mode (mr_render_forward with MR_OUT_ZBUF: the nearest face's
+    depth, -1 where no face; bitwise the modular rasterizer's zbuf), whose backward is the fused
+    depth backward: no (N,H,W,1) pix_to_face / bary_coords / dists tensors written, and no
+    per-fragment-slot raster backward. Reading pix_to_face, bary_coords or dists runs the modular
+    rasterizer (RasterizeMeshesWorld) once for all three (and zbuf, if not read before)."""
+
+    def __init__(self, zbuf_fn, full_fn):  # noqa: D107 (no dataclass __init__: the fields are lazy)
+        self.__dict__["_zbuf_fn"] = zbuf_fn
+        self.__dict__["_full_fn"] = full_fn
+        self.sorted_slots = True
+        self._p2f_sig = None
+
+    def __getattr__(self, name):  # only for fields not computed yet
+        d = self.__dict__
+        if name == "zbuf":
+            d["zbuf"] = d["_zbuf_fn"]()
+            return d["zbuf"]
+        if name in ("pix_to_face", "bary_coords", "dists"):
+            p2f, zbuf, bary, dists = d["_full_fn"]()
+            d.update(pix_to_face=p2f, bary_coords=bary, dists=dists)
+            d.setdefault("zbuf", zbuf)
+            d["_p2f_sig"] = _tensor_sig(p2f)
+            return d[name]
+        raise AttributeError(name)
+
+    def materialize(self) -> "Fragments":
+        _ = self.pix_to_face  # one modular pass for every field (zbuf too, when not read before)
+        return self
 
 
 # --------------------------------------------------------------------------- rasterizer
@@ -262,10 +328,30 @@ class MeshRasterizer(torch.nn.Module):
             # one mesh for every view (Meshes.extend): transform + rasterize in one native call,
             # bitwise the two-step result below
             R, T, intr = _views(meshes, cameras, (H, W), kwargs)
-            p2f, zbuf, bary, dists = RasterizeMeshesWorld.apply(
-                meshes.shared_verts(), R, T, meshes.shared_faces(), intr, R.shape[0], H, W,
-                int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
-                rs.max_faces_per_bin, _z_clip_value(cameras, rs))
+            zc = _z_clip_value(cameras, rs)
+            from .kernels import _require_cuda
+
+            _require_cuda(meshes.shared_verts(), meshes.shared_faces(), R, T)  # fail at the call, not at first use
+
+            def full():
+                return RasterizeMeshesWorld.apply(
+                    meshes.shared_verts(), R, T, meshes.shared_faces(), intr, R.shape[0], H, W,
+                    int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
+                    rs.max_faces_per_bin, zc)
+
+            if int(rs.faces_per_pixel) == 1 and float(rs.blur_radius) == 0.0:
+                def zbuf_only():  # the fused render in zbuf mode (see _LazyFragments)
+                    from .kernels import render_views
+
+                    cfg = ShadeConfig(H=H, W=W, persp=persp, clip=clip, cull=bool(rs.cull_backfaces),
+                                      max_faces_per_bin=rs.max_faces_per_bin, light_kind=1, want_depth=True,
+                                      want_sil=False, want_rgb=False, zbuf=True, z_clip=zc)
+                    cc = torch.zeros((1, 3), device=R.device)
+                    return render_views(meshes.shared_verts(), R, T, meshes.shared_faces(), intr, cc,
+                                        cfg)["depth"].unsqueeze(-1)
+
+                return _LazyFragments(zbuf_only, full)
+            p2f, zbuf, bary, dists = full()
             return Fragments(pix_to_face=p2f, zbuf=zbuf, bary_coords=bary, dists=dists, sorted_slots=True)
         fv = self.transform(meshes, **{**kwargs, "raster_settings": rs})
         first = meshes.mesh_to_faces_packed_first_idx().to(fv.device)
@@ -331,7 +417,7 @@ def shade_fragments(fragments: Fragments, meshes: Meshes, cfg: ShadeConfig, cam_
     p2f = fragments.pix_to_face
     N = p2f.shape[0]
     tex = meshes.textures
-    if getattr(fragments, "sorted_slots", False) and not cfg.frag_sorted:
+    if isinstance(fragments, Fragments) and fragments.slots_sorted() and not cfg.frag_sorted:
         cfg = dataclasses.replace(cfg, frag_sorted=True)
     if cfg.want_rgb and tex is None:
         raise ValueError("Meshes does not have textures")  # upstream Meshes.sample_textures
@@ -475,6 +561,8 @@ class MeshRenderer(torch.nn.Module):
         # 8x8 tiles, <= 256 per side, <= 65,536 faces per view)
         tx, ty = (W + 7) // 8, (H + 7) // 8
         if tx * ty > 16384 or tx > 256 or ty > 256 or Fn > 65536:
+            return None
+        if N * tx * ty * 64 * int(rs.faces_per_pixel) >= 2 ** 31:  # mr_soft_silhouette_forward's slot bound
             return None
         return SoftSilhouetteWorld.apply(meshes.shared_verts(), R, T, meshes.shared_faces(), intr, N, H, W,
                                          int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip,

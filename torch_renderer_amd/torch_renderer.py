@@ -48,11 +48,11 @@ def _union_topology(meshes: Meshes):
     """(faces (F,3) int64 of the union, view_face_first (N+1), view_face_count (N) int64 device
     tensors, largest face count, view_vert_first (N+1), largest vertex count) of a batch of distinct
     meshes, cached on the identity and version of the faces tensors (the union faces tensor keeps
-    its identity, so its CSR stays cached too)."""
+    its identity, so its CSR stays cached too). The entry holds the source tensors themselves and is
+    matched by `is`, so a garbage-collected batch cannot hand its ids to a new one."""
     fl, vl = meshes.faces_list(), meshes.verts_list()
-    key = tuple((id(f), f._version, v.shape[0]) for f, v in zip(fl, vl))
     hit = _UNION_CACHE.get(id(meshes))
-    if hit is not None and hit[0] == key:
+    if hit is not None and _same_sources(hit[0], fl, vl):
         return hit[1]
     voff, out = 0, []
     for v, f in zip(vl, fl):
@@ -70,8 +70,19 @@ def _union_topology(meshes: Meshes):
            torch.tensor(vfirst, dtype=torch.int64, device=dev), max(vcounts))
     if len(_UNION_CACHE) > 16:
         _UNION_CACHE.clear()
-    _UNION_CACHE[id(meshes)] = (key, res)
+    _UNION_CACHE[id(meshes)] = (_sources(fl, vl), res)
     return res
+
+
+def _sources(al, bl):
+    """Cache-entry record of two tensor lists: the tensors (kept alive) and their versions."""
+    return tuple((a, a._version, b, b._version) for a, b in zip(al, bl)), len(al)
+
+
+def _same_sources(rec, al, bl):
+    entries, n = rec
+    return n == len(al) == len(bl) and all(a is a0 and a._version == va and b is b0 and b._version == vb
+                                           for (a0, va, b0, vb), a, b in zip(entries, al, bl))
 
 
 def union_texture_args(meshes: Meshes, need_color: bool):
@@ -92,17 +103,16 @@ def union_texture_args(meshes: Meshes, need_color: bool):
         if any(m is not maps[0] and (m.data_ptr() != maps[0].data_ptr() or m.shape != maps[0].shape) for m in maps):
             return None
         vl = meshes.verts_list()
-        key = ("uv",) + tuple((id(a), a._version, id(b), b._version) for a, b in
-                              zip(tex.verts_uvs_list(), tex.faces_uvs_list()))
+        vul, ful = list(tex.verts_uvs_list()), list(tex.faces_uvs_list())
         hit = _UNION_CACHE.get(("uv", id(tex)))
-        if hit is None or hit[0] != key:
+        if hit is None or not _same_sources(hit[0], vul, ful):
             vus, fus, off = [], [], 0
             for i in range(len(vl)):
                 vu, fu = tex.verts_uvs_list()[i], tex.faces_uvs_list()[i]
                 vus.append(vu.float())
                 fus.append(fu.to(torch.int32) + off)
                 off += vu.shape[0]
-            hit = (key, (torch.cat(vus, 0).contiguous(), torch.cat(fus, 0).contiguous()))
+            hit = (_sources(vul, ful), (torch.cat(vus, 0).contiguous(), torch.cat(fus, 0).contiguous()))
             _UNION_CACHE[("uv", id(tex))] = hit
         vuv, fuv = hit[1]
         u8 = tex.u8_map(0)
@@ -139,6 +149,8 @@ def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfi
     ut = union_texture_args(meshes, need_color)
     if ut is not None:  # distinct meshes: their union in one launch, view n rendering mesh n
         faces_u, first, count, fmax = _union_topology(meshes)[:4]
+        if ut[0].kind == 2 and ut[0].faces_uvs.shape[0] != faces_u.shape[0]:
+            raise RuntimeError(f"union faces_uvs ({ut[0].faces_uvs.shape[0]}) and faces ({faces_u.shape[0]}) differ")
         return render_views(torch.cat(list(meshes.verts_list()), 0), Rb, Tb, faces_u, intr, cam_center, cfg, ut[0],
                             vcolors=ut[1], pose_cv=pose_cv, ranges=(first, count, fmax))
     outs = []
@@ -268,7 +280,7 @@ class DepthColorRender(DifferentiableRenderer):
             (rast, sil_r), (_, phong_r) = self._soft
             Rs, ts = self._camera_pose_from_opencv_to_pytorch(R, tvec)
             # one raster pass feeds all three (the three renderers' rasterizers are identical)
-            frags = rast(meshes, R=Rs, T=ts)
+            frags = rast(meshes, R=Rs, T=ts).materialize()  # the shaders read every field: one pass
             depth = torch.relu(frags.zbuf[..., 0])
             sil = sil_r.shader(frags, meshes, R=Rs, T=ts)[..., 3]
             return depth, sil, phong_r.shader(frags, meshes, R=Rs, T=ts)[..., :3]

@@ -173,13 +173,15 @@ def main():
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
     ap.add_argument("--texture", choices=("uv", "white"), default="uv",
                     help="experiments only: 'white' drops the UV texture (not the benchmark workload)")
-    ap.add_argument("--mode", choices=("render", "fragments", "soft", "gather", "pose"), default="render",
+    ap.add_argument("--mode", choices=("render", "fragments", "soft", "gather", "pose", "c5"), default="render",
                     help="render: the headline fwd+bwd step; fragments: the rasterizer alone "
                          "(MeshRasterizer -> PyTorch3D Fragments, K=1; the north-star fragment-pass roofline); "
                          "soft: K=50 soft silhouette fwd+bwd (deform_mesh_with_color.py); gather: C4, depth "
                          "render of --views views IN TOTAL sharded over the ranks + RCCL gather to rank 0 "
                          "(batch_rendering_test.py, strong scaling); pose: C3, camera_pose_optimizer.py's step "
-                         "(three renders, calc_loss, backward, Adam) for --views poses per GPU")
+                         "(three renders, calc_loss, backward, Adam) for --views poses per GPU; c5: "
+                         "mesh_deformer.py color_train's step (F=81,920 sphere, 1024x1024, --views single-view "
+                         "renders per step, default 5)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -205,6 +207,8 @@ def main():
         return bench_gather(args, dev, world, rank)
     if args.mode == "pose":
         return bench_pose(args, dev, world, rank)
+    if args.mode == "c5":
+        return bench_c5(args, dev, world, rank)
     from torch_renderer_amd import _lib
     from torch_renderer_amd import distributed as D
     from torch_renderer_amd.assets import load_asset, load_asset_arrays
@@ -867,6 +871,138 @@ def bench_pose(args, dev, world, rank):
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c5(args, dev, world, rank):
+    """C5 (BASELINE.json configs[4]; mesh_deformer.py:130-222 color_train) as the caller runs it: the
+    F=81,920 subdivided sphere (data/sphere.obj subdivided twice), 1024x1024 (--size), PerspectiveCameras
+    (NDC, focal 1) at look_at_view_transform(2, elev, azim) over 10 target views, AmbientLights,
+    perspective_correct=False, TexturesVertex(hardtanh(verts_rgb)) with grad; one step = --views
+    (default 5: num_views_per_iteration) single-view renderer(mesh, cameras=target_cameras[j], lights=)
+    calls (:196-204), the MSE losses + the colour penalty (:207), backward to the per-vertex colours AND
+    positions (the mesh is src_mesh.offset_verts(deform_verts)), one SGD(lr=1, momentum=0.9) step."""
+    from torch_renderer_amd import _lib
+    from torch_renderer_amd.cameras import PerspectiveCameras
+    from torch_renderer_amd.kernels import render_stats
+    from torch_renderer_amd.mesh_renderer import (AmbientLights, MeshRasterizer, MeshRenderer, RasterizationSettings,
+                                                  SoftPhongShader)
+    from torch_renderer_amd.structures import Meshes, TexturesVertex
+    from torch_renderer_amd.transforms import look_at_view_transform
+    from torch_renderer_amd.utils import subdivided_sphere
+
+    H = W = args.size if args.size != 512 else 1024
+    nper = args.views if args.views != 64 else 5
+    n_targets = 10
+    sph = subdivided_sphere(2)
+    verts0, faces = sph.verts_list()[0].to(dev), sph.faces_list()[0].to(dev)
+    Fn, Vn = faces.shape[0], verts0.shape[0]
+    elev = torch.linspace(0, 360, n_targets)
+    azim = torch.linspace(-180, 180, n_targets)
+    R, T = look_at_view_transform(dist=2.0, elev=elev, azim=azim)
+    R, T = R.to(dev), T.to(dev)
+    lights = AmbientLights(device=dev)
+    rs = RasterizationSettings(image_size=H, blur_radius=0.0, faces_per_pixel=1, perspective_correct=False)
+    cams = PerspectiveCameras(device=dev, R=R, T=T)
+    renderer = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs),
+                            SoftPhongShader(device=dev, cameras=cams, lights=lights))
+    target_cameras = [PerspectiveCameras(device=dev, R=R[None, i], T=T[None, i]) for i in range(n_targets)]
+    gen = torch.Generator().manual_seed(7 + rank)
+    with torch.no_grad():  # targets: the sphere coloured by a smooth function of position
+        tcol = (0.5 + 0.5 * torch.sin(3.0 * verts0.cpu() + torch.rand(3, generator=gen))).to(dev)
+        tmesh = Meshes([verts0], [faces], TexturesVertex([tcol])).extend(n_targets)
+        target_rgb = renderer(tmesh, cameras=cams, lights=lights)[..., :3]
+    deform = torch.zeros_like(verts0, requires_grad=True)  # geometry_train's offsets (grads reach them)
+    verts_rgb = torch.full((1, Vn, 3), 0.5, device=dev, requires_grad=True)
+    opt = torch.optim.SGD([verts_rgb], lr=1.0, momentum=0.9)
+    perms = [torch.randperm(n_targets, generator=gen)[:nper].tolist() for _ in range(64)]
+    it = [0]
+
+    def step():
+        opt.zero_grad()
+        deform.grad = None
+        norm = torch.nn.functional.hardtanh(verts_rgb, min_val=0.0, max_val=1.0)
+        mesh = Meshes([verts0 + deform], [faces], TexturesVertex(verts_features=norm))
+        loss = 0
+        for j in perms[it[0] % len(perms)]:
+            img = renderer(mesh, cameras=target_cameras[j], lights=lights)
+            loss = loss + ((img[..., :3].squeeze() - target_rgb[j]) ** 2).mean()
+        loss = loss + ((norm - verts_rgb) ** 2).sum()
+        loss.backward()
+        opt.step()
+        it[0] += 1
+
+    elapsed = _time_steps(step, args, dev, world)
+    kt = _kernel_times(step, min(args.steps, 10))
+    # work counters of one view's forward (render_stats reads the live workspace)
+    norm = torch.nn.functional.hardtanh(verts_rgb, 0.0, 1.0).detach()
+    keep = renderer(Meshes([verts0], [faces], TexturesVertex(verts_features=norm)), cameras=target_cameras[0],
+                    lights=lights)
+    wstats = render_stats()
+    del keep
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+    value = nper * world * args.steps / elapsed
+    kernels = {k: {"launches": v[0], "avg_us": round(v[1] / max(v[0], 1) * 1e3, 2)} for k, v in kt.items()}
+    # roofline of the longest kernel (per launch = one view): algorithmic bytes as the render mode's table
+    dom = max(kt.items(), key=lambda kv: kv[1][1])
+    name, (launches, total_ms) = dom
+    avg_s = total_ms / launches / 1e3
+    b = algorithmic_bytes(name, H, W, Fn, 1, wstats, 0)
+    roof = None
+    if b is not None:
+        roof = {"bound": "hbm", "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
+                "algorithmic_bytes_per_launch": b, "achieved": round(b / avg_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(b / avg_s / 1e9 / HBM_PEAK_GBS, 4), "traffic": None}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = c5_cpu_baseline(verts0.cpu(), faces.cpu(), R.cpu(), T.cpu(), H, W)
+    line = {
+        "metric": f"frames/sec C5 colour-fitting step (mesh_deformer.py color_train), subdivided sphere F={Fn}, {H}x{W}",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "launch": "eager", "data": "synthetic target colours on the subdivided "
+                                                                        "reference sphere",
+        "config": {"workload": f"ico-sphere (F={Fn}, V={Vn}), {H}x{W}, {nper} single-view renders per step "
+                               "(PerspectiveCameras, AmbientLights, TexturesVertex, perspective_correct=False), "
+                               "MSE + colour penalty, backward to vertex colours and positions, SGD",
+                   "mesh": "subdivided sphere", "H": H, "W": W, "views_per_step": nper,
+                   "parallelism": f"replicas x{world}"},
+        "roofline": roof, "cpu_baseline": cpu, "work": wstats, "kernels": kernels,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c5_cpu_baseline(verts, faces, R, T, H, W, win=128, reps=1):
+    """The reference CPU path (oracle: C naive rasterizer + torch-CPU ambient shading / blend / autograd) on a
+    bounded sample: a win x win window of one C5 view, fwd + bwd to colours and positions, scaled to
+    frames/s by the window's share of the image (the naive rasterizer's cost is per pixel x face)."""
+    from oracle import oracle as O
+
+    cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    threads = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or cores, cores)
+    O.set_threads(threads)
+    y0, x0 = H // 2 - win // 2, W // 2 - win // 2
+    window = (y0, y0 + win, x0, x0 + win)
+    intr = torch.tensor([[1.0, 0.0, 1.0, 0.0]])
+
+    def one():
+        v = verts.clone().requires_grad_(True)
+        vc = torch.full(verts.shape, 0.5).requires_grad_(True)
+        ref = O.render_ref(v, faces, R[:1], T[:1], intr, H, W, texture=("vertex", vc),
+                           light={"kind": "ambient", "ambient": (1.0, 1.0, 1.0)}, persp=False, window=window)
+        ref["rgba"][..., :3].sum().backward()
+
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        one()
+    sec = (time.perf_counter() - t0) / reps
+    scale = (H * W) / float(win * win)
+    return {"value": 1.0 / (sec * scale), "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"a {win}x{win} window of one view (fwd + bwd, {sec:.2f} s), scaled by the image/window pixel "
+                      f"ratio {scale:.0f}: C naive rasterizer (OpenMP {threads} threads) + torch-CPU shading/autograd"}
 
 
 def soft_cpu_baseline(verts, faces, R, T, H, W, K, blur, sigma, target, n_views=2, reps=2):

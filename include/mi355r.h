@@ -363,6 +363,11 @@ int32_t mr_quaternion_to_matrix_backward(const float* q, int64_t q_stride, const
  * (same N, total faces, H, W, max_faces_per_bin). Synchronises `stream`; for benchmarks and tools.
  * out[0] = (tile, face) list entries, out[1] = raster work units, out[2] = non-empty 8x8 tiles,
  * out[3] = covered pixels. */
+/* 1 when a batch of N views with total_faces face instances at H x W takes the per-view binning
+ * (k_bin_rect_* -> k_bin_view: tile grids of <= 16,384 8x8 tiles, <= 256 a side), 0 when it takes
+ * count -> scan -> fill. The fused soft silhouette and the deterministic face gradients need the former. */
+int32_t mr_per_view_binning(int64_t N, int64_t total_faces, int32_t H, int32_t W);
+
 int32_t mr_workspace_stats(const void* workspace, int64_t N, int64_t total_faces, int32_t H, int32_t W,
                            int32_t max_faces_per_bin, int64_t* out, void* stream);
 

@@ -27,3 +27,9 @@ for r in sorted(csv.DictReader(open(sys.argv[1])), key=lambda r:-float(r['TotalD
 PY
 timeout -k 10 300 python bench.py --mode pose --no-cpu-baseline --steps 20 --warmup 5 > gpurun_out/pose_${TAG}.json 2> gpurun_out/pose_${TAG}.err || { tail -20 gpurun_out/pose_${TAG}.err; exit 1; }
 python -c "import json,sys; d=json.loads(open('gpurun_out/pose_${TAG}.json').read().strip().splitlines()[-1]); print('pose', d['value'], d['ms_per_step'])"
+timeout -k 10 300 python bench.py --mode c5 --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/c5_${TAG}.json 2> gpurun_out/c5_${TAG}.err || { tail -20 gpurun_out/c5_${TAG}.err; exit 1; }
+python -c "import json,sys; d=json.loads(open('gpurun_out/c5_${TAG}.json').read().strip().splitlines()[-1]); print('c5', d['value'], d['ms_per_step'], {k:v['avg_us'] for k,v in d['kernels'].items()})"
+if [ -f exp/fmax64k.so ]; then
+MI355R_LIB=exp/fmax64k.so timeout -k 10 300 python bench.py --mode c5 --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/c5old_${TAG}.json 2> gpurun_out/c5old_${TAG}.err || { tail -20 gpurun_out/c5old_${TAG}.err; exit 1; }
+python -c "import json,sys; d=json.loads(open('gpurun_out/c5old_${TAG}.json').read().strip().splitlines()[-1]); print('c5 (count-scan)', d['value'], d['ms_per_step'], {k:v['avg_us'] for k,v in d['kernels'].items()})"
+fi

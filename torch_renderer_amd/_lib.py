@@ -138,6 +138,7 @@ _SIGS = [
     ("mr_quaternion_to_matrix_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_workspace_counters", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
+    ("mr_per_view_binning", _I32, [_I64, _I64, _I32, _I32]),
     ("mr_timing_enable", _I32, [_I32]),
     ("mr_timing_read", _I32, [_VP, _VP, _I32]),
     ("mr_timing_kernel_name", ctypes.c_char_p, [_I32]),

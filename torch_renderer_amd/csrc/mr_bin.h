@@ -639,7 +639,9 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
 // counters, no per-tile global atomics, one launch instead of two). List, slot and unit space
 // come from one atomic each per view; the raster result does not depend on their order.
 #define MR_VIEW_TMAX 16384              // LDS histogram: 64 KB
-#define MR_VIEW_FMAX 65536              // faces per view (mean) above which the count -> scan path is used
+#ifndef MR_VIEW_FMAX
+#define MR_VIEW_FMAX 1048576            // faces per view (mean) above which the count -> scan path is used
+#endif
 #define MR_RECT_NONE 0x000000ffu        // tx0 = 255 > tx1 = 0: an empty rectangle
 #define MR_CURSOR_OFF 0x40000000        // fill cursor of a tile whose list is not filled (list_cap <= it)
 #define MR_VIEW_RPT 8                   // rectangles per thread per chunk

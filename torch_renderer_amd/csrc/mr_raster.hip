@@ -226,6 +226,12 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
 }
 }  // extern "C++"
 
+int32_t mr_per_view_binning(int64_t N, int64_t total_faces, int32_t H, int32_t W) {
+  if (N <= 0 || H <= 0 || W <= 0) return 0;
+  const int64_t Ft = total_faces > 0 ? total_faces : 1;
+  return view_binning(bin_geom(H, W, N, Ft, 0), N, Ft) ? 1 : 0;
+}
+
 int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W, int32_t mode) {
   if (N <= 0 || H <= 0 || W <= 0) return 0;
   BinGeom g = bin_geom(H, W, N, N * (F > 0 ? F : 1), 0);

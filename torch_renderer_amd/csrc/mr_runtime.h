@@ -79,7 +79,9 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // fill), work units, compact per-tile depth keys, and (fused path) the compact
 // per-view list of covered (pixel, face) pairs.
 // ---------------------------------------------------------------------------
-#define MR_BANDS_MAX 8  // per-view binning: workgroups (bands of tile rows) per view
+#ifndef MR_BANDS_MAX
+#define MR_BANDS_MAX 32  // per-view binning: workgroups (bands of tile rows) per view
+#endif
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
 // ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)

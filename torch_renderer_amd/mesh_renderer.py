@@ -558,9 +558,11 @@ class MeshRenderer(torch.nn.Module):
         R, T, intr = _views(meshes, cameras, (H, W), kwargs)
         N, Fn = R.shape[0], meshes.shared_faces().shape[0]
         # the fused pass needs the per-view binning (mr_rasterize_meshes_world's common case: <= 16,384
-        # 8x8 tiles, <= 256 per side, <= 65,536 faces per view)
+        # 8x8 tiles, <= 256 per side)
+        from . import _lib
+
         tx, ty = (W + 7) // 8, (H + 7) // 8
-        if tx * ty > 16384 or tx > 256 or ty > 256 or Fn > 65536:
+        if not _lib.load().mr_per_view_binning(N, N * Fn, H, W):
             return None
         if N * tx * ty * 64 * int(rs.faces_per_pixel) >= 2 ** 31:  # mr_soft_silhouette_forward's slot bound
             return None

@@ -262,8 +262,14 @@ def main():
     # Default: the fwd+bwd kernels are captured once into a HIP graph and replayed (every kernel
     # of the step runs each replay; only the Python/launch enqueue work is removed). The
     # collective stays outside the graph.
+    # One step = fwd+bwd of the rank's views (+ the shared-vertex-gradient all-reduce when N > 1).
+    # Default: the forward and the backward are each captured once into a HIP graph (one memory pool)
+    # and replayed (every kernel of the step runs each replay; only the Python/launch enqueue work is
+    # removed). With N > 1 the all-reduce of step k's vertex gradient runs on a side stream while step
+    # k+1's forward replays (the forward never reads verts.grad); the backward of step k+1, which
+    # rewrites it, waits for the collective — so RCCL's latency hides behind the forward.
     if args.eager:
-        run_fwd_bwd = eager_step
+        fwd_only = bwd_only = None
     else:
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
@@ -274,23 +280,39 @@ def main():
         verts.grad = None
         R_cv.grad = None
         t_cv.grad = None
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            fwd_bwd()
-        run_fwd_bwd = graph.replay
+        pool = torch.cuda.graph_pool_handle()
+        g_fwd, g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fwd, pool=pool):
+            outs_static = renderer.render(bmesh, R_cv, t_cv)
+        with torch.cuda.graph(g_bwd, pool=pool):
+            torch.autograd.backward(list(outs_static), [gD, gS, gC], retain_graph=True)
+        fwd_only, bwd_only = g_fwd.replay, g_bwd.replay
 
-    ar_events = []  # (start, end) HIP events around each timed step's all_reduce (on the compute stream)
+    comm = torch.cuda.Stream() if world > 1 else None
+    ar_events = []  # (start, end) HIP events around each timed step's all_reduce (on the comm stream)
+    pending = [False]
 
     def step(timed=False):
-        run_fwd_bwd()
+        if fwd_only is None:  # eager launches (--eager)
+            eager_step()
+            if world > 1:
+                D.allreduce_grads([verts])
+            return
+        fwd_only()
+        if pending[0]:  # step k's all-reduce must finish before step k+1's backward rewrites verts.grad
+            torch.cuda.current_stream().wait_stream(comm)
+        bwd_only()
         if world > 1:
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-            D.allreduce_grads([verts])  # the step's only exchange: shared vertex grads
-            if timed:
-                e1.record()
-                ar_events.append((e0, e1))
+            comm.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(comm):
+                if timed:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                D.allreduce_grads([verts])  # the step's only exchange: shared vertex grads
+                if timed:
+                    e1.record()
+                    ar_events.append((e0, e1))
+            pending[0] = True
 
     for _ in range(2):
         step()
@@ -304,8 +326,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    # the collective's share of the step as the compute stream sees it (RCCL's stream waits on it and
-    # the compute stream waits on RCCL): mean over the timed steps, max over ranks
+    # the collective's duration on its side stream (overlapped with the next step's forward): mean over
+    # the timed steps, max over ranks
     allreduce_us = None
     if ar_events:
         allreduce_us = sum(a.elapsed_time(b) for a, b in ar_events) / len(ar_events) * 1e3
@@ -324,11 +346,35 @@ def main():
     torch.cuda.synchronize()
     kt = _lib.timing_read()
     _lib.timing_enable(False)
+    # rehearsal check (MR_BENCH_REHEARSE, N ranks sharing one GPU over gloo): the all-reduced vertex
+    # gradient equals rank 0's single-process fwd+bwd of ALL the ranks' views (tolerance: the per-face sums
+    # are grouped by rank there)
+    ar_check = None
+    if world > 1 and rehearse:
+        step()
+        torch.cuda.synchronize()
+        g_ar = verts.grad.detach().clone()
+        if rank == 0:
+            Rf, tf = R_all.to(dev).contiguous(), t_all.to(dev).contiguous()
+            vf = meshes.shared_verts().clone().requires_grad_(True)
+            genf = torch.Generator().manual_seed(1)
+            parts = []
+            for r in range(world):  # each rank's upstream grads (seeded 1 + r), in rank order
+                gr = torch.Generator().manual_seed(1 + r)
+                parts.append(((torch.rand(nv, H, W, generator=gr) * 2 - 1), (torch.rand(nv, H, W, generator=gr) * 2 - 1),
+                              (torch.rand(nv, H, W, 3, generator=gr) * 2 - 1)))
+            del genf
+            full = DepthColorRender(K.to(dev), (H, W), device=dev)
+            fm = Meshes([vf], [faces], tex).extend(nv * world)
+            outs_f = full.render(fm, Rf, tf)
+            torch.autograd.backward(list(outs_f), [torch.cat([p[i] for p in parts]).to(dev) for i in range(3)])
+            err = (vf.grad - g_ar).abs().max().item()
+            scale = max(1.0, vf.grad.abs().max().item())
+            ar_check = {"vertex_grad_max_abs_diff": err, "scale": scale, "ok": bool(err <= 1e-4 * scale)}
     # the north-star fragment pass (MeshRasterizer -> Fragments, K = 1) on the same mesh, size and views,
     # timed in the same run so that the driver's record carries it
-    del run_fwd_bwd
     if not args.eager:
-        del graph
+        del g_fwd, g_bwd, outs_static
     torch.cuda.synchronize()
     frag = None
     if not args.no_fragment_pass:
@@ -392,6 +438,8 @@ def main():
         "cpu_baseline": cpu,
         "work": wstats, "kernels": kernels,
         "allreduce_us": None if allreduce_us is None else round(allreduce_us, 2),
+        "allreduce_overlapped_with_forward": world > 1 and not args.eager,
+        "allreduce_check": ar_check,
         "allreduce_bytes": 4 * 3 * int(verts0.shape[0]) if world > 1 else 0,
     }
     print(json.dumps(line), flush=True)

@@ -35,7 +35,8 @@ def test_all_header_symbols_exported(lib):
 
 
 def test_version_and_workspace_queries(lib):
-    assert lib.mr_version() == 3  # 2: mr_raster_settings_t gained clip_z / z_clip_value; 3: mr_mesh_t vnormals_out
+    assert lib.mr_version() == 4  # 2: mr_raster_settings_t gained clip_z / z_clip_value; 3: mr_mesh_t vnormals_out;
+    # 4: mr_pose_loss_* take sil_stride (RGBA slices read in place), MR_OUT_ZBUF, quaternion kernels
     a = lib.mr_render_workspace(64, 5856, 512, 512, 0)
     b = lib.mr_render_workspace(8, 5856, 512, 512, 0)
     assert a > b > 0

@@ -48,7 +48,7 @@ extern "C" {
 const char* mr_last_error(void) { return g_err; }
 
 
-int32_t mr_version(void) { return 3; }
+int32_t mr_version(void) { return 4; }
 
 int32_t mr_struct_size(int32_t which) {
   switch (which) {

@@ -537,7 +537,9 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 
 // CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
 // instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
+#ifndef MR_BWD_ATTR
 #define MR_BWD_ATTR
+#endif
 // The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
 // through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
 // loop, overflow the SGPR file and are spilled into VGPR lanes (one v_readlane per use; k_bwd_fused had

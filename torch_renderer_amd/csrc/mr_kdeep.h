@@ -151,7 +151,7 @@ MR_DEV void insert_ns(unsigned long long (&q)[KP], unsigned long long key) {
 #endif
 #define MR_KP_ZBINS 256
 struct KpStage {
-  float rec[16][64];
+  StageRecs rec;
   int id[64];
   int meta[64];
   int mark[64];

@@ -168,10 +168,20 @@ static int bin_bands(int64_t N, const BinGeom& g) {
   if (b > g.TY) b = g.TY;
   return b < 1 ? 1 : (int)b;
 }
+// Background workgroups of the k_bin_view launch: the workgroup slots the binning (nbin = views x bands
+// workgroups) and the ShadeRec packing (sb) leave free — one per CU with one workgroup per view (98 KB
+// of LDS each), MR_BG_WG_PER_CU per CU with bands (64 KB: two fit a CU, so a background workgroup can
+// stream stores on every CU beside a binning one).
+#ifndef MR_BG_WG_PER_CU
+#define MR_BG_WG_PER_CU 1
+#endif
+static int64_t bin_bg_wgs(int64_t nbin, int64_t sb, bool banded) {
+  return (int64_t)num_cus() * (banded ? MR_BG_WG_PER_CU : 1) - nbin - sb;
+}
 // Background chunks the k_bin_view launch takes over (chunks of 64 lanes x 4 pixels when W % 4 == 0,
-// else 64 pixels); 0 when the binning workgroups (nbin = views x bands) leave no CU idle.
+// else 64 pixels); 0 when the binning leaves no workgroup slot free.
 static int64_t bg_chunks(int64_t N, int64_t nbin, int64_t sb, int H, int W, int mode) {
-  const int64_t nbg = (int64_t)num_cus() - nbin - sb;
+  const int64_t nbg = bin_bg_wgs(nbin, sb, nbin > N);
   if (nbg <= 0) return 0;
   const int64_t HW = (int64_t)H * W;
   const int64_t nchunks = N * ((W & 3) == 0 ? (HW / 4 + 63) / 64 : (HW + 63) / 64);
@@ -212,7 +222,7 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
   const size_t shm = std::max(hist_b, B > 1 ? (size_t)MR_VIEW_LDS_BANDED : view_lds_bytes());
   V.stage_cap = (int)((shm - hist_b) / sizeof(int));
   if constexpr (MODE >= 0) {
-    const int64_t nbg = (int64_t)num_cus() - nbin - sb;
+    const int64_t nbg = bin_bg_wgs(nbin, sb, B > 1);
     if (Pf && nbg > 0 && (MODE != 0 || Pf->K == 1)) {
       Pf->fill_first = (int)bg_chunks(N, nbin, sb, Pf->H, Pf->W, MODE);
       MR_TIMED(KID_BIN_VIEW, st, (k_bin_view<MODE, CH><<<(unsigned)(nbin + sb + nbg), 1024, shm, st>>>(V, *Pf)));

@@ -91,6 +91,10 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
         * zbuf[..., 0] of K = 1 fragments (the nearest face's depth, -1 where no face) instead of
         * DepthRender's relu of it (camera_pose_optimizer.py:244-246 reads rasterizer(...).zbuf). */
        MR_OUT_ZBUF = 64,
+       /* bits 8-9 (MR_SREC_SLOT(k), k < 4), mr_render_forward / _reshade / _backward: which of the forward
+        * workspace's four per-face shading-record sets this call packs and its backward reads (0 for a
+        * plain forward; mr_render_reshade calls sharing one workspace take distinct slots) */
+       MR_SREC_SLOT_SHIFT = 8,
        /* mr_shade_fragments_* only: every pixel's empty slots (pix_to_face = -1) follow its filled
         * ones, as mr_rasterize_meshes[_world] (and PyTorch3D's rasterizer) write them; the kernels
         * then stop at a pixel's first empty slot instead of reading all K (same results) */
@@ -263,6 +267,20 @@ int32_t mr_render_forward_opencv(const mr_mesh_t* mesh, const mr_opencv_poses_t*
  * Writes grad_verts (V,3), grad_views (N,12), grad_vcolors (V,3; tex_kind 1 only, may be NULL).
  * `fwd_workspace` must be the one passed to the matching mr_render_forward: its face records and
  * covered-pixel list are reused (nothing is re-rasterized). */
+/* The caller's renderers often shade the SAME raster several times per step (camera_pose_optimizer.py:
+ * 244,248,250: rasterizer zbuf, silhouette and Phong renders of identical meshes / R / T / cameras /
+ * settings). mr_render_reshade shades again from a workspace a previous mr_render_forward[_opencv]
+ * filled for the same mesh geometry, views (`views` = that call's view records), sizes and raster
+ * settings: it skips projection, binning and rasterization (the winners, face records and fragments
+ * are reused) and runs vertex normals (when needed) -> this call's shading records (out_flags slot,
+ * MR_SREC_SLOT(k), k != the slots of the other calls still to be differentiated) -> background ->
+ * covered pixels. Outputs bitwise those of a full mr_render_forward with the same arguments. Its
+ * backward is mr_render_backward[_opencv] over the same workspace with the same out_flags slot. */
+int32_t mr_render_reshade(const mr_mesh_t* mesh, const mr_view_t* views, int64_t N, const float* cam_centers,
+                          int64_t n_cam_centers, const mr_raster_settings_t* s, const mr_shade_params_t* sp,
+                          float* depth, float* sil, float* rgb, int32_t* pix_to_face, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W);
 int32_t mr_render_backward(const mr_mesh_t* mesh, const float* vnormals_raw, const mr_view_t* views, int64_t N,
                            const float* cam_centers, int64_t num_cam_centers, const mr_raster_settings_t* rs,

@@ -166,3 +166,56 @@ def test_soft_silhouette_bench_config_vs_oracle():
     ref, r64, spread = oracle_runs(run, seeds=1)
     report("soft bench config silhouette (views 0, 40)", sel.detach(), ref[0], ref64=r64[0], sens=spread[0])
     report("soft bench config vertex grad", v.grad, ref[1], ref64=r64[1], sens=spread[1])
+
+
+def test_c3_three_calls_share_one_raster():
+    """camera_pose_optimizer.py:244,248,250: the rasterizer's zbuf, the silhouette render and the Phong render of
+    the same meshes / R / T / cameras / settings. The second and third calls re-shade the first call's raster
+    (mr_render_reshade). Outputs bitwise, and pose / vertex gradients bitwise, against three independent passes."""
+    from torch_renderer_amd import kernels as Kn
+    from torch_renderer_amd.mesh_renderer import PointLights, SoftPhongShader
+    from torch_renderer_amd.transforms import matrix_to_quaternion
+
+    H = W = 256
+    N = 6
+    meshes = load_asset("cow", device=DEV).extend(N)
+    cams = FoVPerspectiveCameras(device=DEV)
+    blend = BlendParams(sigma=1e-4, gamma=1e-4, background_color=(0, 0, 0))
+    rs = RasterizationSettings(image_size=H, blur_radius=0.0, faces_per_pixel=1)
+    sil_r = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs), SoftSilhouetteShader(blend_params=blend))
+    rast = MeshRasterizer(cameras=cams, raster_settings=rs)
+    lights = PointLights(device=DEV, location=[[0.0, 0.0, -3.0]])
+    phong = MeshRenderer(MeshRasterizer(cameras=cams, raster_settings=rs),
+                         SoftPhongShader(device=DEV, cameras=cams, lights=lights, blend_params=blend))
+    R0, T0 = look_at_view_transform(0.7, torch.linspace(10, 50, N), torch.linspace(0, 300, N), device=DEV)
+    q0 = torch.cat((T0, matrix_to_quaternion(R0)), -1)
+    g = torch.Generator().manual_seed(9)
+    gd, gs, gc = ((torch.rand(N, H, W, generator=g) - 0.5).to(DEV), (torch.rand(N, H, W, generator=g) - 0.5).to(DEV),
+                  (torch.rand(N, H, W, 3, generator=g) - 0.5).to(DEV))
+
+    def step(enabled):
+        Kn._RESHADE["enabled"] = enabled
+        Kn._RESHADE["entry"] = None
+        try:
+            q = q0.clone().requires_grad_(True)
+            R = quaternion_to_matrix(q[:, 3:])
+            T = q[:, :3]
+            depth = torch.relu(rast(meshes_world=meshes, R=R, T=T).zbuf[..., 0])
+            reused_after_sil = None
+            sil = sil_r(meshes, R=R, T=T)[..., 3]
+            ent = Kn._RESHADE["entry"]
+            reused_after_sil = None if ent is None else len(ent["served"])
+            color = phong(meshes, R=R, T=T)[..., :3]
+            ((depth * gd).sum() + (sil * gs).sum() + (color * gc).sum()).backward()
+            torch.cuda.synchronize()
+            return (depth.detach(), sil.detach(), color.detach(), q.grad.detach().clone()), reused_after_sil
+        finally:
+            Kn._RESHADE["enabled"] = True
+            Kn._RESHADE["entry"] = None
+
+    shared, served = step(True)
+    indep, served_off = step(False)
+    print(f"[reshade] shadings served by the first raster: {served} (disabled: {served_off})")
+    assert served == 2 and served_off == 1
+    for nm, a, b in zip(("depth", "silhouette", "colour", "pose grad"), shared, indep):
+        assert torch.equal(a, b), f"{nm} differs between the shared raster and three passes"

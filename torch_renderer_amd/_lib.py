@@ -26,6 +26,7 @@ MR_OUT_RGB = 4
 MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
 MR_OUT_SIL_RGBA = 32  # silhouette as (N,H,W,4) RGBA (1, 1, 1, alpha), fused render path
 MR_OUT_ZBUF = 64  # depth output = MeshRasterizer's zbuf[..., 0] (background -1), fused render path
+MR_SREC_SLOT_SHIFT = 8  # out_flags bits 8-9: the workspace's ShadeRec slot (mr_render_reshade)
 MR_FRAG_SORTED = 64  # mr_shade_fragments_*: empty slots follow the filled ones (this library's rasterizer)
 MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
 
@@ -139,6 +140,8 @@ _SIGS = [
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_workspace_counters", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),
     ("mr_per_view_binning", _I32, [_I64, _I64, _I32, _I32]),
+    ("mr_render_reshade", _I32, [ctypes.POINTER(MrMesh), _VP, _I64, _VP, _I64, ctypes.POINTER(MrRasterSettings),
+                                 ctypes.POINTER(MrShadeParams), _VP, _VP, _VP, _VP, _VP, _SZ, _VP]),
     ("mr_timing_enable", _I32, [_I32]),
     ("mr_timing_read", _I32, [_VP, _VP, _I32]),
     ("mr_timing_kernel_name", ctypes.c_char_p, [_I32]),

@@ -200,7 +200,7 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
   int64_t sb = 0;
   if (S) {
     V.S = *S;
-    V.srec = w.srec;
+    V.srec = Pf ? (ShadeRec*)Pf->srec : w.srec;  // the call's ShadeRec slot
     V.Fs = F;
     sb = ceil_div(F, 1024);
     // the fused render path: per-(record, tile) gradient rows for the deterministic backward
@@ -648,6 +648,8 @@ int32_t mr_vertex_normals(const float* verts, int64_t V, const int32_t* faces, i
   return MR_OK;
 }
 
+static int srec_slot(const mr_shade_params_t* sp) { return (sp->out_flags >> MR_SREC_SLOT_SHIFT) & (MR_SREC_SLOTS - 1); }
+
 static ShadeParams make_shade(const mr_mesh_t* m, const mr_shade_params_t* sp, const float* cc, int64_t ncc) {
   ShadeParams S;
   memset(&S, 0, sizeof(S));
@@ -765,7 +767,7 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   FwdParams P = make_fwd(s, g, w, N, m->view_face_first, multi ? 0 : m->F, NF);
   P.view_count = m->view_face_count;
   P.S = make_shade(m, sp, cc, ncc);
-  P.srec = w.srec;
+  P.srec = w.srec + (size_t)srec_slot(sp) * m->F;
   P.out_flags = sp->out_flags;
   P.depth = depth;
   P.sil = sil;
@@ -818,12 +820,74 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   MR_CHECK_LAUNCH("k_bin_count_world");
   if ((rc = launch_scan(w, N, g, m->view_face_count, m->F, st))) return rc;
   if (lds)
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<fgrid, 256, shm, st>>>(SP, m->F, fpt, (int)N, P.S, w.srec)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<true><<<fgrid, 256, shm, st>>>(SP, m->F, fpt, (int)N, P.S, (ShadeRec*)P.srec)));
   else
-    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<fgrid, 256, 0, st>>>(SP, m->F, fpt, (int)N, P.S, w.srec)));
+    MR_TIMED(KID_BIN_FILL, st, (k_bin_fill_world<false><<<fgrid, 256, 0, st>>>(SP, m->F, fpt, (int)N, P.S, (ShadeRec*)P.srec)));
   MR_CHECK_LAUNCH("k_bin_fill_world");
   if (sp->rgb_channels == 4) return launch_raster_and_shade<1, 4>(P, g, N, st, s->clip_z != 0);
   return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
+}
+
+int32_t mr_render_reshade(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
+                          const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
+                          float* rgb, int32_t* p2f32, void* ws, size_t ws_bytes, void* stream) {
+  int rc = check_settings(s);
+  if (rc) return rc;
+  rc = check_mesh(m, sp);
+  if (rc) return rc;
+  if (s->faces_per_pixel != 1) return set_err(MR_EUNSUPPORTED, "the fused render path is K = 1");
+  if (sp->out_flags & MR_OUT_HARD) return set_err(MR_EUNSUPPORTED, "hard_rgb_blend runs on the fragment-shader path");
+  if (N <= 0 || N > 65535) return set_err(MR_EINVAL, "N out of range");
+  const bool multi = m->view_face_first != nullptr;
+  const int64_t NF = multi ? m->F : N * m->F;
+  if ((int64_t)N * s->H * s->W >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "N*H*W >= 2^31");
+  if (!views || !ws) return set_err(MR_EINVAL, "NULL views / workspace");
+  if ((sp->out_flags & MR_OUT_DEPTH) && !depth) return set_err(MR_EINVAL, "depth output NULL");
+  if ((sp->out_flags & MR_OUT_SIL) && !sil) return set_err(MR_EINVAL, "silhouette output NULL");
+  if ((sp->out_flags & MR_OUT_RGB) && !rgb) return set_err(MR_EINVAL, "rgb output NULL");
+  if (sp->light_kind == 0 && (!cc || (ncc != 1 && ncc != N))) return set_err(MR_EINVAL, "camera centres");
+  hipStream_t st = (hipStream_t)stream;
+  BinGeom g = bin_geom(s->H, s->W, N, NF, s->max_faces_per_bin);
+  RasterWS w = carve_raster_ws(ws, N, NF, s->H, s->W, g, m->F);
+  if (ws_bytes < w.bytes) return set_err(MR_EWORKSPACE, "workspace too small: %zu < %zu", ws_bytes, w.bytes);
+  FwdParams P = make_fwd(s, g, w, N, m->view_face_first, multi ? 0 : m->F, NF);
+  P.view_count = m->view_face_count;
+  P.S = make_shade(m, sp, cc, ncc);
+  P.srec = w.srec + (size_t)srec_slot(sp) * m->F;
+  P.out_flags = sp->out_flags;
+  P.depth = depth;
+  P.sil = sil;
+  P.rgb = rgb;
+  P.p2f32 = p2f32;
+  if (sp->light_kind == 0 && m->vnormals_out) {  // this call's vertex normals (as the forward's first launch)
+    if (!m->vraw_out) return set_err(MR_EINVAL, "vnormals_out without vraw_out");
+    P.S.vnormals = m->vnormals_out;
+    MR_TIMED(KID_VNORMALS, st, (k_vertex_normals<<<ceil_div(m->V, 256), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out)));
+    MR_CHECK_LAUNCH("k_vertex_normals");
+  }
+  MR_TIMED(KID_SHADE_REC, st, (k_shade_rec<<<ceil_div(m->F, 256), 256, 0, st>>>(P.S, m->F, (ShadeRec*)P.srec)));
+  MR_CHECK_LAUNCH("k_shade_rec");
+  static int fg3 = 0, fg4 = 0, sg3 = 0, sg4 = 0;
+  const int64_t slots_cap = N * (int64_t)g.T;
+  auto shade_grid = [&](int gr) {
+    int sg = (int)(slots_cap / 4 + 1 < gr ? slots_cap / 4 + 1 : gr);
+    return (sg + 7) / 8 * 8;  // XCD-partitioned slot ranges
+  };
+  if (sp->rgb_channels == 4) {
+    if (!fg4) fg4 = resident_grid(k_fill<1, 4>, 256, 8);
+    if (!sg4) sg4 = resident_grid(k_shade<1, 4>, 256, 6);
+    MR_TIMED(KID_FILL_FRAG, st, (k_fill<1, 4><<<fg4, 256, 0, st>>>(P)));
+    MR_CHECK_LAUNCH("k_fill");
+    MR_TIMED(KID_SHADE_RENDER, st, (k_shade<1, 4><<<shade_grid(sg4), 256, 0, st>>>(P)));
+  } else {
+    if (!fg3) fg3 = resident_grid(k_fill<1, 3>, 256, 8);
+    if (!sg3) sg3 = resident_grid(k_shade<1, 3>, 256, 6);
+    MR_TIMED(KID_FILL_FRAG, st, (k_fill<1, 3><<<fg3, 256, 0, st>>>(P)));
+    MR_CHECK_LAUNCH("k_fill");
+    MR_TIMED(KID_SHADE_RENDER, st, (k_shade<1, 3><<<shade_grid(sg3), 256, 0, st>>>(P)));
+  }
+  MR_CHECK_LAUNCH("k_shade");
+  return MR_OK;
 }
 
 size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, int32_t W) {
@@ -914,7 +978,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.rgb_ch = sp->rgb_channels;
   P.sil_rgba = (sp->out_flags & MR_OUT_SIL_RGBA) ? 1 : 0;
   P.S = make_shade(m, sp, cc, ncc);
-  P.srec = w.srec;
+  P.srec = w.srec + (size_t)srec_slot(sp) * m->F;  // the forward's ShadeRec slot
   P.F = multi ? 0 : m->F;
   P.NF = NF;
   P.crec = w.crec;

@@ -82,6 +82,7 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 #ifndef MR_BANDS_MAX
 #define MR_BANDS_MAX 32  // per-view binning: workgroups (bands of tile rows) per view
 #endif
+#define MR_SREC_SLOTS 4  // ShadeRec sets per fused-forward workspace (out_flags bits 8-9 pick one)
 #define MR_UE 64  // (tile, face) entries per raster work unit (one wave, one entry per lane)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
 // ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)
@@ -178,8 +179,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(unsigned long long) * 64 * NT, 256);
   w.sface = (int*)(b + off);
   off = align_up(off + sizeof(int) * 64 * NT, 256);
-  w.srec = (ShadeRec*)(b + off);
-  off = align_up(off + sizeof(ShadeRec) * (size_t)Fshade, 256);
+  w.srec = (ShadeRec*)(b + off);  // MR_SREC_SLOTS slots of Fshade records (mr_render_reshade)
+  off = align_up(off + sizeof(ShadeRec) * MR_SREC_SLOTS * (size_t)Fshade, 256);
   w.grows = (float*)(b + off);
   off = align_up(off + sizeof(float) * 27 * (size_t)Fshade, 256);
   w.frec = (float4*)(b + off);

@@ -36,17 +36,24 @@ DEV = torch.device("cuda:0")
 @pytest.mark.parametrize("camera", ["fov_clip", "perspective"])
 def test_lazy_zbuf_fused_equals_modular(camera):
     """camera_pose_optimizer.py:244-246: rasterizer(meshes_world=..., R=, T=).zbuf[..., 0] (FoV camera:
-    near-plane clipping at znear / 2) and the PerspectiveCameras rasterizer of batch_rendering_test.py:274."""
-    H = W = 256
-    N = 8
+    near-plane clipping at znear / 2) and the PerspectiveCameras rasterizer of batch_rendering_test.py:274.
+    zbuf bitwise the modular rasterizer's; the gradients of relu(zbuf) (the fused depth backward) against the
+    oracle's within the per-entry bar (the modular path's too)."""
+    H = W = 192
+    N = 3
     meshes = load_asset("cow", device=DEV, textures=False)
     v0 = meshes.shared_verts().detach()
-    R, T = look_at_view_transform(0.35 if camera == "fov_clip" else 0.7, torch.linspace(5, 60, N),
-                                  torch.linspace(0, 330, N), device=DEV, at=(v0.mean(0).tolist(),))
+    dist = 0.35 if camera == "fov_clip" else 0.7
+    R, T = look_at_view_transform(dist, torch.linspace(5, 60, N), torch.linspace(0, 330, N), device=DEV,
+                                  at=(v0.mean(0).tolist(),))
     if camera == "fov_clip":
-        cams = FoVPerspectiveCameras(device=DEV, znear=0.3)
+        znear = 0.3
+        cams = FoVPerspectiveCameras(device=DEV, znear=znear)
+        t = 1.0 / math.tan(math.radians(30.0))
+        intr, z_clip = torch.tensor([[t, 0.0, t, 0.0]]), znear / 2
     else:
         cams = PerspectiveCameras(device=DEV, focal_length=((2.0, 2.0),))
+        intr, z_clip = torch.tensor([[2.0, 0.0, 2.0, 0.0]]), None
     rs = RasterizationSettings(image_size=H, blur_radius=0.0, faces_per_pixel=1)
     rast = MeshRasterizer(cameras=cams, raster_settings=rs)
     g = torch.Generator().manual_seed(5)
@@ -72,9 +79,23 @@ def test_lazy_zbuf_fused_equals_modular(camera):
     cov = int((zl >= 0).sum())
     print(f"[lazy zbuf] {camera}: covered {cov} of {zl.numel()} pixels, bitwise equal")
     assert cov > 0.02 * zl.numel()
-    _, *gm2 = run(False)
-    for nm, a, b, b2 in zip(("verts", "R", "T"), gl, gm, gm2):
-        report(f"lazy zbuf {camera} grad {nm} (fused vs modular)", a, b, tol=1e-5, sens=(b - b2).abs())
+    # the oracle: the same relu(zbuf) loss on the CPU restatement (and its float64 shadow)
+    verts_c, faces_c = v0.cpu(), meshes.shared_faces().cpu()
+    Rc, Tc, goc = R.cpu(), T.cpu(), go.cpu()
+
+    def oracle(precision):
+        vo = verts_c.clone().requires_grad_(True)
+        Ro, To = Rc.clone().requires_grad_(True), Tc.clone().requires_grad_(True)
+        ref = O.render_ref(vo, faces_c, Ro, To, intr.expand(N, 4).contiguous(), H, W, z_clip=z_clip,
+                           precision=precision)
+        (torch.relu(ref["zbuf"][..., 0]) * goc.to(ref["zbuf"].dtype)).sum().backward()
+        return ref["zbuf"].detach(), vo.grad, Ro.grad, To.grad
+
+    ref, r64, spread = oracle_runs(oracle, seeds=1)
+    assert torch.equal(zl.cpu(), ref[0]), "zbuf differs from the oracle's"
+    for nm, a, b, i in zip(("verts", "R", "T"), gl, gm, (1, 2, 3)):
+        report(f"lazy zbuf {camera} grad {nm} (fused depth backward)", a, ref[i], ref64=r64[i], sens=spread[i])
+        report(f"lazy zbuf {camera} grad {nm} (modular raster backward)", b, ref[i], ref64=r64[i], sens=spread[i])
 
 
 def test_pose_loss_rgba_slices_match_torch():
@@ -142,11 +163,11 @@ def test_soft_silhouette_bench_config_vs_oracle():
     ren = MeshRenderer(rasterizer=MeshRasterizer(cameras=cams, raster_settings=rs),
                        shader=SoftSilhouetteShader(blend_params=BlendParams(sigma=sigma)))
     img = ren(Meshes([v], [faces.to(DEV)]).extend(nv), cameras=cams, R=Rd, T=Td)
+    ws = img.grad_fn.saved_tensors[6]  # (read before the backward frees the saved tensors)
     sel = img[idx, ..., 3]
     ((sel - target.to(DEV)) ** 2).mean().backward()
     torch.cuda.synchronize()
     # the workspace's counters: the K-deep raster walked some tiles near-to-far (> 64 listed faces)
-    ws = img.grad_fn.saved_tensors[6]
     out8 = (ctypes.c_int32 * 8)()
     _lib.check(_lib.load().mr_workspace_counters(_lib.ptr(ws), nv, nv * faces.shape[0], H, W, 0,
                                                  ctypes.cast(out8, ctypes.c_void_p), _lib.stream_handle(DEV)))

@@ -451,7 +451,7 @@ MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__
       if (j < tot) {
         const float x = lrow[j];
         const int q = lq[r];
-        if (q >= 0) rows[(int64_t)q * ACC + c] = x;
+        if (q >= 0) rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
         else if (x != 0.0f) atomicAdd(gface + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
       }
     }
@@ -734,39 +734,53 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // rows the backward tagged — plus whatever the backward had to add with float atomics (gface rows of
 // records without rows, zero otherwise). Shared mesh: records n F + f (and NF + n F + f for a split
 // face's second triangle); distinct meshes (F_shared = 0): record f (and NF + f).
+// G lanes per face (G = the views rounded up to a power of two, at most 64: one wave per face for 64
+// views, 64 faces per wave for one view), each lane summing views j, j + G, ...; the G partial rows are
+// then summed by a fixed xor tree. Workgroups are dispatched round-robin over the 8 XCDs: block b takes
+// faces from XCD-contiguous ranges, so the per-record arrays (rbase, rects: n F + f) of neighbouring
+// faces are fetched into one XCD's L2 once.
 template <int ACC>
-__global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip,
+__global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
                                                      const int* __restrict__ rbase, const uint32_t* __restrict__ rects,
                                                      const uint8_t* __restrict__ rtag, const float* __restrict__ rows,
                                                      const float* __restrict__ gatom, float* __restrict__ gout) {
-  __shared__ float red[4][ACC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t f = (int64_t)blockIdx.x * 4 + wave;
-  if (f >= F) return;  // uniform over the wave (no workgroup barrier below)
+  const int fpb = 256 / G;  // faces per workgroup
+  const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
+  const int per = (int)gridDim.x / parts;
+  const int64_t blk = (int64_t)(blockIdx.x % parts) * per + blockIdx.x / parts;
+  const int64_t f = blk * fpb + (int64_t)((wave * 64 + lane) / G);
+  const int j = lane & (G - 1);
   float acc[ACC];
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
-  for (int n = lane; n < nv; n += 64) {
+  for (int n = j; n < nv && f < F; n += G) {
     for (int q = 0; q <= clip; ++q) {
       const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
       const int rb = rbase[rid];
       const int sz = rb >= 0 ? rect_size(rects[rid]) : 0;
       for (int k = 0; k < sz; ++k) {
         if (!rtag[rb + k]) continue;
-        const float* x = rows + (int64_t)(rb + k) * ACC;
+        const float4* x4 = (const float4*)(rows + (int64_t)(rb + k) * MR_ROW_STRIDE(ACC));
+        float x[MR_ROW_STRIDE(ACC)];
+#pragma unroll
+        for (int i = 0; i < MR_ROW_STRIDE(ACC) / 4; ++i) {
+          const float4 w = x4[i];
+          x[4 * i] = w.x; x[4 * i + 1] = w.y; x[4 * i + 2] = w.z; x[4 * i + 3] = w.w;
+        }
 #pragma unroll
         for (int i = 0; i < ACC; ++i) acc[i] += x[i];
       }
     }
   }
 #pragma unroll
-  for (int i = 0; i < ACC; ++i) {
-    const float t = wave_sum_f_dpp(acc[i]);
-    if (lane == 63) red[wave][i] = t;
+  for (int i = 0; i < ACC; ++i)
+    for (int o = 1; o < G; o <<= 1) acc[i] += __shfl_xor(acc[i], o, 64);  // fixed order inside the group
+  if (j == 0 && f < F) {
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) gout[f * ACC + i] = acc[i] + gatom[f * ACC + i];
   }
-  wave_lds_sync();
-  if (lane < ACC) gout[f * ACC + lane] = red[wave][lane] + gatom[f * ACC + lane];
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).
@@ -782,15 +796,23 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
   float acc[12];
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
-  for (int b = 0; b < bands; ++b) {
-    const int s0 = vslot[n * bands + b], ns = vslot[N * bands + n * bands + b];
-    for (int t = threadIdx.x; t < ns; t += 256) {
-      const float4* q = (const float4*)(part + ((int64_t)s0 + t) * 12);
-      const float4 a = q[0], c4 = q[1], c = q[2];
-      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-      acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
-      acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+  // the view's slots in tile order: its bands' ranges concatenated (band b holds tile rows above band b+1's).
+  // Thread t sums the slots t, t + 256, ... of that sequence, whatever the band split — the result does not
+  // depend on how many bands (i.e. on the batch size: a view's gradient is bitwise the same in any batch)
+  int b = 0, bs0 = vslot[n * bands], bn = vslot[N * bands + n * bands], before = 0;
+  for (int t = threadIdx.x;; t += 256) {
+    while (t - before >= bn && b + 1 < bands) {  // advance to the band holding sequence position t
+      before += bn;
+      ++b;
+      bs0 = vslot[n * bands + b];
+      bn = vslot[N * bands + n * bands + b];
     }
+    if (t - before >= bn) break;
+    const float4* q = (const float4*)(part + ((int64_t)bs0 + (t - before)) * 12);
+    const float4 a = q[0], c4 = q[1], c = q[2];
+    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+    acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
+    acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
   }
 #pragma unroll
   for (int i = 0; i < 12; ++i) {

@@ -1014,12 +1014,15 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   }
   MR_CHECK_LAUNCH("k_bwd_fused");
   {
-    const int nb = ceil_div(m->F, 4);
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
+    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 64)
+    while (G < 64 && G < (multi ? 1 : (int)N)) G <<= 1;
+    int nb = ceil_div(m->F, 256 / G);
+    nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {
-      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
-      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
       MR_CHECK_LAUNCH("k_face_reduce");
       gface = gtot;
     }

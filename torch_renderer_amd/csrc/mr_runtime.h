@@ -140,8 +140,10 @@ struct RasterWS {
   float* rrows;    // (list_cap * 18 floats) rows of 18 or 27 floats
   size_t bytes;
 };
-// Gradient rows of `acc` floats that fit the forward's row space (one per list entry of 18-float rows).
-static int64_t rows_cap(const BinGeom& g, int acc) { return g.list_cap * 18 / acc; }
+// Gradient rows of `acc` floats are stored 16-B aligned (stride MR_ROW_STRIDE(acc) floats: whole float4
+// loads in k_face_reduce); the row space holds one 18-float row per list entry.
+#define MR_ROW_STRIDE(acc) ((acc) == 27 ? 28 : 20)
+static int64_t rows_cap(const BinGeom& g, int acc) { return g.list_cap * 18 / MR_ROW_STRIDE(acc); }
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
                                 int64_t Fshade = 0) {
   (void)H; (void)W;

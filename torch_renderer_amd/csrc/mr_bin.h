@@ -963,8 +963,22 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int ex0 = block_incl_sum<true>(le, part, te) - le;
   const int iu = block_incl_sum<true>(my_u, part, au);
   const int is = block_incl_sum<true>(my_s, part, as);
-  // the three allocations from three waves: their round trips overlap instead of queueing
-  if (t == 0) {
+  // a view of one chunk (rectangles still in registers): its gradient rows are allocated here too,
+  // a fourth allocation overlapping the other three (see the rows block below)
+  const bool one = vcount <= 1024 * MR_VIEW_RPT;
+  int rows_mine = 0, rows_incl = 0, rows_tot = 0;
+  if (P.rbase && one) {
+#pragma unroll
+    for (int k = 0; k < MR_VIEW_RPT; ++k)
+      if (k % B == b)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) rows_mine += rect_size(rr[k][q]);
+    rows_incl = block_incl_sum<true>(rows_mine, part, rows_tot);
+  }
+  // the allocations from separate waves: their round trips overlap instead of queueing
+  if (t == 192 && P.rbase && one) {
+    rows_base = rows_tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], rows_tot) : 0;
+  } else if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
   } else if (t == 64) {
     // slot range of (view, band): the R/T reduction walks a view's bands in order
@@ -1024,20 +1038,23 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     // tile (row-major inside the rectangle) at rbase[rid] + k; the backward writes the row of every
     // (record, tile) it shades and k_face_reduce sums a face's rows in a fixed order (deterministic
     // vertex gradients, no float atomics). The records of chunk slot k belong to band k % bands; one
-    // row allocation per workgroup and chunk; the rows' tags are cleared here.
+    // row allocation per workgroup and chunk (a view of one chunk: made with the list allocations
+    // above); the rows' tags are cleared here.
 #pragma unroll 1
     for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
-      if (vcount > 1024 * MR_VIEW_RPT) load_chunk(i0);  // a view of one chunk: still in registers
-      int mine = 0;
+      int mine = rows_mine, incl = rows_incl, tot = rows_tot;
+      if (!one) {
+        load_chunk(i0);
+        mine = 0;
 #pragma unroll
-      for (int k = 0; k < MR_VIEW_RPT; ++k)
-        if (k % B == b)
+        for (int k = 0; k < MR_VIEW_RPT; ++k)
+          if (k % B == b)
 #pragma unroll
-          for (int q = 0; q < 2; ++q) mine += rect_size(rr[k][q]);
-      int tot;
-      const int incl = block_incl_sum<true>(mine, part, tot);
-      if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
-      lds_barrier();
+            for (int q = 0; q < 2; ++q) mine += rect_size(rr[k][q]);
+        incl = block_incl_sum<true>(mine, part, tot);
+        if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
+        lds_barrier();
+      }
       const long long wb = rows_base;
       long long rb = wb + incl - mine;
 #pragma unroll
@@ -1062,7 +1079,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // lane per cycle), the rest (a band larger than the stage) go straight to the pool
   int* stage = hist + ((Tb + (Tb >> 6) + 3) & ~3);
   const int lst = min(te, P.stage_cap);
-  const bool one = vcount <= 1024 * MR_VIEW_RPT;  // the rectangles are still in registers
 #pragma unroll 1
   for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
     if (!one) load_chunk(i0);

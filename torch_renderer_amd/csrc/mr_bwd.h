@@ -537,8 +537,12 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 
 // CLIP: near-plane clipping on (clipped sub-triangles may be present); the CLIP = false
 // instantiation carries none of the clip chain rule (fewer registers, no dynamic corner indexing).
+// Three waves per SIMD (<= 168 VGPRs): the sort / row staging pushed the kernel past 168, to two
+// waves; capped at three it keeps no VGPR spills (a few SGPRs) and measured 75 -> 64 us per launch
+// (render step 223k -> 232k frames/s, profiles/r4f_bands_ab.txt). Not the CLIP instantiation: its
+// clip chain rule would spill ~60 VGPRs under the cap.
 #ifndef MR_BWD_ATTR
-#define MR_BWD_ATTR
+#define MR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(CLIP ? 1 : 3)))
 #endif
 // The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
 // through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
@@ -755,22 +759,34 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
+  // Latency: the record's (rbase, rect) pair is loaded together, then the tags of up to 4 of its
+  // tiles at once, then those tiles' rows at once (an untagged tile loads the record's first row
+  // again, an L1 hit, and adds zero): three dependent round trips per 4 tiles instead of two per tile.
   for (int n = j; n < nv && f < F; n += G) {
     for (int q = 0; q <= clip; ++q) {
       const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
       const int rb = rbase[rid];
-      const int sz = rb >= 0 ? rect_size(rects[rid]) : 0;
-      for (int k = 0; k < sz; ++k) {
-        if (!rtag[rb + k]) continue;
-        const float4* x4 = (const float4*)(rows + (int64_t)(rb + k) * MR_ROW_STRIDE(ACC));
-        float x[MR_ROW_STRIDE(ACC)];
+      const uint32_t rc = rects[rid];
+      const int sz = rb >= 0 ? rect_size(rc) : 0;
+#pragma unroll 1
+      for (int k0 = 0; k0 < sz; k0 += 4) {
+        bool tg[4];
 #pragma unroll
-        for (int i = 0; i < MR_ROW_STRIDE(ACC) / 4; ++i) {
-          const float4 w = x4[i];
-          x[4 * i] = w.x; x[4 * i + 1] = w.y; x[4 * i + 2] = w.z; x[4 * i + 3] = w.w;
+        for (int u = 0; u < 4; ++u) tg[u] = k0 + u < sz && rtag[rb + min(k0 + u, sz - 1)] != 0;
+        float4 x4[4][MR_ROW_STRIDE(ACC) / 4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4* src = (const float4*)(rows + (int64_t)(tg[u] ? rb + k0 + u : rb) * MR_ROW_STRIDE(ACC));
+#pragma unroll
+          for (int i = 0; i < MR_ROW_STRIDE(ACC) / 4; ++i) x4[u][i] = src[i];
         }
 #pragma unroll
-        for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+        for (int u = 0; u < 4; ++u) {
+          if (!tg[u]) continue;
+          const float* x = (const float*)x4[u];
+#pragma unroll
+          for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+        }
       }
     }
   }

@@ -160,10 +160,16 @@ static int num_cus() {
   return cus;
 }
 // Workgroups (bands of tile rows) per view of the per-view binning: enough for the views to cover
-// the CUs (64 views -> 4 bands on 256 CUs), at most MR_BANDS_MAX and one tile row per band. A pure
-// function of the batch geometry: the backward's R/T reduction walks the same (view, band) ranges.
+// 1 / MR_BAND_CU_DIV of the CUs (1 view -> 32 bands, 16 views -> 4, 64 views -> 1 on 256 CUs), at
+// most MR_BANDS_MAX and one tile row per band. The CUs left over stream the background beside the
+// binning: banding 64 views 4 ways starved that share (fragment pass 421k -> 363k frames/s, render
+// 240k -> 223k, profiles/r4f_bands_ab.txt). A pure function of the batch geometry: the backward's
+// R/T reduction walks the same (view, band) ranges.
+#ifndef MR_BAND_CU_DIV
+#define MR_BAND_CU_DIV 4
+#endif
 static int bin_bands(int64_t N, const BinGeom& g) {
-  int64_t b = (int64_t)num_cus() / (N > 0 ? N : 1);
+  int64_t b = (int64_t)num_cus() / ((N > 0 ? N : 1) * MR_BAND_CU_DIV);
   if (b > MR_BANDS_MAX) b = MR_BANDS_MAX;
   if (b > g.TY) b = g.TY;
   return b < 1 ? 1 : (int)b;
@@ -859,7 +865,8 @@ int32_t mr_render_reshade(const mr_mesh_t* m, const mr_view_t* views, int64_t N,
   P.sil = sil;
   P.rgb = rgb;
   P.p2f32 = p2f32;
-  if (sp->light_kind == 0 && m->vnormals_out) {  // this call's vertex normals (as the forward's first launch)
+  // this call's vertex normals (as the forward's first launch), when its shading reads them: Phong RGB only
+  if (sp->light_kind == 0 && m->vnormals_out && (sp->out_flags & MR_OUT_RGB)) {
     if (!m->vraw_out) return set_err(MR_EINVAL, "vnormals_out without vraw_out");
     P.S.vnormals = m->vnormals_out;
     MR_TIMED(KID_VNORMALS, st, (k_vertex_normals<<<ceil_div(m->V, 256), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out)));

@@ -479,6 +479,39 @@ MR_DEV void fill_frag_unlisted(const FwdParams& P, int n, int c) {
 // on a forked stream overlapping binning was slower in the graph-replayed step, and the
 // raster's time barely drops without the fill.) k_fill is the stand-alone version, used
 // before k_raster_k (K > 1).
+// The fused render's background of one 64-quad chunk with lane-contiguous stores (one 1-KB burst per
+// store instruction, as the fragment background): the stand-alone fill of mr_render_reshade. (Inside
+// k_tile_raster the per-lane layout of fill_chunk measured faster: its stores interleave with the raster.)
+MR_DEV void fill_chunk_render_lc(const FwdParams& P, const Bg& b, int n, int c, int CH) {
+  const int lane = threadIdx.x & 63;
+  const int64_t HW = (int64_t)P.H * P.W;
+  const int64_t q0 = (int64_t)c * 64;
+  const int nq = (int)min((int64_t)64, HW / 4 - q0);
+  if (nq <= 0) return;
+  const int64_t pix = (int64_t)n * HW + 4 * q0;
+  if (P.out_flags & MR_OUT_DEPTH) fill_words<1>((float4*)(P.depth + pix), nq, lane, make_float4(b.d, b.d, b.d, b.d));
+  if (P.out_flags & MR_OUT_SIL) {
+    if (P.out_flags & MR_OUT_SIL_RGBA) fill_words<4>((float4*)(P.sil + pix * 4), nq, lane, make_float4(1.0f, 1.0f, 1.0f, b.s));
+    else fill_words<1>((float4*)(P.sil + pix), nq, lane, make_float4(b.s, b.s, b.s, b.s));
+  }
+  if (P.p2f32) fill_words<1>((int4*)(P.p2f32 + pix), nq, lane, make_int4(-1, -1, -1, -1));
+  if (P.out_flags & MR_OUT_RGB) {
+    float4* q = (float4*)(P.rgb + pix * CH);
+    if (CH == 4) {
+      fill_words<4>(q, nq, lane, make_float4(b.c[0], b.c[1], b.c[2], b.c[3]));
+    } else {  // period-3 pattern: word j of the chunk holds channels (4 j .. 4 j + 3) mod 3
+      const float4 w0 = make_float4(b.c[0], b.c[1], b.c[2], b.c[0]);
+      const float4 w1 = make_float4(b.c[1], b.c[2], b.c[0], b.c[1]);
+      const float4 w2 = make_float4(b.c[2], b.c[0], b.c[1], b.c[2]);
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int j = k * 64 + lane;
+        if (j < 3 * nq) q[j] = (j % 3) == 0 ? w0 : (j % 3) == 1 ? w1 : w2;
+      }
+    }
+  }
+}
+
 template <int MODE, int CH>
 __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
   const int gw = blockIdx.x * 4 + (threadIdx.x >> 6), G = gridDim.x * 4;
@@ -488,7 +521,10 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
   const int nchunks = P.N * cpv;
   const Bg bg = background<MODE>(P);
 #pragma unroll 1
-  for (int c = gw; c < nchunks; c += G) fill_chunk<MODE, CH>(P, bg, c / cpv, c - (c / cpv) * cpv, vec);
+  for (int c = gw; c < nchunks; c += G) {
+    if (MODE == 1 && vec) fill_chunk_render_lc(P, bg, c / cpv, c - (c / cpv) * cpv, CH);
+    else fill_chunk<MODE, CH>(P, bg, c / cpv, c - (c / cpv) * cpv, vec);
+  }
 }
 
 

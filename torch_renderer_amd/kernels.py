@@ -483,6 +483,9 @@ class RenderViews(torch.autograd.Function):
                 pose_cv=False, ranges=None):
         _require_cuda(verts, R, T, faces)
         ctx.set_materialize_grads(False)  # unused outputs get no zero-filled (N,H,W) grads
+        if not cfg.want_rgb and cfg.light_kind != 1:
+            # lights only shape the Phong colours: depth / silhouette renders need no vertex normals
+            cfg = ShadeConfig(**{**cfg.__dict__, "light_kind": 1})
         L = _lib.load()
         dev = verts.device
         v = verts.detach().float().contiguous()

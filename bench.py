@@ -807,6 +807,33 @@ def bench_gather(args, dev, world, rank):
         dist.destroy_process_group()
 
 
+def _host_profile(step, dev, n=20):
+    """Experiments only (MR_BENCH_CPROFILE=<file>): cProfile of n eager steps — where an eager caller
+    loop spends its host time (Python glue, launches) — written as text to <file>."""
+    path = os.environ.get("MR_BENCH_CPROFILE")
+    if not path:
+        return
+    import cProfile
+    import io
+    import pstats
+
+    pr = cProfile.Profile()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    pr.enable()
+    for _ in range(n):
+        step()
+    pr.disable()
+    torch.cuda.synchronize(dev)
+    s = io.StringIO()
+    s.write(f"{n} steps, {(time.perf_counter() - t0) / n * 1e3:.3f} ms/step under the profiler\n")
+    ps = pstats.Stats(pr, stream=s)
+    ps.sort_stats("tottime").print_stats(45)
+    ps.sort_stats("cumulative").print_stats(45)
+    with open(path, "w") as f:
+        f.write(s.getvalue())
+
+
 def _pose_refs(meshes, renderers, R, T):
     """camera_pose_optimizer.py:173-191: the reference silhouette mask, depth (-1 -> 0) and colour."""
     rast, sil_r, phong = renderers
@@ -914,6 +941,7 @@ def bench_pose(args, dev, world, rank):
 
     elapsed = _time_steps(step, args, dev, world)
     kt = _kernel_times(step, min(args.steps, 10))
+    _host_profile(step, dev)
     if rank != 0:
         dist.destroy_process_group()
         return

@@ -367,6 +367,19 @@ int32_t mr_pose_loss_backward(const float* depth, const float* sil, int64_t sil_
                               int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
                               int64_t npix, float delta, float w_color, const float* g_total, const void* fwd_ws,
                               float* g_depth, float* g_sil, float* g_rgb, void* stream);
+/* The forward that also writes the gradients for dL/dtotal = 1 (same layouts as mr_pose_loss_backward):
+ * the loss is linear in dL/dtotal, so one pass over the inputs serves both directions;
+ * mr_pose_loss_scale then multiplies the three buffers by the device scalar dL/dtotal in place (a no-op
+ * grid when it is 1). total (1 float) and terms (3: sil_loss, hloss, color_loss) are separate outputs;
+ * the gradient buffers are all three or all NULL (the loss alone). npix % 4 == 0 and 16-B aligned tensors
+ * take one fused launch, others the two-pass kernels. mr_pose_loss_scale needs npix % 4 == 0 and 16-B
+ * aligned gradient buffers. */
+int32_t mr_pose_loss_forward_grad(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                                  int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                                  int64_t npix, float delta, float w_color, float* total, float* terms, void* ws,
+                                  size_t ws_bytes, float* g_depth, float* g_sil, float* g_rgb, void* stream);
+int32_t mr_pose_loss_scale(const float* g_total, int64_t npix, int64_t sil_stride, int64_t rgb_stride, float* g_depth,
+                           float* g_sil, float* g_rgb, void* stream);
 
 /* upstream pytorch3d.transforms.quaternion_to_matrix (camera_pose_optimizer.py:241: the 7-vector
  * pose's real-first quaternion, not renormalised: two_s = 2 / |q|^2) for N quaternions q (rows

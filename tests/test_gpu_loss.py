@@ -66,3 +66,31 @@ def test_pose_loss_deterministic_and_empty_mask():
     assert torch.equal(a, b)
     args[3] = torch.zeros(shape, dtype=torch.bool, device=DEV)
     assert torch.isnan(pose_loss(*args))  # torch: mean over an empty selection
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 80), (3, 33, 47)])
+def test_pose_loss_upstream_scale_and_second_backward(shape):
+    """The forward writes the gradients for dL/dtotal = 1 (mr_pose_loss_forward_grad, one pass; the
+    (2, 64, 80) case is the vectorised kernel, (3, 33, 47) the two-pass fallback); a backward with
+    another upstream rescales them (mr_pose_loss_scale), and a second backward over a retained graph
+    recomputes them from the saved inputs: both against torch."""
+    g = torch.Generator().manual_seed(11)
+    depth = torch.rand(shape, generator=g) * 2
+    depth_ref = depth + (torch.rand(shape, generator=g) - 0.5) * 0.2
+    mask = torch.rand(shape, generator=g) > 0.4
+    sil = torch.rand(shape + (4,), generator=g)
+    rgba = torch.rand(shape + (4,), generator=g)
+    rgb_ref = torch.rand(shape + (3,), generator=g)
+    dr_, sr_, ir_ = (t.clone().requires_grad_(True) for t in (depth, sil, rgba))
+    tot_r, _ = _torch_loss(dr_, sr_[..., 3], ir_[..., :3], mask, depth_ref, rgb_ref)
+    (2.5 * tot_r).backward()
+    dg, sg, ig = (t.to(DEV).requires_grad_(True) for t in (depth, sil, rgba))
+    tot = pose_loss(dg, sg[..., 3], ig[..., :3], mask.to(DEV), depth_ref.to(DEV), rgb_ref.to(DEV))
+    (2.5 * tot).backward(retain_graph=True)
+    report("pose_loss x2.5 grad depth", dg.grad, dr_.grad, tol=1e-6)
+    report("pose_loss x2.5 grad sil image", sg.grad, sr_.grad, tol=1e-6)
+    report("pose_loss x2.5 grad rgba", ig.grad, ir_.grad, tol=1e-6)
+    g1 = [t.grad.clone() for t in (dg, sg, ig)]
+    tot.backward()  # second backward, upstream 1: the slow path from the saved inputs
+    for a, b, name in zip((dg.grad, sg.grad, ig.grad), g1, ("depth", "sil", "rgba")):
+        report(f"pose_loss second backward {name}", a - b, b / 2.5, tol=1e-6)

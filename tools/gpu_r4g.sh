@@ -31,6 +31,6 @@ timeout -k 10 300 python bench.py --mode pose --no-cpu-baseline --steps 20 --war
 python -c "import json,sys; d=json.loads(open('gpurun_out/pose_${TAG}.json').read().strip().splitlines()[-1]); print('pose', d['value'], d['ms_per_step'])"
 timeout -k 10 300 python bench.py --mode c5 --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/c5_${TAG}.json 2> gpurun_out/c5_${TAG}.err || { tail -20 gpurun_out/c5_${TAG}.err; exit 1; }
 python -c "import json,sys; d=json.loads(open('gpurun_out/c5_${TAG}.json').read().strip().splitlines()[-1]); print('c5', d['value'], d['ms_per_step'], {k:v['avg_us'] for k,v in d['kernels'].items()})"
-bash tools/gpu_ab_r4.sh ${TAG}r "" div2 div1 || exit 1
-bash tools/gpu_ab_r4.sh ${TAG}f "--mode fragments" div2 div1 || exit 1
+[ -n "$AB_R" ] && { bash tools/gpu_ab_r4.sh ${TAG}r "" $AB_R || exit 1; }
+[ -n "$AB_F" ] && { bash tools/gpu_ab_r4.sh ${TAG}f "--mode fragments" $AB_F || exit 1; }
 echo done

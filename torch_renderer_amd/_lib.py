@@ -135,6 +135,9 @@ _SIGS = [
                                     _VP, _VP, _SZ, _VP]),
     ("mr_pose_loss_backward", _I32, [_VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float, ctypes.c_float,
                                      _VP, _VP, _VP, _VP, _VP, _VP]),
+    ("mr_pose_loss_forward_grad", _I32, [_VP, _VP, _I64, _VP, _I64, _VP, _VP, _VP, _I64, ctypes.c_float,
+                                         ctypes.c_float, _VP, _VP, _VP, _SZ, _VP, _VP, _VP, _VP]),
+    ("mr_pose_loss_scale", _I32, [_VP, _I64, _I64, _I64, _VP, _VP, _VP, _VP]),
     ("mr_quaternion_to_matrix", _I32, [_VP, _I64, _I64, _VP, _VP]),
     ("mr_quaternion_to_matrix_backward", _I32, [_VP, _I64, _VP, _I64, _VP, _VP]),
     ("mr_workspace_stats", _I32, [_VP, _I64, _I64, _I32, _I32, _I32, _VP, _VP]),

@@ -24,7 +24,22 @@ struct SetupParams {
   uint32_t* rects;  // k_bin_view path: per-record tile rectangles
   float* fv_out;    // k_bin_rect_world: face_verts (N*F,3,3) written beside the records (NULL: none)
   const int64_t* vff;  // world mode, distinct meshes: first union face of each view (N+1); NULL: shared mesh
+  // fused render: the gradient-row slot tags of each record (one 32-bit word of MR_ROW_SLOTS tags at
+  // rec_slot(rid)), cleared by k_bin_rect_world beside the record (NULL: no rows)
+  uint32_t* rtagw;
+  int64_t rs_F;  // faces of the shared mesh (0: distinct meshes)
+  int rs_N;      // views
 };
+
+// Face-major slot of record rid (its MR_ROW_SLOTS gradient rows start at row MR_ROW_SLOTS * slot): a
+// shared mesh's face f has its N views' records side by side (second triangles of split faces after
+// every first one), so k_face_reduce reads a face's rows as one block; distinct meshes: the record id.
+MR_DEV int64_t rec_slot(int64_t rid, int64_t NF, int64_t F, int N) {
+  if (F == 0) return rid;
+  const int64_t q = rid >= NF ? 1 : 0, r = rid - q * NF;
+  const int64_t n = r / F, f = r - n * F;
+  return (q * F + f) * N + n;
+}
 
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP). Full EXEC required.
@@ -805,6 +820,11 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
     for (int q = 0; q < 4; ++q) s4[4 * t + q + (t >> 2)] = q4[q];
     P.rects[rid] = rec_rect(P, r);
     if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
+    if (P.rtagw) {
+      static_assert(MR_ROW_SLOTS == 4, "one 32-bit tag word per record");
+      P.rtagw[P.vff ? rid : fl * P.rs_N + n] = 0u;
+      if (CLIP) P.rtagw[P.vff ? P.NF + rid : (P.rs_F + fl) * P.rs_N + n] = 0u;
+    }
   }
   __syncthreads();
   float4* d4 = (float4*)(P.recs + rid0);
@@ -871,16 +891,23 @@ struct ViewBinParams {
   int64_t Fs;
   int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
   int stage_cap;  // list entries of a view staged in LDS (after the histogram)
-  // fused path: per-(record, tile) gradient rows for the deterministic backward (rbase NULL: none)
+  // fused path: overflow gradient rows (records of more than MR_ROW_SLOTS tiles) for the deterministic
+  // backward (rbase NULL: none); rtag = the pool's tags, rows_cap = its rows
   int* rbase;
   uint8_t* rtag;
   int64_t rows_cap;
 };
 
+
 // Tiles of a rectangle (0 for MR_RECT_NONE).
 MR_DEV int rect_size(uint32_t r) {
   const int tx0 = r & 255, tx1 = (r >> 8) & 255, ty0 = (r >> 16) & 255, ty1 = r >> 24;
   return tx1 < tx0 ? 0 : (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
+}
+// Pool rows of a record: its tiles when they exceed the record's fixed slots.
+MR_DEV int ovf_rows(uint32_t r) {
+  const int sz = rect_size(r);
+  return sz > MR_ROW_SLOTS ? sz : 0;
 }
 
 // The band-local tiles (ty - by0) * TX + tx of rectangle r inside tile rows [by0, by1).
@@ -972,7 +999,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     for (int k = 0; k < MR_VIEW_RPT; ++k)
       if (k % B == b)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) rows_mine += rect_size(rr[k][q]);
+        for (int q = 0; q < 2; ++q) rows_mine += ovf_rows(rr[k][q]);
     rows_incl = block_incl_sum<true>(rows_mine, part, rows_tot);
   }
   // the allocations from separate waves: their round trips overlap instead of queueing
@@ -1034,12 +1061,13 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
   if (P.rbase) {
-    // Gradient rows (fused render path): each record's tile rectangle gets consecutive rows, its k-th
-    // tile (row-major inside the rectangle) at rbase[rid] + k; the backward writes the row of every
-    // (record, tile) it shades and k_face_reduce sums a face's rows in a fixed order (deterministic
-    // vertex gradients, no float atomics). The records of chunk slot k belong to band k % bands; one
-    // row allocation per workgroup and chunk (a view of one chunk: made with the list allocations
-    // above); the rows' tags are cleared here.
+    // Overflow gradient rows (fused render path): a record of more than MR_ROW_SLOTS tiles gets
+    // consecutive pool rows, its k-th tile (row-major inside the rectangle) at rbase[rid] + k (the
+    // others use their fixed slots); the backward writes the row of every (record, tile) it shades and
+    // k_face_reduce sums a face's rows in a fixed order (deterministic vertex gradients, no float
+    // atomics). The records of chunk slot k belong to band k % bands; one pool allocation per
+    // workgroup and chunk (a view of one chunk: made with the list allocations above, none when no
+    // record overflows); the allocated rows' tags are cleared here.
 #pragma unroll 1
     for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
       int mine = rows_mine, incl = rows_incl, tot = rows_tot;
@@ -1050,7 +1078,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
         for (int k = 0; k < MR_VIEW_RPT; ++k)
           if (k % B == b)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) mine += rect_size(rr[k][q]);
+            for (int q = 0; q < 2; ++q) mine += ovf_rows(rr[k][q]);
         incl = block_incl_sum<true>(mine, part, tot);
         if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
         lds_barrier();
@@ -1063,9 +1091,9 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
           for (int q = 0; q < 2; ++q) {
             const int i = i0 + k * 1024 + j;
-            if (q < nq && i < vcount) {
-              const int sz = rect_size(rr[k][q]);
-              P.rbase[(q ? P.NF : 0) + f0 + i] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: rows full (atomics)
+            const int sz = ovf_rows(rr[k][q]);
+            if (q < nq && i < vcount && sz > 0) {
+              P.rbase[(q ? P.NF : 0) + f0 + i] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
               rb += sz;
             }
           }

@@ -351,11 +351,13 @@ struct RenderBwdParams {
                  // count -> scan path, and records whose rows did not fit)
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
   const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
-  // deterministic face gradients (k_bin_view's rows; rbase NULL: float atomics into gface)
+  // deterministic face gradients (rtag NULL: float atomics into gface): a record's fixed rows at
+  // MR_ROW_SLOTS * rec_slot(rid) + k, or (more than MR_ROW_SLOTS tiles) pool rows ovf0 + rbase[rid] + k
   const int* rbase;
   const uint32_t* rects;
   uint8_t* rtag;
   float* rrows;
+  int64_t ovf0;
 };
 
 // Order the 64 pixels of a slot by winning record (groups in order of first appearance, pixels of a
@@ -385,10 +387,11 @@ MR_DEV int sort_slot_pixels(int& f, int lane, int* lperm) {
 }
 
 // seg_stage for the row path: key = record id (runs are whole (tile, record) groups after
-// sort_slot_pixels), q = the run's gradient row (-1: float atomics into gface row `face`). The run
-// totals are staged in LDS with their row / face; the row's tag is set by the emitting lane.
+// sort_slot_pixels), q = the run's gradient row (-1: float atomics into gface row `face`), qf = the
+// record's slot-0 tag when q is a pool row (-1 otherwise). The run totals are staged in LDS with their
+// row / face; the row's tag is set by the emitting lane.
 template <int ACC>
-MR_DEV int seg_stage_rows(int key, int face, int q, float (&v)[ACC], float* lrow, int* lkey, int* lq,
+MR_DEV int seg_stage_rows(int key, int face, int q, int qf, float (&v)[ACC], float* lrow, int* lkey, int* lq,
                           uint8_t* __restrict__ rtag) {
   const int lane = threadIdx.x & 63;
   const int prev = dpp_wave_shr1(key, -2);
@@ -428,6 +431,7 @@ MR_DEV int seg_stage_rows(int key, int face, int q, float (&v)[ACC], float* lrow
     lkey[slot] = face;
     lq[slot] = q;
     if (q >= 0) rtag[q] = 1;
+    if (qf >= 0) rtag[qf] = 2;  // the record's rows are in the pool (its slot 0 says so)
 #pragma unroll
     for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
   }
@@ -713,16 +717,26 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
       }
     }
     // the run's gradient row: tile (tx, ty) is the k-th of the record's rectangle (row-major), its row
-    // rbase + k; -1 (float atomics) without rows, when the record's rows did not fit, or for a tile
-    // outside the rectangle (not expected: a winning pixel lies inside the record's padded bbox)
-    int q = -1;
-    if (P.rbase && f >= 0 && rb >= 0) {
+    // the record's slot row k (rectangles of <= MR_ROW_SLOTS tiles) or pool row rbase + k; -1 (float
+    // atomics) without rows, when the pool was full, or for a tile outside the rectangle (not expected:
+    // a winning pixel lies inside the record's padded bbox)
+    int q = -1, qf = -1;
+    if (P.rtag && f >= 0) {
       const int t = gt - n * P.T;
       const int ty = t / P.TX, tx = t - ty * P.TX;
       const int rx0 = rect & 255, rx1 = (rect >> 8) & 255, ry0 = (rect >> 16) & 255, ry1 = rect >> 24;
-      if (tx >= rx0 && tx <= rx1 && ty >= ry0 && ty <= ry1) q = rb + (ty - ry0) * (rx1 - rx0 + 1) + (tx - rx0);
+      if (tx >= rx0 && tx <= rx1 && ty >= ry0 && ty <= ry1) {
+        const int k = (ty - ry0) * (rx1 - rx0 + 1) + (tx - rx0);
+        const int slot0 = MR_ROW_SLOTS * (int)(P.F ? ((f >= P.NF ? P.F : 0) + face) * P.N + n : f);
+        if ((rx1 - rx0 + 1) * (ry1 - ry0 + 1) <= MR_ROW_SLOTS) {
+          q = slot0 + k;
+        } else if (rb >= 0) {
+          q = (int)P.ovf0 + rb + k;
+          qf = slot0;
+        }
+      }
     }
-    nt_prev = seg_stage_rows<ACC>(f >= 0 ? f : -1, key, q, row, lrow[wave], lkey[wave], lq[wave], P.rtag);
+    nt_prev = seg_stage_rows<ACC>(f >= 0 ? f : -1, key, q, qf, row, lrow[wave], lkey[wave], lq[wave], P.rtag);
     rt_prev = rt_partial(gR, gT, lane);
     s_prev = s;
   }
@@ -732,22 +746,22 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   }
 }
 
-// Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of its records'
-// (tile) rows over the views — one wave per face, lane = view (views 64 apart summed in order per
-// lane, then a fixed DPP tree), each lane walking its record's rectangle row by row and adding the
-// rows the backward tagged — plus whatever the backward had to add with float atomics (gface rows of
-// records without rows, zero otherwise). Shared mesh: records n F + f (and NF + n F + f for a split
-// face's second triangle); distinct meshes (F_shared = 0): record f (and NF + f).
-// G lanes per face (G = the views rounded up to a power of two, at most 64: one wave per face for 64
-// views, 64 faces per wave for one view), each lane summing views j, j + G, ...; the G partial rows are
-// then summed by a fixed xor tree. Workgroups are dispatched round-robin over the 8 XCDs: block b takes
-// faces from XCD-contiguous ranges, so the per-record arrays (rbase, rects: n F + f) of neighbouring
-// faces are fetched into one XCD's L2 once.
+// Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of the rows the
+// backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
+// with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
+// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block), read by
+// G lanes per face (G = the block's rows rounded up to a power of two, at most 64): lane j adds rows
+// j, j + G, ... of the block (one tag byte, then the row when tagged: consecutive lanes read consecutive
+// tags and rows), a record whose slot 0 holds 2 walks its pool rows instead; the G partial sums are then
+// added by a fixed xor tree. Workgroups are dispatched round-robin over the 8 XCDs: block b takes faces
+// from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
-                                                     const int* __restrict__ rbase, const uint32_t* __restrict__ rects,
-                                                     const uint8_t* __restrict__ rtag, const float* __restrict__ rows,
-                                                     const float* __restrict__ gatom, float* __restrict__ gout) {
+                                                     int64_t ovf0, const int* __restrict__ rbase,
+                                                     const uint32_t* __restrict__ rects, const uint8_t* __restrict__ rtag,
+                                                     const float* __restrict__ rows, const float* __restrict__ gatom,
+                                                     float* __restrict__ gout) {
+  constexpr int RS = MR_ROW_STRIDE(ACC);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fpb = 256 / G;  // faces per workgroup
   const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
@@ -759,33 +773,35 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
-  // Latency: the record's (rbase, rect) pair is loaded together, then the tags of up to 4 of its
-  // tiles at once, then those tiles' rows at once (an untagged tile loads the record's first row
-  // again, an L1 hit, and adds zero): three dependent round trips per 4 tiles instead of two per tile.
-  for (int n = j; n < nv && f < F; n += G) {
+  const int ns = nv * MR_ROW_SLOTS;  // rows of a face's block
+  auto add_row = [&](int64_t row) {
+    const float4* x4 = (const float4*)(rows + row * RS);
+    float x[RS];
+#pragma unroll
+    for (int i = 0; i < RS / 4; ++i) {
+      const float4 w = x4[i];
+      x[4 * i] = w.x; x[4 * i + 1] = w.y; x[4 * i + 2] = w.z; x[4 * i + 3] = w.w;
+    }
+#pragma unroll
+    for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+  };
+  if (f < F) {
     for (int q = 0; q <= clip; ++q) {
-      const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
-      const int rb = rbase[rid];
-      const uint32_t rc = rects[rid];
-      const int sz = rb >= 0 ? rect_size(rc) : 0;
+      // first slot of the block: rec_slot of the face's record in view 0
+      const int64_t b0 = (int64_t)MR_ROW_SLOTS * (F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f);
 #pragma unroll 1
-      for (int k0 = 0; k0 < sz; k0 += 4) {
-        bool tg[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) tg[u] = k0 + u < sz && rtag[rb + min(k0 + u, sz - 1)] != 0;
-        float4 x4[4][MR_ROW_STRIDE(ACC) / 4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4* src = (const float4*)(rows + (int64_t)(tg[u] ? rb + k0 + u : rb) * MR_ROW_STRIDE(ACC));
-#pragma unroll
-          for (int i = 0; i < MR_ROW_STRIDE(ACC) / 4; ++i) x4[u][i] = src[i];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (!tg[u]) continue;
-          const float* x = (const float*)x4[u];
-#pragma unroll
-          for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+      for (int sidx = j; sidx < ns; sidx += G) {
+        const uint8_t tg = rtag[b0 + sidx];
+        if (tg == 1) {
+          add_row(b0 + sidx);
+        } else if (tg == 2) {  // (slot 0 of a record whose rows are in the pool)
+          const int n = sidx / MR_ROW_SLOTS;
+          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
+          const int rb = rbase[rid];
+          const int sz = rect_size(rects[rid]);
+#pragma unroll 1
+          for (int k = 0; k < sz; ++k)
+            if (rtag[ovf0 + rb + k]) add_row(ovf0 + rb + k);
         }
       }
     }

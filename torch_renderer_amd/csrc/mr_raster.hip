@@ -80,6 +80,7 @@ size_t mr_rasterize_meshes_workspace(int64_t num_meshes, int64_t total_faces, in
 
 static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, const RasterWS& w) {
   SetupParams P;
+  memset(&P, 0, sizeof(P));
   P.H = s->H; P.W = s->W; P.TX = g.TX; P.TY = g.TY; P.T = g.T;
   P.bbox_pad = sqrtf(s->blur_radius);
   P.persp = s->perspective_correct;
@@ -209,10 +210,12 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.srec = Pf ? (ShadeRec*)Pf->srec : w.srec;  // the call's ShadeRec slot
     V.Fs = F;
     sb = ceil_div(F, 1024);
-    // the fused render path: per-(record, tile) gradient rows for the deterministic backward
-    V.rbase = w.rbase;
-    V.rtag = w.rtag;
-    V.rows_cap = rows_cap(g, S->tex_kind == 1 ? 27 : 18);
+    // the fused render path: pool rows of the records too large for their fixed gradient-row slots
+    if (rows_fit(w)) {
+      V.rbase = w.rbase;
+      V.rtag = w.rtag + w.ovf0;
+      V.rows_cap = w.ovf_cap;
+    }
   }
   V.nsrec_wg = (int)sb;
   V.T = g.T; V.TX = g.TX; V.TY = g.TY; V.mfpb = g.mfpb; V.clipz = SP.clipz;
@@ -770,6 +773,11 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   SetupParams SP = make_setup(s, g, w);
   SP.NF = NF;
   SP.vff = m->view_face_first;
+  if (rows_fit(w)) {  // the gradient rows' slot tags, cleared beside the records
+    SP.rtagw = (uint32_t*)w.rtag;
+    SP.rs_F = multi ? 0 : m->F;
+    SP.rs_N = (int)N;
+  }
   FwdParams P = make_fwd(s, g, w, N, m->view_face_first, multi ? 0 : m->F, NF);
   P.view_count = m->view_face_count;
   P.S = make_shade(m, sp, cc, ncc);
@@ -994,14 +1002,15 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.gface = gface;
   P.rt_part = rt_part;
   P.frec = w.frec;
-  // per-(record, tile) gradient rows: allocated by the per-view binning (k_bin_view) of the fused
-  // forward; the count -> scan path has none (float atomics into gface)
-  const bool vpath = view_binning(g, N, NF);
+  // per-(record, tile) gradient rows: fixed slots (tags cleared by k_bin_rect_world) and the pool the
+  // per-view binning (k_bin_view) allocates; the count -> scan path has none (float atomics into gface)
+  const bool vpath = view_binning(g, N, NF) && rows_fit(w);
   if (vpath) {
     P.rbase = w.rbase;
     P.rects = w.rects;
     P.rtag = w.rtag;
     P.rrows = w.rrows;
+    P.ovf0 = w.ovf0;
   }
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
@@ -1023,13 +1032,13 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   {
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 64)
-    while (G < 64 && G < (multi ? 1 : (int)N)) G <<= 1;
+    int G = 1;  // lanes per face: the rows of a face's slot block, rounded up to a power of two (<= 64)
+    while (G < 64 && G < (multi ? 1 : (int)N) * MR_ROW_SLOTS) G <<= 1;
     int nb = ceil_div(m->F, 256 / G);
     nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {
-      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
-      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.ovf0, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
+      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.ovf0, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
       MR_CHECK_LAUNCH("k_face_reduce");
       gface = gtot;
     }
@@ -1270,7 +1279,8 @@ static int pose_loss_params(PoseLossParams& P, const float* depth, const float* 
 
 size_t mr_pose_loss_workspace(int64_t npix) {
   (void)npix;
-  return align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256) + 256;
+  return align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256) + 256 +
+         align_up(sizeof(int) * MR_LOSS_BLOCKS, 256);
 }
 
 int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
@@ -1290,8 +1300,71 @@ int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_s
   hipStream_t st = (hipStream_t)stream;
   k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
   MR_CHECK_LAUNCH("k_pose_loss_partial");
-  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, out, count);
+  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, out, out + 1, count);
   MR_CHECK_LAUNCH("k_pose_loss_final");
+  return MR_OK;
+}
+
+// The forward writing the gradients for dL/dtotal = 1 too (see k_pose_loss_fused); mr_pose_loss_scale
+// turns them into the backward's for any dL/dtotal.
+int32_t mr_pose_loss_forward_grad(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
+                                  int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
+                                  int64_t npix, float delta, float w_color, float* total, float* terms, void* ws,
+                                  size_t ws_bytes, float* g_depth, float* g_sil, float* g_rgb, void* stream) {
+  PoseLossParams P;
+  int rc = pose_loss_params(P, depth, sil, sil_stride, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
+  if (rc) return rc;
+  if (!total || !terms || !ws) return set_err(MR_EINVAL, "NULL output / workspace");
+  const bool grads = g_depth || g_sil || g_rgb;
+  if (grads && !(g_depth && g_sil && g_rgb)) return set_err(MR_EINVAL, "gradient buffers: all three or none");
+  if (ws_bytes < mr_pose_loss_workspace(npix)) return set_err(MR_EWORKSPACE, "loss workspace too small");
+  if ((sil_stride == 4 && ((uintptr_t)g_sil & 15)) || (rgb_stride == 4 && ((uintptr_t)g_rgb & 15)))
+    return set_err(MR_EINVAL, "RGBA gradient buffers must be 16-byte aligned");
+  char* w = (char*)ws;
+  float* part = (float*)w;
+  int* pcnt = (int*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256));
+  int64_t* count = (int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
+  int* mcnt = (int*)((char*)count + 256);
+  hipStream_t st = (hipStream_t)stream;
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  const bool vec = grads && npix % 4 == 0 && a16(depth) && a16(depth_ref) && ((uintptr_t)mask & 3) == 0 &&
+                   a16(sil_stride == 4 ? (const void*)(sil - 3) : (const void*)sil) && a16(rgb) && a16(rgb_ref) &&
+                   a16(g_depth) && a16(g_sil) && a16(g_rgb);
+  if (!vec) {  // the two-pass kernels (the loss alone without gradient buffers)
+    const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
+    k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
+    MR_CHECK_LAUNCH("k_pose_loss_partial");
+    k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, total, terms, count);
+    MR_CHECK_LAUNCH("k_pose_loss_final");
+    if (grads) {
+      k_pose_loss_bwd<<<(unsigned)ceil_div(npix, 256), 256, 0, st>>>(P, nullptr, count, g_depth, g_sil, g_rgb);
+      MR_CHECK_LAUNCH("k_pose_loss_bwd");
+    }
+    return MR_OK;
+  }
+  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix / 4, 256));
+  k_mask_count<<<nb, 256, 0, st>>>(mask, npix, mcnt);
+  MR_CHECK_LAUNCH("k_mask_count");
+  k_pose_loss_fused<<<nb, 256, 0, st>>>(P, mcnt, nb, part, pcnt, g_depth, g_sil, g_rgb);
+  MR_CHECK_LAUNCH("k_pose_loss_fused");
+  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, total, terms, count);
+  MR_CHECK_LAUNCH("k_pose_loss_final");
+  return MR_OK;
+}
+
+int32_t mr_pose_loss_scale(const float* g_total, int64_t npix, int64_t sil_stride, int64_t rgb_stride, float* g_depth,
+                           float* g_sil, float* g_rgb, void* stream) {
+  if (npix <= 0) return set_err(MR_EINVAL, "npix must be > 0");
+  if (!g_total || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL argument");
+  if ((sil_stride != 1 && sil_stride != 4) || (rgb_stride != 3 && rgb_stride != 4))
+    return set_err(MR_EINVAL, "bad strides");
+  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (npix % 4 || !a16(g_depth) || !a16(g_sil) || !a16(g_rgb))
+    return set_err(MR_EINVAL, "gradient buffers: npix % 4 == 0 and 16-byte alignment required");
+  const int64_t nd = npix / 4, ns = npix * sil_stride / 4, nc = npix * rgb_stride / 4;
+  k_pose_loss_scale<<<1024, 256, 0, (hipStream_t)stream>>>(g_total, nd, ns, nc, (float4*)g_depth, (float4*)g_sil,
+                                                            (float4*)g_rgb);
+  MR_CHECK_LAUNCH("k_pose_loss_scale");
   return MR_OK;
 }
 

@@ -134,16 +134,27 @@ struct RasterWS {
   float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
   // fused path, deterministic face gradients: the backward writes one gradient row per (record, tile)
-  // it shades (plain stores, no float atomics), k_face_reduce sums each face's rows in a fixed order
-  int* rbase;      // (2 * Ftot) first row of each record's tile rectangle (k_bin_view; -1: rows full)
-  uint8_t* rtag;   // (rows_cap) 1 = the backward wrote the row, cleared by k_bin_view
-  float* rrows;    // (list_cap * 18 floats) rows of 18 or 27 floats
+  // it shades (plain stores, no float atomics), k_face_reduce sums each face's rows in a fixed order.
+  // Rows: MR_ROW_SLOTS fixed slots per record, face-major (rec_slot: a face's records of all views
+  // side by side, so the reduction reads each face's rows as one contiguous block), for records of
+  // <= MR_ROW_SLOTS tiles; the rest (larger faces) take rows from an overflow pool allocated by k_bin_view.
+  int* rbase;      // (2 * Ftot) overflow records: first pool row of their tile rectangle (-1: pool full)
+  uint8_t* rtag;   // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) 1 = the backward wrote the row; a record's slot 0 holds
+                   // 2 when its rows are in the pool. Slot tags cleared by k_bin_rect_world, pool tags by k_bin_view
+  float* rrows;    // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) rows of MR_ROW_STRIDE(acc) floats
+  int64_t ovf0;    // first pool row (= MR_ROW_SLOTS * 2 Ftot)
+  int64_t ovf_cap; // pool rows
   size_t bytes;
 };
 // Gradient rows of `acc` floats are stored 16-B aligned (stride MR_ROW_STRIDE(acc) floats: whole float4
-// loads in k_face_reduce); the row space holds one 18-float row per list entry.
+// loads in k_face_reduce). MR_ROW_SLOTS = 4 fixed rows per record cover a face's 1, 2 (straddling a tile
+// edge) or 4 (a tile corner) tiles; the overflow pool holds list_cap / 2 rows (room for one screen-filling
+// face per view besides ~3 Ftot entries), past which rows fall back to float atomics.
 #define MR_ROW_STRIDE(acc) ((acc) == 27 ? 28 : 20)
-static int64_t rows_cap(const BinGeom& g, int acc) { return g.list_cap * 18 / MR_ROW_STRIDE(acc); }
+#ifndef MR_ROW_SLOTS
+#define MR_ROW_SLOTS 4
+#endif
+static int64_t row_ovf_cap(const BinGeom& g) { return g.list_cap / 2; }
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
                                 int64_t Fshade = 0) {
   (void)H; (void)W;
@@ -191,13 +202,18 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   w.rbase = (int*)(b + off);
   off = align_up(off + (Fshade > 0 ? sizeof(int) * 2 * (size_t)(Ftot > 0 ? Ftot : 1) : 0), 256);
+  w.ovf0 = (int64_t)MR_ROW_SLOTS * 2 * (Ftot > 0 ? Ftot : 1);
+  w.ovf_cap = row_ovf_cap(g);
+  const size_t nrows = Fshade > 0 ? (size_t)(w.ovf0 + w.ovf_cap) : 0;
   w.rtag = (uint8_t*)(b + off);
-  off = align_up(off + (Fshade > 0 ? (size_t)g.list_cap : 0), 256);
+  off = align_up(off + nrows, 256);
   w.rrows = (float*)(b + off);
-  off = align_up(off + (Fshade > 0 ? sizeof(float) * 18 * (size_t)g.list_cap : 0), 256);
+  off = align_up(off + sizeof(float) * MR_ROW_STRIDE(27) * nrows, 256);
   w.bytes = off;
   return w;
 }
+// The fused path's gradient rows are addressed with 32-bit row numbers (else: float atomics).
+static bool rows_fit(const RasterWS& w) { return w.ovf0 + w.ovf_cap < (1ll << 31) - 1; }
 // Bytes to clear from w.ctr before a forward: the counters and, on the count -> scan path, the
 // per-tile counts and per-view totals.
 static size_t zero_bytes(int64_t N, const BinGeom& g, bool view_path) {

@@ -1,7 +1,9 @@
 """Fused pose-optimiser loss.
 
-``pose_loss`` is camera_pose_optimizer.py:257-276 ``Model.calc_loss`` in two HIP launches forward
-and one backward (``mr_pose_loss_*``), instead of ~15 torch elementwise / reduction kernels:
+``pose_loss`` is camera_pose_optimizer.py:257-276 ``Model.calc_loss`` in three HIP launches forward
+(mask count, one pass that sums the loss AND writes its gradients for dL/dtotal = 1, final reduction)
+and one near-empty rescale in the backward (``mr_pose_loss_*``), instead of ~15 torch elementwise /
+reduction kernels forward and as many backward:
 
 * ``sil_loss   = torch.nn.L1Loss()(silhouette, mask.float())``
 * ``hloss      = torch.nn.HuberLoss(delta=0.05)(depth[mask], depth_ref[mask])``
@@ -79,21 +81,39 @@ class PoseLoss(torch.autograd.Function):
         rr = rgb_ref.detach().float().contiguous()
         wsb = int(L.mr_pose_loss_workspace(npix))
         ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
-        out = torch.empty(4, device=dev)
-        stream = _lib.stream_handle(dev)
-        check(L.mr_pose_loss_forward(_vp(d), s_ptr, s_stride, _vp(c), stride, _vp(m), _vp(dr), _vp(rr), npix,
-                                     float(delta), float(w_color), _vp(out), _vp(ws), wsb, stream))
+        total = torch.empty((), device=dev)
+        terms = torch.empty(3, device=dev)
+        ctx.pre = None
+        gd = gs = gc = None
+        if any(ctx.needs_input_grad[:3]):
+            # one pass: the gradients for dL/dtotal = 1 are written with the forward (the loss is linear
+            # in dL/dtotal); the first backward rescales them in place unless dL/dtotal is 1
+            gd = torch.empty_like(d)
+            gs = torch.empty((npix, s_stride), device=dev)
+            gc = torch.empty((npix, stride), device=dev)
+            ctx.pre = (gd, gs, gc)
+        check(L.mr_pose_loss_forward_grad(_vp(d), s_ptr, s_stride, _vp(c), stride, _vp(m), _vp(dr), _vp(rr), npix,
+                                          float(delta), float(w_color), _vp(total), _vp(terms), _vp(ws), wsb,
+                                          _lib.ptr(gd), _lib.ptr(gs), _lib.ptr(gc), _lib.stream_handle(dev)))
         ctx.save_for_backward(d, s, c, m, dr, rr, ws)
         ctx.stride, ctx.s_stride, ctx.npix, ctx.delta, ctx.w_color = stride, s_stride, npix, float(delta), float(w_color)
         ctx.shapes = (depth.shape, sil_in.shape, color_in.shape)
-        terms = out[1:].clone()
         ctx.mark_non_differentiable(terms)
-        return out[0].clone(), terms
+        return total, terms
 
     @staticmethod
     def backward(ctx, g_total, g_terms):
-        d, s, c, m, dr, rr, ws = ctx.saved_tensors
         L = _lib.load()
+        sd, ss, sc = ctx.shapes
+        if ctx.pre is not None:  # the forward's gradients, scaled by dL/dtotal (first backward only)
+            gd, gs, gc = ctx.pre
+            ctx.pre = None
+            dev = gd.device
+            g = (g_total if g_total is not None else torch.zeros((), device=dev)).float().contiguous().reshape(1)
+            check(L.mr_pose_loss_scale(_vp(g), ctx.npix, ctx.s_stride, ctx.stride, _vp(gd), _vp(gs), _vp(gc),
+                                       _lib.stream_handle(dev)))
+            return gd.reshape(sd), gs.reshape(ss), gc.reshape(sc), None, None, None, None, None, None, None
+        d, s, c, m, dr, rr, ws = ctx.saved_tensors
         dev = d.device
         g = (g_total if g_total is not None else torch.zeros((), device=dev)).float().contiguous().reshape(1)
         gd = torch.empty_like(d)
@@ -103,7 +123,6 @@ class PoseLoss(torch.autograd.Function):
         check(L.mr_pose_loss_backward(_vp(d), s_ptr, ctx.s_stride, _vp(c), ctx.stride, _vp(m), _vp(dr), _vp(rr),
                                       ctx.npix, ctx.delta, ctx.w_color, _vp(g), _vp(ws), _vp(gd), _vp(gs), _vp(gc),
                                       _lib.stream_handle(dev)))
-        sd, ss, sc = ctx.shapes
         return gd.reshape(sd), gs.reshape(ss), gc.reshape(sc), None, None, None, None, None, None, None
 
 

@@ -371,9 +371,7 @@ int32_t mr_pose_loss_backward(const float* depth, const float* sil, int64_t sil_
  * the loss is linear in dL/dtotal, so one pass over the inputs serves both directions;
  * mr_pose_loss_scale then multiplies the three buffers by the device scalar dL/dtotal in place (a no-op
  * grid when it is 1). total (1 float) and terms (3: sil_loss, hloss, color_loss) are separate outputs;
- * the gradient buffers are all three or all NULL (the loss alone). npix % 4 == 0 and 16-B aligned tensors
- * take one fused launch, others the two-pass kernels. mr_pose_loss_scale needs npix % 4 == 0 and 16-B
- * aligned gradient buffers. */
+ * the gradient buffers are all three or all NULL (the loss alone); RGBA gradient buffers 16-B aligned. */
 int32_t mr_pose_loss_forward_grad(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
                                   int64_t rgb_stride, const uint8_t* mask, const float* depth_ref, const float* rgb_ref,
                                   int64_t npix, float delta, float w_color, float* total, float* terms, void* ws,

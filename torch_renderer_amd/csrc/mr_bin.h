@@ -24,11 +24,6 @@ struct SetupParams {
   uint32_t* rects;  // k_bin_view path: per-record tile rectangles
   float* fv_out;    // k_bin_rect_world: face_verts (N*F,3,3) written beside the records (NULL: none)
   const int64_t* vff;  // world mode, distinct meshes: first union face of each view (N+1); NULL: shared mesh
-  // fused render: the gradient-row slot tags of each record (one 32-bit word of MR_ROW_SLOTS tags at
-  // rec_slot(rid)), cleared by k_bin_rect_world beside the record (NULL: no rows)
-  uint32_t* rtagw;
-  int64_t rs_F;  // faces of the shared mesh (0: distinct meshes)
-  int rs_N;      // views
 };
 
 // Face-major slot of record rid (its MR_ROW_SLOTS gradient rows start at row MR_ROW_SLOTS * slot): a
@@ -684,6 +679,8 @@ struct NormalsArgs {
   float* vraw;
   float4* zero4;   // the fused backward's face-gradient rows, cleared here (nzero4 float4s; NULL: none)
   int64_t nzero4;
+  uint4* ztag;     // the gradient rows' slot tags, cleared here (nztag 16-B words; NULL: none)
+  int64_t nztag;
 };
 // OpenCV poses converted on the fly (mr_render_forward_opencv): element k of view n's record,
 // as k_views_from_opencv writes it (torch_renderer.py:73-80; bitwise the torch conversion).
@@ -772,6 +769,7 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
     for (int64_t i = v; i < NA.nzero4; i += (int64_t)gridDim.x * blockDim.x) NA.zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int64_t i = v; i < NA.nztag; i += (int64_t)gridDim.x * blockDim.x) NA.ztag[i] = make_uint4(0u, 0u, 0u, 0u);
     if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
     return;
   }
@@ -820,11 +818,6 @@ static_assert(sizeof(FaceRec) == 64, "FaceRec is staged as 4 float4");
     for (int q = 0; q < 4; ++q) s4[4 * t + q + (t >> 2)] = q4[q];
     P.rects[rid] = rec_rect(P, r);
     if (CLIP) P.rects[P.NF + rid] = (r.flags & FR_PAIR) ? rec_rect(P, r2) : MR_RECT_NONE;
-    if (P.rtagw) {
-      static_assert(MR_ROW_SLOTS == 4, "one 32-bit tag word per record");
-      P.rtagw[P.vff ? rid : fl * P.rs_N + n] = 0u;
-      if (CLIP) P.rtagw[P.vff ? P.NF + rid : (P.rs_F + fl) * P.rs_N + n] = 0u;
-    }
   }
   __syncthreads();
   float4* d4 = (float4*)(P.recs + rid0);

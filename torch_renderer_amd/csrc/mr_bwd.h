@@ -510,8 +510,9 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
 // sub-triangle's corners (run with C g_orig); map it to the ORIGINAL face's projected corners
 // through the clip's chain rule (sub-corners and the conversion weights), the original corners
 // re-projected from the world corners. g_orig: gradient w.r.t. the original-face barycentrics.
-MR_DEV void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f, const ViewRec& V, const float X[3][3],
-                          float px, float py, const float g_orig[3], float gfv[3][3]) {
+__attribute__((noinline)) __device__ void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f,
+                                                         const ViewRec& V, const float X[3][3], float px, float py,
+                                                         const float g_orig[3], float gfv[3][3]) {
   const ClipRec cr = P.crec[f];
   FragEval e;
   eval_face(r, px, py, P.bbox_pad, P.blur, P.persp, P.clipb, e);
@@ -751,8 +752,8 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
 // are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block), read by
 // G lanes per face (G = the block's rows rounded up to a power of two, at most 64): lane j adds rows
-// j, j + G, ... of the block (one tag byte, then the row when tagged: consecutive lanes read consecutive
-// tags and rows), a record whose slot 0 holds 2 walks its pool rows instead; the G partial sums are then
+// j, j + G, ... of the block in that order (one tag byte, then the row when tagged: consecutive lanes
+// read consecutive tags and rows), a record whose slot 0 holds 2 walks its pool rows instead; the G partial sums are then
 // added by a fixed xor tree. Workgroups are dispatched round-robin over the 8 XCDs: block b takes faces
 // from XCD-contiguous ranges.
 template <int ACC>
@@ -789,19 +790,36 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
     for (int q = 0; q <= clip; ++q) {
       // first slot of the block: rec_slot of the face's record in view 0
       const int64_t b0 = (int64_t)MR_ROW_SLOTS * (F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f);
+      // four of the lane's slots at a time: their tags together, then their rows together (an untagged
+      // slot loads row 0 — one line shared by the wave — and adds nothing): two dependent round trips
+      // per four slots instead of two per slot
 #pragma unroll 1
-      for (int sidx = j; sidx < ns; sidx += G) {
-        const uint8_t tg = rtag[b0 + sidx];
-        if (tg == 1) {
-          add_row(b0 + sidx);
-        } else if (tg == 2) {  // (slot 0 of a record whose rows are in the pool)
-          const int n = sidx / MR_ROW_SLOTS;
-          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
-          const int rb = rbase[rid];
-          const int sz = rect_size(rects[rid]);
+      for (int s0 = j; s0 < ns; s0 += 4 * G) {
+        uint8_t tg[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) tg[u] = s0 + u * G < ns ? rtag[b0 + s0 + u * G] : 0;
+        float4 x4[4][RS / 4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4* src = (const float4*)(rows + (tg[u] == 1 ? b0 + s0 + u * G : 0) * RS);
+#pragma unroll
+          for (int i = 0; i < RS / 4; ++i) x4[u][i] = src[i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (tg[u] == 1) {
+            const float* x = (const float*)x4[u];
+#pragma unroll
+            for (int i = 0; i < ACC; ++i) acc[i] += x[i];
+          } else if (tg[u] == 2) {  // (slot 0 of a record whose rows are in the pool)
+            const int n = (s0 + u * G) / MR_ROW_SLOTS;
+            const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
+            const int rb = rbase[rid];
+            const int sz = rect_size(rects[rid]);
 #pragma unroll 1
-          for (int k = 0; k < sz; ++k)
-            if (rtag[ovf0 + rb + k]) add_row(ovf0 + rb + k);
+            for (int k = 0; k < sz; ++k)
+              if (rtag[ovf0 + rb + k]) add_row(ovf0 + rb + k);
+          }
         }
       }
     }

@@ -132,23 +132,20 @@ __global__ void __launch_bounds__(256) k_pose_loss_bwd(PoseLossParams P, const f
 // The forward with the gradients (mr_pose_loss_forward_grad): the loss is linear in dL/dtotal, so
 // the gradients for dL/dtotal = 1 are written while the forward reads its inputs, and the backward only
 // rescales them when dL/dtotal != 1 (k_pose_loss_scale) — one pass over the ~53 B/pixel of inputs
-// instead of two. Same formulas (and operation order) as k_pose_loss_bwd with g = 1. Four pixels per
-// thread, 16-B loads and stores (npix % 4 == 0, 16-B aligned buffers; else the scalar kernels). The
-// masked-pixel count the Huber gradient divides by comes first (k_mask_count: per-block counts, summed
-// in a fixed order by every block of this kernel).
+// instead of two. Same formulas (and operation order) as k_pose_loss_bwd with g = 1, and its access
+// pattern: one pixel per lane, a wave's 64 lanes on 64 consecutive pixels (a 16-B strided RGBA channel
+// read is one 1-KB span per load instruction; four pixels per lane measured 339 us against 222 for this
+// pattern, their 64-B lane strides touching 4x the cache lines per instruction). The masked-pixel count
+// the Huber gradient divides by comes first (k_mask_count: per-block counts, summed in a fixed order by
+// every block of this kernel).
 __global__ void __launch_bounds__(256) k_mask_count(const uint8_t* __restrict__ mask, int64_t npix, int* __restrict__ pcnt) {
   __shared__ float sm[4];
   int cnt = 0;
-  const int64_t n4 = npix / 4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const uint32_t m = ((const uint32_t*)mask)[i];
-    cnt += ((m & 0xffu) != 0) + ((m & 0xff00u) != 0) + ((m & 0xff0000u) != 0) + ((m >> 24) != 0);
-  }
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npix; i += (int64_t)gridDim.x * 256) cnt += mask[i] != 0;
   const float n = block_sum_256((float)cnt, sm);  // exact: < 2^24 per block
   if (threadIdx.x == 0) pcnt[blockIdx.x] = (int)n;
 }
 
-MR_DEV float4 f4sub(float4 a, float4 b) { return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w); }
 MR_DEV float sgnf(float e) { return e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f); }
 
 __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const int* __restrict__ mcnt, int nmb,
@@ -156,8 +153,8 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
                                                          float* __restrict__ g_depth, float* __restrict__ g_sil,
                                                          float* __restrict__ g_rgb) {
   __shared__ float sm[4];
-  // the masked-pixel count (every block sums k_mask_count's partials in the same order)
   __shared__ long long smc[4];
+  // the masked-pixel count (every block sums k_mask_count's partials in the same order)
   long long tn = 0;
   for (int i = threadIdx.x; i < nmb; i += 256) tn += mcnt[i];
   for (int o = 32; o > 0; o >>= 1) tn += __shfl_xor(tn, o, 64);
@@ -167,67 +164,29 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
   const float cs = P.w_color * (2.0f / (float)(3 * P.npix));
   float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
   int cnt = 0;
-  const int64_t n4 = P.npix / 4;
-  for (int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
-    const uint32_t mw = ((const uint32_t*)P.mask)[q];
-    const float4 d4 = ((const float4*)P.depth)[q], dr4 = ((const float4*)P.depth_ref)[q];
-    float sv[4], c[4][3];
-    if (P.sil_stride == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) sv[k] = ((const float4*)(P.sil - 3))[4 * q + k].w;
-    } else {
-      const float4 s4 = ((const float4*)P.sil)[q];
-      sv[0] = s4.x; sv[1] = s4.y; sv[2] = s4.z; sv[3] = s4.w;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
+    const bool m = P.mask[i] != 0;
+    const float e = P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f);
+    s_l1 += fabsf(e);
+    const float gs = 1.0f * (sgnf(e) / (float)P.npix);
+    const float dd = P.depth[i] - P.depth_ref[i];
+    if (m) {
+      s_h += huber_val(dd, P.delta);
+      ++cnt;
     }
+    g_depth[i] = m ? 1.0f * (huber_grad(dd, P.delta) / tnf) : 0.0f;
+    if (P.sil_stride == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
+    else g_sil[i] = gs;
+    const float* c = P.rgb + i * P.rgb_stride;
+    const float* r = P.rgb_ref + 3 * i;
+    const float e0 = c[0] - r[0], e1 = c[1] - r[1], e2 = c[2] - r[2];
+    s_mse += (e0 * e0 + e1 * e1) + e2 * e2;
     if (P.rgb_stride == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 c4 = ((const float4*)P.rgb)[4 * q + k];
-        c[k][0] = c4.x; c[k][1] = c4.y; c[k][2] = c4.z;
-      }
+      ((float4*)g_rgb)[i] = make_float4(cs * e0, cs * e1, cs * e2, 0.0f);
     } else {
-      const float4 a = ((const float4*)P.rgb)[3 * q], b = ((const float4*)P.rgb)[3 * q + 1],
-                   e = ((const float4*)P.rgb)[3 * q + 2];
-      c[0][0] = a.x; c[0][1] = a.y; c[0][2] = a.z; c[1][0] = a.w; c[1][1] = b.x; c[1][2] = b.y;
-      c[2][0] = b.z; c[2][1] = b.w; c[2][2] = e.x; c[3][0] = e.y; c[3][1] = e.z; c[3][2] = e.w;
-    }
-    const float4 r0 = ((const float4*)P.rgb_ref)[3 * q], r1 = ((const float4*)P.rgb_ref)[3 * q + 1],
-                 r2 = ((const float4*)P.rgb_ref)[3 * q + 2];
-    const float rr[4][3] = {{r0.x, r0.y, r0.z}, {r0.w, r1.x, r1.y}, {r1.z, r1.w, r2.x}, {r2.y, r2.z, r2.w}};
-    const float dd[4] = {d4.x - dr4.x, d4.y - dr4.y, d4.z - dr4.z, d4.w - dr4.w};
-    float gd[4], gs[4], gc[4][3];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const bool m = ((mw >> (8 * k)) & 0xffu) != 0;
-      const float e = sv[k] - (m ? 1.0f : 0.0f);
-      s_l1 += fabsf(e);
-      gs[k] = 1.0f * (sgnf(e) / (float)P.npix);
-      if (m) {
-        s_h += huber_val(dd[k], P.delta);
-        ++cnt;
-      }
-      gd[k] = m ? 1.0f * (huber_grad(dd[k], P.delta) / tnf) : 0.0f;
-      const float e0 = c[k][0] - rr[k][0], e1 = c[k][1] - rr[k][1], e2 = c[k][2] - rr[k][2];
-      s_mse += (e0 * e0 + e1 * e1) + e2 * e2;
-      gc[k][0] = cs * e0;
-      gc[k][1] = cs * e1;
-      gc[k][2] = cs * e2;
-    }
-    ((float4*)g_depth)[q] = make_float4(gd[0], gd[1], gd[2], gd[3]);
-    if (P.sil_stride == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ((float4*)g_sil)[4 * q + k] = make_float4(0.0f, 0.0f, 0.0f, gs[k]);
-    } else {
-      ((float4*)g_sil)[q] = make_float4(gs[0], gs[1], gs[2], gs[3]);
-    }
-    if (P.rgb_stride == 4) {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ((float4*)g_rgb)[4 * q + k] = make_float4(gc[k][0], gc[k][1], gc[k][2], 0.0f);
-    } else {
-      float4* o = (float4*)g_rgb + 3 * q;
-      o[0] = make_float4(gc[0][0], gc[0][1], gc[0][2], gc[1][0]);
-      o[1] = make_float4(gc[1][1], gc[1][2], gc[2][0], gc[2][1]);
-      o[2] = make_float4(gc[2][2], gc[3][0], gc[3][1], gc[3][2]);
+      g_rgb[3 * i] = cs * e0;
+      g_rgb[3 * i + 1] = cs * e1;
+      g_rgb[3 * i + 2] = cs * e2;
     }
   }
   const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), c = block_sum_256(s_mse, sm);
@@ -242,21 +201,15 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
 
 // dL/dtotal != 1: the forward's gradients (written for dL/dtotal = 1) times dL/dtotal, in place (the
 // grid reads the device scalar and returns when it is 1 — the optimiser's loss.backward()).
-__global__ void __launch_bounds__(256) k_pose_loss_scale(const float* __restrict__ g_total, int64_t n4d, int64_t n4s,
-                                                         int64_t n4c, float4* __restrict__ gd, float4* __restrict__ gs,
-                                                         float4* __restrict__ gc) {
+__global__ void __launch_bounds__(256) k_pose_loss_scale(const float* __restrict__ g_total, int64_t nd, int64_t ns,
+                                                         int64_t nc, float* __restrict__ gd, float* __restrict__ gs,
+                                                         float* __restrict__ gc) {
   const float g = *g_total;
   if (g == 1.0f) return;
   const int64_t G = (int64_t)gridDim.x * 256;
-  auto sc = [&](float4* x, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += G) {
-      const float4 v = x[i];
-      x[i] = make_float4(g * v.x, g * v.y, g * v.z, g * v.w);
-    }
-  };
-  sc(gd, n4d);
-  sc(gs, n4s);
-  sc(gc, n4c);
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nd; i += G) gd[i] = g * gd[i];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < ns; i += G) gs[i] = g * gs[i];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nc; i += G) gc[i] = g * gc[i];
 }
 
 // upstream quaternion_to_matrix, one thread per quaternion (torch's elementwise operation order, no

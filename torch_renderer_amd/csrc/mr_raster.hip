@@ -773,11 +773,6 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   SetupParams SP = make_setup(s, g, w);
   SP.NF = NF;
   SP.vff = m->view_face_first;
-  if (rows_fit(w)) {  // the gradient rows' slot tags, cleared beside the records
-    SP.rtagw = (uint32_t*)w.rtag;
-    SP.rs_F = multi ? 0 : m->F;
-    SP.rs_N = (int)N;
-  }
   FwdParams P = make_fwd(s, g, w, N, m->view_face_first, multi ? 0 : m->F, NF);
   P.view_count = m->view_face_count;
   P.S = make_shade(m, sp, cc, ncc);
@@ -797,11 +792,16 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
   }
   if (vpath) {
     NormalsArgs NA;
+    memset(&NA, 0, sizeof(NA));
     NA.V = m->V; NA.ptr = m->vadj_ptr; NA.adj = m->vadj;
     NA.vn = vb ? m->vnormals_out : nullptr;
     NA.vraw = m->vraw_out;
     NA.zero4 = (float4*)w.grows;
     NA.nzero4 = (27 * m->F + 3) / 4;
+    if (rows_fit(w)) {  // the gradient rows' slot tags (second triangles' too when clipping), 256-B aligned
+      NA.ztag = (uint4*)w.rtag;
+      NA.nztag = (int64_t)MR_ROW_SLOTS * NF * (SP.clipz ? 2 : 1) / 16 + 1;
+    }
     const int64_t bx = std::max<int64_t>(ceil_div(maxvf, 256), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
     if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C, FragBg{})));
@@ -1326,23 +1326,15 @@ int32_t mr_pose_loss_forward_grad(const float* depth, const float* sil, int64_t 
   int64_t* count = (int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
   int* mcnt = (int*)((char*)count + 256);
   hipStream_t st = (hipStream_t)stream;
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  const bool vec = grads && npix % 4 == 0 && a16(depth) && a16(depth_ref) && ((uintptr_t)mask & 3) == 0 &&
-                   a16(sil_stride == 4 ? (const void*)(sil - 3) : (const void*)sil) && a16(rgb) && a16(rgb_ref) &&
-                   a16(g_depth) && a16(g_sil) && a16(g_rgb);
-  if (!vec) {  // the two-pass kernels (the loss alone without gradient buffers)
+  if (!grads) {  // the loss alone
     const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
     k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
     MR_CHECK_LAUNCH("k_pose_loss_partial");
     k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, total, terms, count);
     MR_CHECK_LAUNCH("k_pose_loss_final");
-    if (grads) {
-      k_pose_loss_bwd<<<(unsigned)ceil_div(npix, 256), 256, 0, st>>>(P, nullptr, count, g_depth, g_sil, g_rgb);
-      MR_CHECK_LAUNCH("k_pose_loss_bwd");
-    }
     return MR_OK;
   }
-  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix / 4, 256));
+  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
   k_mask_count<<<nb, 256, 0, st>>>(mask, npix, mcnt);
   MR_CHECK_LAUNCH("k_mask_count");
   k_pose_loss_fused<<<nb, 256, 0, st>>>(P, mcnt, nb, part, pcnt, g_depth, g_sil, g_rgb);
@@ -1358,12 +1350,8 @@ int32_t mr_pose_loss_scale(const float* g_total, int64_t npix, int64_t sil_strid
   if (!g_total || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL argument");
   if ((sil_stride != 1 && sil_stride != 4) || (rgb_stride != 3 && rgb_stride != 4))
     return set_err(MR_EINVAL, "bad strides");
-  auto a16 = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
-  if (npix % 4 || !a16(g_depth) || !a16(g_sil) || !a16(g_rgb))
-    return set_err(MR_EINVAL, "gradient buffers: npix % 4 == 0 and 16-byte alignment required");
-  const int64_t nd = npix / 4, ns = npix * sil_stride / 4, nc = npix * rgb_stride / 4;
-  k_pose_loss_scale<<<1024, 256, 0, (hipStream_t)stream>>>(g_total, nd, ns, nc, (float4*)g_depth, (float4*)g_sil,
-                                                            (float4*)g_rgb);
+  k_pose_loss_scale<<<1024, 256, 0, (hipStream_t)stream>>>(g_total, npix, npix * sil_stride, npix * rgb_stride, g_depth,
+                                                            g_sil, g_rgb);
   MR_CHECK_LAUNCH("k_pose_loss_scale");
   return MR_OK;
 }

@@ -140,7 +140,7 @@ struct RasterWS {
   // <= MR_ROW_SLOTS tiles; the rest (larger faces) take rows from an overflow pool allocated by k_bin_view.
   int* rbase;      // (2 * Ftot) overflow records: first pool row of their tile rectangle (-1: pool full)
   uint8_t* rtag;   // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) 1 = the backward wrote the row; a record's slot 0 holds
-                   // 2 when its rows are in the pool. Slot tags cleared by k_bin_rect_world, pool tags by k_bin_view
+                   // 2 when its rows are in the pool. Slot tags cleared by k_bin_rect_world (its normals row), pool tags by k_bin_view
   float* rrows;    // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) rows of MR_ROW_STRIDE(acc) floats
   int64_t ovf0;    // first pool row (= MR_ROW_SLOTS * 2 Ftot)
   int64_t ovf_cap; // pool rows

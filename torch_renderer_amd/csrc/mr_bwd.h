@@ -510,9 +510,8 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
 // sub-triangle's corners (run with C g_orig); map it to the ORIGINAL face's projected corners
 // through the clip's chain rule (sub-corners and the conversion weights), the original corners
 // re-projected from the world corners. g_orig: gradient w.r.t. the original-face barycentrics.
-__attribute__((noinline)) __device__ void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f,
-                                                         const ViewRec& V, const float X[3][3], float px, float py,
-                                                         const float g_orig[3], float gfv[3][3]) {
+MR_DEV void clipped_chain(const RenderBwdParams& P, const FaceRec& r, int f, const ViewRec& V, const float X[3][3],
+                          float px, float py, const float g_orig[3], float gfv[3][3]) {
   const ClipRec cr = P.crec[f];
   FragEval e;
   eval_face(r, px, py, P.bbox_pad, P.blur, P.persp, P.clipb, e);
@@ -750,12 +749,14 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of the rows the
 // backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
-// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block), read by
-// G lanes per face (G = the block's rows rounded up to a power of two, at most 64): lane j adds rows
-// j, j + G, ... of the block in that order (one tag byte, then the row when tagged: consecutive lanes
-// read consecutive tags and rows), a record whose slot 0 holds 2 walks its pool rows instead; the G partial sums are then
-// added by a fixed xor tree. Workgroups are dispatched round-robin over the 8 XCDs: block b takes faces
-// from XCD-contiguous ranges.
+// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) of
+// ns = N * MR_ROW_SLOTS rows whose tag bytes are contiguous: each of the face's G lanes takes SPL
+// consecutive slots (16, or all ns when fewer), reads their tags as 32-bit words in one round trip, then
+// adds its tagged rows in slot order, two row loads in flight (a slot tagged 2 — slot 0 of a record
+// whose rows are in the pool — walks the pool rows instead); the G partial sums are then added by a
+// fixed xor tree. (Per-slot tag loads cost a round trip per slot: 29 us per render step against this
+// layout's single tag round trip.) Workgroups are dispatched round-robin over the 8 XCDs: block b takes
+// faces from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
                                                      int64_t ovf0, const int* __restrict__ rbase,
@@ -774,51 +775,64 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
-  const int ns = nv * MR_ROW_SLOTS;  // rows of a face's block
-  auto add_row = [&](int64_t row) {
-    const float4* x4 = (const float4*)(rows + row * RS);
-    float x[RS];
-#pragma unroll
-    for (int i = 0; i < RS / 4; ++i) {
-      const float4 w = x4[i];
-      x[4 * i] = w.x; x[4 * i + 1] = w.y; x[4 * i + 2] = w.z; x[4 * i + 3] = w.w;
-    }
+  const int ns = nv * MR_ROW_SLOTS;  // rows of a face's block (a multiple of 4)
+  const int spl = ns < 16 ? ns : 16;  // slots per lane
+  auto add4 = [&](const float4 (&x4)[RS / 4]) {
+    const float* x = (const float*)x4;
 #pragma unroll
     for (int i = 0; i < ACC; ++i) acc[i] += x[i];
   };
+  auto load4 = [&](int64_t row, float4 (&x4)[RS / 4]) {
+    const float4* src = (const float4*)(rows + row * RS);
+#pragma unroll
+    for (int i = 0; i < RS / 4; ++i) x4[i] = src[i];
+  };
   if (f < F) {
     for (int q = 0; q <= clip; ++q) {
-      // first slot of the block: rec_slot of the face's record in view 0
+      // first slot of the block: rec_slot of the face's record in view 0 (4-B aligned: MR_ROW_SLOTS = 4)
       const int64_t b0 = (int64_t)MR_ROW_SLOTS * (F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f);
-      // four of the lane's slots at a time: their tags together, then their rows together (an untagged
-      // slot loads row 0 — one line shared by the wave — and adds nothing): two dependent round trips
-      // per four slots instead of two per slot
 #pragma unroll 1
-      for (int s0 = j; s0 < ns; s0 += 4 * G) {
-        uint8_t tg[4];
+      for (int s0 = j * spl; s0 < ns; s0 += G * spl) {
+        uint32_t tw[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) tg[u] = s0 + u * G < ns ? rtag[b0 + s0 + u * G] : 0;
-        float4 x4[4][RS / 4];
+        for (int u = 0; u < 4; ++u) tw[u] = 4 * u < spl && s0 + 4 * u < ns ? ((const uint32_t*)(rtag + b0 + s0))[u] : 0u;
+        uint32_t m1 = 0, m2 = 0;  // bit i: slot s0 + i tagged 1 / 2
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4* src = (const float4*)(rows + (tg[u] == 1 ? b0 + s0 + u * G : 0) * RS);
-#pragma unroll
-          for (int i = 0; i < RS / 4; ++i) x4[u][i] = src[i];
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t t = (tw[i >> 2] >> (8 * (i & 3))) & 255u;
+          m1 |= (t == 1u ? 1u : 0u) << i;
+          m2 |= (t == 2u ? 1u : 0u) << i;
         }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (tg[u] == 1) {
-            const float* x = (const float*)x4[u];
-#pragma unroll
-            for (int i = 0; i < ACC; ++i) acc[i] += x[i];
-          } else if (tg[u] == 2) {  // (slot 0 of a record whose rows are in the pool)
-            const int n = (s0 + u * G) / MR_ROW_SLOTS;
+#pragma unroll 1
+        while (m1 | m2) {
+          const int i = __builtin_ctz(m1 | m2);
+          if ((m2 >> i) & 1u) {
+            m2 &= m2 - 1u;
+            const int n = (s0 + i) / MR_ROW_SLOTS;
             const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
             const int rb = rbase[rid];
             const int sz = rect_size(rects[rid]);
 #pragma unroll 1
             for (int k = 0; k < sz; ++k)
-              if (rtag[ovf0 + rb + k]) add_row(ovf0 + rb + k);
+              if (rtag[ovf0 + rb + k]) {
+                float4 x4[RS / 4];
+                load4(ovf0 + rb + k, x4);
+                add4(x4);
+              }
+            continue;
+          }
+          m1 &= m1 - 1u;
+          // slot i and, when the next tagged slot is also a fixed row, that one too: two loads in flight
+          const uint32_t rest = m1 | m2;
+          const int i2 = rest ? __builtin_ctz(rest) : -1;
+          const bool two = i2 >= 0 && ((m1 >> i2) & 1u);
+          float4 xa[RS / 4], xb[RS / 4];
+          load4(b0 + s0 + i, xa);
+          load4(b0 + s0 + (two ? i2 : i), xb);
+          add4(xa);
+          if (two) {
+            m1 &= m1 - 1u;
+            add4(xb);
           }
         }
       }

@@ -133,9 +133,10 @@ __global__ void __launch_bounds__(256) k_pose_loss_bwd(PoseLossParams P, const f
 // the gradients for dL/dtotal = 1 are written while the forward reads its inputs, and the backward only
 // rescales them when dL/dtotal != 1 (k_pose_loss_scale) — one pass over the ~53 B/pixel of inputs
 // instead of two. Same formulas (and operation order) as k_pose_loss_bwd with g = 1, and its access
-// pattern: one pixel per lane, a wave's 64 lanes on 64 consecutive pixels (a 16-B strided RGBA channel
-// read is one 1-KB span per load instruction; four pixels per lane measured 339 us against 222 for this
-// pattern, their 64-B lane strides touching 4x the cache lines per instruction). The masked-pixel count
+// pattern: a wave's 64 lanes on 64 consecutive pixels (a 16-B strided RGBA channel read is one 1-KB span
+// per load instruction; four adjacent pixels per lane measured 339 us, their 64-B lane strides touching
+// 4x the cache lines per instruction), four such pixels per thread with all their loads issued first.
+// The masked-pixel count
 // the Huber gradient divides by comes first (k_mask_count: per-block counts, summed in a fixed order by
 // every block of this kernel).
 __global__ void __launch_bounds__(256) k_mask_count(const uint8_t* __restrict__ mask, int64_t npix, int* __restrict__ pcnt) {
@@ -154,6 +155,15 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
                                                          float* __restrict__ g_rgb) {
   __shared__ float sm[4];
   __shared__ long long smc[4];
+  // restrict-qualified copies: the gradient stores cannot alias the inputs, so the loads of the next
+  // pixels are not held behind the stores of the previous ones
+  const float* __restrict__ depth = P.depth;
+  const float* __restrict__ dref = P.depth_ref;
+  const float* __restrict__ sil = P.sil;
+  const float* __restrict__ rgb = P.rgb;
+  const float* __restrict__ rref = P.rgb_ref;
+  const uint8_t* __restrict__ mask = P.mask;
+  const int64_t ss = P.sil_stride, rs = P.rgb_stride, npix = P.npix;
   // the masked-pixel count (every block sums k_mask_count's partials in the same order)
   long long tn = 0;
   for (int i = threadIdx.x; i < nmb; i += 256) tn += mcnt[i];
@@ -161,40 +171,62 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
   if ((threadIdx.x & 63) == 0) smc[threadIdx.x >> 6] = tn;
   __syncthreads();
   const float tnf = (float)(((smc[0] + smc[1]) + smc[2]) + smc[3]);  // as k_pose_loss_bwd's (float)count
-  const float cs = P.w_color * (2.0f / (float)(3 * P.npix));
+  const float cs = P.w_color * (2.0f / (float)(3 * npix));
   float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
   int cnt = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
-    const bool m = P.mask[i] != 0;
-    const float e = P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f);
-    s_l1 += fabsf(e);
-    const float gs = 1.0f * (sgnf(e) / (float)P.npix);
-    const float dd = P.depth[i] - P.depth_ref[i];
-    if (m) {
-      s_h += huber_val(dd, P.delta);
-      ++cnt;
+  constexpr int U = 4;  // pixels per thread per iteration, G apart (each load instruction lane-contiguous)
+  const int64_t G = (int64_t)gridDim.x * 256;
+#pragma unroll 1
+  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < npix; i0 += U * G) {
+    bool m[U], ok[U];
+    float sv[U], d[U], dr[U], c[U][3], r[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // every load of the U pixels first
+      const int64_t i = i0 + u * G;
+      ok[u] = i < npix;
+      const int64_t k = ok[u] ? i : 0;
+      m[u] = mask[k] != 0;
+      sv[u] = sil[k * ss];
+      d[u] = depth[k];
+      dr[u] = dref[k];
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        c[u][ch] = rgb[k * rs + ch];
+        r[u][ch] = rref[3 * k + ch];
+      }
     }
-    g_depth[i] = m ? 1.0f * (huber_grad(dd, P.delta) / tnf) : 0.0f;
-    if (P.sil_stride == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
-    else g_sil[i] = gs;
-    const float* c = P.rgb + i * P.rgb_stride;
-    const float* r = P.rgb_ref + 3 * i;
-    const float e0 = c[0] - r[0], e1 = c[1] - r[1], e2 = c[2] - r[2];
-    s_mse += (e0 * e0 + e1 * e1) + e2 * e2;
-    if (P.rgb_stride == 4) {
-      ((float4*)g_rgb)[i] = make_float4(cs * e0, cs * e1, cs * e2, 0.0f);
-    } else {
-      g_rgb[3 * i] = cs * e0;
-      g_rgb[3 * i + 1] = cs * e1;
-      g_rgb[3 * i + 2] = cs * e2;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      const int64_t i = i0 + u * G;
+      const float e = sv[u] - (m[u] ? 1.0f : 0.0f);
+      s_l1 += fabsf(e);
+      const float gs = 1.0f * (sgnf(e) / (float)npix);
+      const float dd = d[u] - dr[u];
+      if (m[u]) {
+        s_h += huber_val(dd, P.delta);
+        ++cnt;
+      }
+      g_depth[i] = m[u] ? 1.0f * (huber_grad(dd, P.delta) / tnf) : 0.0f;
+      if (ss == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
+      else g_sil[i] = gs;
+      const float e0 = c[u][0] - r[u][0], e1 = c[u][1] - r[u][1], e2 = c[u][2] - r[u][2];
+      s_mse += (e0 * e0 + e1 * e1) + e2 * e2;
+      if (rs == 4) {
+        ((float4*)g_rgb)[i] = make_float4(cs * e0, cs * e1, cs * e2, 0.0f);
+      } else {
+        g_rgb[3 * i] = cs * e0;
+        g_rgb[3 * i + 1] = cs * e1;
+        g_rgb[3 * i + 2] = cs * e2;
+      }
     }
   }
-  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), c = block_sum_256(s_mse, sm);
+  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), cc = block_sum_256(s_mse, sm);
   const float n = block_sum_256((float)cnt, sm);
   if (threadIdx.x == 0) {
     part[3 * blockIdx.x] = a;
     part[3 * blockIdx.x + 1] = b;
-    part[3 * blockIdx.x + 2] = c;
+    part[3 * blockIdx.x + 2] = cc;
     pcnt[blockIdx.x] = (int)n;
   }
 }

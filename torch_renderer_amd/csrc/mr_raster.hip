@@ -1032,8 +1032,8 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   {
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: the rows of a face's slot block, rounded up to a power of two (<= 64)
-    while (G < 64 && G < (multi ? 1 : (int)N) * MR_ROW_SLOTS) G <<= 1;
+    int G = 1;  // lanes per face: 16 slots each (k_face_reduce), rounded up to a power of two (<= 64)
+    while (G < 64 && G * 16 < (multi ? 1 : (int)N) * MR_ROW_SLOTS) G <<= 1;
     int nb = ceil_div(m->F, 256 / G);
     nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {

@@ -940,7 +940,11 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // band tile lt lives at hist[lt + lt / 64] (the scan's per-thread runs of C tiles spread over the
   // banks); a view's rectangles are read in chunks of MR_VIEW_RPT per thread, all loads of a
   // chunk in flight together, and a view of one chunk keeps them in registers for the fill.
+#ifdef MR_VIEW_PERM  // experiment: a wave's lanes on faces 16 apart (mesh-order neighbours hit the same tiles)
+  const int j = (t & 63) * 16 + (t >> 6);
+#else
   const int j = t;
+#endif
   const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   for (int i = t; i < Tb + (Tb >> 6); i += 1024) hist[i] = 0;

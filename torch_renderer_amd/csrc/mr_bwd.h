@@ -749,20 +749,20 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of the rows the
 // backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
-// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) of
-// ns = N * MR_ROW_SLOTS rows whose tag bytes are contiguous: each of the face's G lanes takes SPL
-// consecutive slots (16, or all ns when fewer), reads their tags as 32-bit words in one round trip, then
-// adds its tagged rows in slot order, two row loads in flight (a slot tagged 2 — slot 0 of a record
-// whose rows are in the pool — walks the pool rows instead); the G partial sums are then added by a
-// fixed xor tree. (Per-slot tag loads cost a round trip per slot: 29 us per render step against this
-// layout's single tag round trip.) Workgroups are dispatched round-robin over the 8 XCDs: block b takes
-// faces from XCD-contiguous ranges.
+// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) whose tag
+// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 64), lane j
+// taking views j, j + G, ...: per view one 32-bit load of the record's four tags, then its tagged rows,
+// two loads in flight (a record whose slot 0 holds 2 walks its pool rows instead); the G partial sums
+// are then added by a fixed xor tree. Two dependent round trips per (face, view) — per-slot tag loads
+// spread over four rounds measured 29 us per render step, 16-slot lanes walking their rows one by one 41.
+// Workgroups are dispatched round-robin over the 8 XCDs: block b takes faces from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
                                                      int64_t ovf0, const int* __restrict__ rbase,
                                                      const uint32_t* __restrict__ rects, const uint8_t* __restrict__ rtag,
                                                      const float* __restrict__ rows, const float* __restrict__ gatom,
                                                      float* __restrict__ gout) {
+  static_assert(MR_ROW_SLOTS == 4, "one 32-bit tag word per record");
   constexpr int RS = MR_ROW_STRIDE(ACC);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int fpb = 256 / G;  // faces per workgroup
@@ -775,8 +775,6 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
-  const int ns = nv * MR_ROW_SLOTS;  // rows of a face's block (a multiple of 4)
-  const int spl = ns < 16 ? ns : 16;  // slots per lane
   auto add4 = [&](const float4 (&x4)[RS / 4]) {
     const float* x = (const float*)x4;
 #pragma unroll
@@ -789,49 +787,40 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
   };
   if (f < F) {
     for (int q = 0; q <= clip; ++q) {
-      // first slot of the block: rec_slot of the face's record in view 0 (4-B aligned: MR_ROW_SLOTS = 4)
-      const int64_t b0 = (int64_t)MR_ROW_SLOTS * (F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f);
+      // the face's record in view 0: its rec_slot (the views' records follow)
+      const int64_t r0 = F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f;
 #pragma unroll 1
-      for (int s0 = j * spl; s0 < ns; s0 += G * spl) {
-        uint32_t tw[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) tw[u] = 4 * u < spl && s0 + 4 * u < ns ? ((const uint32_t*)(rtag + b0 + s0))[u] : 0u;
-        uint32_t m1 = 0, m2 = 0;  // bit i: slot s0 + i tagged 1 / 2
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t t = (tw[i >> 2] >> (8 * (i & 3))) & 255u;
-          m1 |= (t == 1u ? 1u : 0u) << i;
-          m2 |= (t == 2u ? 1u : 0u) << i;
+      for (int n = j; n < nv; n += G) {
+        const uint32_t tw = ((const uint32_t*)rtag)[r0 + n];
+        if (tw == 0u) continue;
+        if ((tw & 255u) == 2u) {  // the record's rows are in the pool
+          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
+          const int rb = rbase[rid];
+          const int sz = rect_size(rects[rid]);
+#pragma unroll 1
+          for (int k = 0; k < sz; ++k)
+            if (rtag[ovf0 + rb + k]) {
+              float4 x4[RS / 4];
+              load4(ovf0 + rb + k, x4);
+              add4(x4);
+            }
+          continue;
         }
+        uint32_t m = 0;  // bit k: tile k's row tagged
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m |= (((tw >> (8 * k)) & 255u) == 1u ? 1u : 0u) << k;
+        const int64_t row0 = (r0 + n) * MR_ROW_SLOTS;
 #pragma unroll 1
-        while (m1 | m2) {
-          const int i = __builtin_ctz(m1 | m2);
-          if ((m2 >> i) & 1u) {
-            m2 &= m2 - 1u;
-            const int n = (s0 + i) / MR_ROW_SLOTS;
-            const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
-            const int rb = rbase[rid];
-            const int sz = rect_size(rects[rid]);
-#pragma unroll 1
-            for (int k = 0; k < sz; ++k)
-              if (rtag[ovf0 + rb + k]) {
-                float4 x4[RS / 4];
-                load4(ovf0 + rb + k, x4);
-                add4(x4);
-              }
-            continue;
-          }
-          m1 &= m1 - 1u;
-          // slot i and, when the next tagged slot is also a fixed row, that one too: two loads in flight
-          const uint32_t rest = m1 | m2;
-          const int i2 = rest ? __builtin_ctz(rest) : -1;
-          const bool two = i2 >= 0 && ((m1 >> i2) & 1u);
+        while (m) {
+          const int k1 = __builtin_ctz(m);
+          m &= m - 1u;
+          const int k2 = m ? __builtin_ctz(m) : k1;
           float4 xa[RS / 4], xb[RS / 4];
-          load4(b0 + s0 + i, xa);
-          load4(b0 + s0 + (two ? i2 : i), xb);
+          load4(row0 + k1, xa);
+          load4(row0 + k2, xb);
           add4(xa);
-          if (two) {
-            m1 &= m1 - 1u;
+          if (m) {
+            m &= m - 1u;
             add4(xb);
           }
         }
@@ -861,22 +850,46 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
   // the view's slots in tile order: its bands' ranges concatenated (band b holds tile rows above band b+1's).
-  // Thread t sums the slots t, t + 256, ... of that sequence, whatever the band split — the result does not
-  // depend on how many bands (i.e. on the batch size: a view's gradient is bitwise the same in any batch)
-  int b = 0, bs0 = vslot[n * bands], bn = vslot[N * bands + n * bands], before = 0;
-  for (int t = threadIdx.x;; t += 256) {
-    while (t - before >= bn && b + 1 < bands) {  // advance to the band holding sequence position t
-      before += bn;
-      ++b;
-      bs0 = vslot[n * bands + b];
-      bn = vslot[N * bands + n * bands + b];
+  // Thread t sums the slots t, t + 256, ... of that sequence in that order, whatever the band split — the
+  // result does not depend on how many bands (i.e. on the batch size: a view's gradient is bitwise the same
+  // in any batch). Four positions' rows are loaded together (a single-view batch has thousands of slots:
+  // one dependent load per 256 slots made k_rt_reduce 24 us at C5), then added in sequence order.
+  __shared__ int bfirst[MR_BANDS_MAX], bpre[MR_BANDS_MAX + 1];
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int b = 0; b < bands; ++b) {
+      bfirst[b] = vslot[n * bands + b];
+      bpre[b] = tot;
+      tot += vslot[N * bands + n * bands + b];
     }
-    if (t - before >= bn) break;
-    const float4* q = (const float4*)(part + ((int64_t)bs0 + (t - before)) * 12);
-    const float4 a = q[0], c4 = q[1], c = q[2];
-    acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
-    acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
-    acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+    bpre[bands] = tot;
+  }
+  __syncthreads();
+  const int total = bpre[bands];
+  auto slot_at = [&](int p) {  // sequence position -> slot
+    int b = 0;
+    while (b + 1 < bands && bpre[b + 1] <= p) ++b;
+    return bfirst[b] + (p - bpre[b]);
+  };
+#pragma unroll 1
+  for (int p0 = threadIdx.x; p0 < total; p0 += 4 * 256) {
+    float4 r[4][3];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int p = p0 + u * 256;
+      const float4* q = (const float4*)(part + (int64_t)slot_at(p < total ? p : p0) * 12);
+      r[u][0] = q[0];
+      r[u][1] = q[1];
+      r[u][2] = q[2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (p0 + u * 256 >= total) break;
+      const float4 a = r[u][0], c4 = r[u][1], c = r[u][2];
+      acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
+      acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
+      acc[8] += c.x; acc[9] += c.y; acc[10] += c.z; acc[11] += c.w;
+    }
   }
 #pragma unroll
   for (int i = 0; i < 12; ++i) {

@@ -9,7 +9,7 @@
 //   color_loss = MSELoss()(color, rgb_ref)                mean over all pixels x 3
 //   total      = sil_loss + hloss + w_color * color_loss
 // Forward: per-block partial sums (fixed-order wave / block reductions), then one block sums the
-// partials in block order (deterministic). Backward: the elementwise gradients of the three
+// partials in a fixed order (deterministic). Backward: the elementwise gradients of the three
 // means, scaled by the device scalar dL/dtotal (no host read).
 // ---------------------------------------------------------------------------
 struct PoseLossParams {
@@ -42,59 +42,63 @@ MR_DEV float block_sum_256(float v, float* sm) {
   return t;
 }
 
-__global__ void __launch_bounds__(256) k_pose_loss_partial(PoseLossParams P, float* __restrict__ part,
-                                                           int* __restrict__ pcnt) {
-  __shared__ float sm[4];
-  float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
-  int cnt = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P.npix; i += (int64_t)gridDim.x * 256) {
-    const bool m = P.mask[i] != 0;
-    s_l1 += fabsf(P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f));
-    if (m) {
-      s_h += huber_val(P.depth[i] - P.depth_ref[i], P.delta);
-      ++cnt;
-    }
-    const float* c = P.rgb + i * P.rgb_stride;
-    const float* r = P.rgb_ref + 3 * i;
-    const float d0 = c[0] - r[0], d1 = c[1] - r[1], d2 = c[2] - r[2];
-    s_mse += (d0 * d0 + d1 * d1) + d2 * d2;
-  }
-  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), c = block_sum_256(s_mse, sm);
-  const float n = block_sum_256((float)cnt, sm);  // exact: <= 2^24 pixels per block
-  if (threadIdx.x == 0) {
-    part[3 * blockIdx.x] = a;
-    part[3 * blockIdx.x + 1] = b;
-    part[3 * blockIdx.x + 2] = c;
-    pcnt[blockIdx.x] = (int)n;
-  }
-}
-
-// out: {total, sil_loss, hloss, color_loss}; count: the number of masked pixels (backward)
-// out[0] = total; terms[0..2] = the three terms (out + 1 for the 4-float output of mr_pose_loss_forward)
-__global__ void __launch_bounds__(256) k_pose_loss_final(PoseLossParams P, const float* __restrict__ part,
-                                                         const int* __restrict__ pcnt, int nb, float* __restrict__ out,
-                                                         float* __restrict__ terms, int64_t* __restrict__ count) {
-  __shared__ float sm[4];
+// out[0] = total; terms[0..2] = the three terms (out + 1 for the 4-float output of mr_pose_loss_forward);
+// count = the masked pixels (the backward's Huber divisor). 1024 threads, each summing the block partials
+// i, i + 1024, ... in order with four partials' loads in flight, then a fixed tree: deterministic.
+__global__ void __launch_bounds__(1024) k_pose_loss_final(PoseLossParams P, const float* __restrict__ part,
+                                                          const int* __restrict__ pcnt, int nb, float* __restrict__ out,
+                                                          float* __restrict__ terms, int64_t* __restrict__ count) {
+  __shared__ float sm[3][16];
+  __shared__ long long sn[16];
   float a = 0.0f, b = 0.0f, c = 0.0f;
   long long n = 0;
-  for (int i = threadIdx.x; i < nb; i += 256) {
-    a += part[3 * i];
-    b += part[3 * i + 1];
-    c += part[3 * i + 2];
-    n += pcnt[i];
+#pragma unroll 1
+  for (int i0 = threadIdx.x; i0 < nb; i0 += 4 * 1024) {
+    float pa[4], pb[4], pc[4];
+    int pn[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * 1024 < nb ? i0 + u * 1024 : i0;
+      pa[u] = part[3 * i];
+      pb[u] = part[3 * i + 1];
+      pc[u] = part[3 * i + 2];
+      pn[u] = pcnt[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * 1024 < nb) {
+        a += pa[u];
+        b += pb[u];
+        c += pc[u];
+        n += pn[u];
+      }
   }
-  a = block_sum_256(a, sm);
-  b = block_sum_256(b, sm);
-  c = block_sum_256(c, sm);
-  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
-  __shared__ long long sn[4];
-  if ((threadIdx.x & 63) == 0) sn[threadIdx.x >> 6] = n;
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
+    c += __shfl_xor(c, o, 64);
+    n += __shfl_xor(n, o, 64);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[0][w] = a;
+    sm[1][w] = b;
+    sm[2][w] = c;
+    sn[w] = n;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const long long tn = ((sn[0] + sn[1]) + sn[2]) + sn[3];
-    const float l1 = a / (float)P.npix;
-    const float hl = b / (float)tn;  // an empty mask gives NaN, as torch's mean of nothing
-    const float ms = c / (float)(3 * P.npix);
+    float ta = 0.0f, tb = 0.0f, tc = 0.0f;
+    long long tn = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) {
+      ta += sm[0][k];
+      tb += sm[1][k];
+      tc += sm[2][k];
+      tn += sn[k];
+    }
+    const float l1 = ta / (float)P.npix;
+    const float hl = tb / (float)tn;  // an empty mask gives NaN, as torch's mean of nothing
+    const float ms = tc / (float)(3 * P.npix);
     out[0] = (l1 + hl) + P.w_color * ms;
     terms[0] = l1;
     terms[1] = hl;
@@ -146,73 +150,52 @@ __global__ void __launch_bounds__(256) k_mask_count(const uint8_t* __restrict__ 
   const float n = block_sum_256((float)cnt, sm);  // exact: < 2^24 per block
   if (threadIdx.x == 0) pcnt[blockIdx.x] = (int)n;
 }
+// the masked-pixel total of k_mask_count's nb partials, in a fixed order (one 256-thread block)
+__global__ void __launch_bounds__(256) k_mask_total(const int* __restrict__ pcnt, int nb, int64_t* __restrict__ tot) {
+  __shared__ long long sn[4];
+  long long n = 0;
+  for (int i = threadIdx.x; i < nb; i += 256) n += pcnt[i];
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o, 64);
+  if ((threadIdx.x & 63) == 0) sn[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) *tot = ((sn[0] + sn[1]) + sn[2]) + sn[3];
+}
 
 MR_DEV float sgnf(float e) { return e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f); }
 
-__global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const int* __restrict__ mcnt, int nmb,
+// One pixel per thread, one launch over the image (GRAD: also the gradients for dL/dtotal = 1); per-block
+// partial sums for k_pose_loss_final. (A grid-stride version over 2048 workgroups took 323-384 us for the
+// 16.7M-pixel C3 batch against this shape's ~220: its loop issues each iteration's loads only after the
+// previous iteration's stores.)
+template <bool GRAD>
+__global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const int64_t* __restrict__ mtot,
                                                          float* __restrict__ part, int* __restrict__ pcnt,
                                                          float* __restrict__ g_depth, float* __restrict__ g_sil,
                                                          float* __restrict__ g_rgb) {
   __shared__ float sm[4];
-  __shared__ long long smc[4];
-  // restrict-qualified copies: the gradient stores cannot alias the inputs, so the loads of the next
-  // pixels are not held behind the stores of the previous ones
-  const float* __restrict__ depth = P.depth;
-  const float* __restrict__ dref = P.depth_ref;
-  const float* __restrict__ sil = P.sil;
-  const float* __restrict__ rgb = P.rgb;
-  const float* __restrict__ rref = P.rgb_ref;
-  const uint8_t* __restrict__ mask = P.mask;
-  const int64_t ss = P.sil_stride, rs = P.rgb_stride, npix = P.npix;
-  // the masked-pixel count (every block sums k_mask_count's partials in the same order)
-  long long tn = 0;
-  for (int i = threadIdx.x; i < nmb; i += 256) tn += mcnt[i];
-  for (int o = 32; o > 0; o >>= 1) tn += __shfl_xor(tn, o, 64);
-  if ((threadIdx.x & 63) == 0) smc[threadIdx.x >> 6] = tn;
-  __syncthreads();
-  const float tnf = (float)(((smc[0] + smc[1]) + smc[2]) + smc[3]);  // as k_pose_loss_bwd's (float)count
-  const float cs = P.w_color * (2.0f / (float)(3 * npix));
-  float s_l1 = 0.0f, s_h = 0.0f, s_mse = 0.0f;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float l1 = 0.0f, h = 0.0f, mse = 0.0f;
   int cnt = 0;
-  constexpr int U = 4;  // pixels per thread per iteration, G apart (each load instruction lane-contiguous)
-  const int64_t G = (int64_t)gridDim.x * 256;
-#pragma unroll 1
-  for (int64_t i0 = (int64_t)blockIdx.x * 256 + threadIdx.x; i0 < npix; i0 += U * G) {
-    bool m[U], ok[U];
-    float sv[U], d[U], dr[U], c[U][3], r[U][3];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {  // every load of the U pixels first
-      const int64_t i = i0 + u * G;
-      ok[u] = i < npix;
-      const int64_t k = ok[u] ? i : 0;
-      m[u] = mask[k] != 0;
-      sv[u] = sil[k * ss];
-      d[u] = depth[k];
-      dr[u] = dref[k];
-#pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        c[u][ch] = rgb[k * rs + ch];
-        r[u][ch] = rref[3 * k + ch];
-      }
+  if (i < P.npix) {
+    const bool m = P.mask[i] != 0;
+    const float e = P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f);
+    l1 = fabsf(e);
+    const float dd = P.depth[i] - P.depth_ref[i];
+    if (m) {
+      h = huber_val(dd, P.delta);
+      cnt = 1;
     }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (!ok[u]) continue;
-      const int64_t i = i0 + u * G;
-      const float e = sv[u] - (m[u] ? 1.0f : 0.0f);
-      s_l1 += fabsf(e);
-      const float gs = 1.0f * (sgnf(e) / (float)npix);
-      const float dd = d[u] - dr[u];
-      if (m[u]) {
-        s_h += huber_val(dd, P.delta);
-        ++cnt;
-      }
-      g_depth[i] = m[u] ? 1.0f * (huber_grad(dd, P.delta) / tnf) : 0.0f;
-      if (ss == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
+    const float* c = P.rgb + i * P.rgb_stride;
+    const float* r = P.rgb_ref + 3 * i;
+    const float e0 = c[0] - r[0], e1 = c[1] - r[1], e2 = c[2] - r[2];
+    mse = (e0 * e0 + e1 * e1) + e2 * e2;
+    if (GRAD) {
+      const float gs = 1.0f * (sgnf(e) / (float)P.npix);
+      if (P.sil_stride == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
       else g_sil[i] = gs;
-      const float e0 = c[u][0] - r[u][0], e1 = c[u][1] - r[u][1], e2 = c[u][2] - r[u][2];
-      s_mse += (e0 * e0 + e1 * e1) + e2 * e2;
-      if (rs == 4) {
+      g_depth[i] = m ? 1.0f * (huber_grad(dd, P.delta) / (float)*mtot) : 0.0f;
+      const float cs = P.w_color * (2.0f / (float)(3 * P.npix));
+      if (P.rgb_stride == 4) {
         ((float4*)g_rgb)[i] = make_float4(cs * e0, cs * e1, cs * e2, 0.0f);
       } else {
         g_rgb[3 * i] = cs * e0;
@@ -221,7 +204,7 @@ __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const
       }
     }
   }
-  const float a = block_sum_256(s_l1, sm), b = block_sum_256(s_h, sm), cc = block_sum_256(s_mse, sm);
+  const float a = block_sum_256(l1, sm), b = block_sum_256(h, sm), cc = block_sum_256(mse, sm);
   const float n = block_sum_256((float)cnt, sm);
   if (threadIdx.x == 0) {
     part[3 * blockIdx.x] = a;

@@ -1032,8 +1032,8 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   {
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: 16 slots each (k_face_reduce), rounded up to a power of two (<= 64)
-    while (G < 64 && G * 16 < (multi ? 1 : (int)N) * MR_ROW_SLOTS) G <<= 1;
+    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 64)
+    while (G < 64 && G < (multi ? 1 : (int)N)) G <<= 1;
     int nb = ceil_div(m->F, 256 / G);
     nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {
@@ -1277,10 +1277,58 @@ static int pose_loss_params(PoseLossParams& P, const float* depth, const float* 
   return MR_OK;
 }
 
-size_t mr_pose_loss_workspace(int64_t npix) {
-  (void)npix;
-  return align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256) + 256 +
-         align_up(sizeof(int) * MR_LOSS_BLOCKS, 256);
+// Loss workspace: per-block partials of the one-pixel-per-thread pass (3 floats + a count per 256
+// pixels), the masked-pixel total, k_mask_count's partials and the backward's count.
+struct LossWS {
+  float* part;
+  int* pcnt;
+  int64_t* count;
+  int64_t* mtot;
+  int* mcnt;
+  size_t bytes;
+};
+static LossWS carve_loss(void* ws, int64_t npix) {
+  const size_t nb = (size_t)std::max<int64_t>(ceil_div(npix, 256), 1);
+  LossWS w;
+  char* b = (char*)ws;
+  size_t off = 0;
+  w.part = (float*)(b + off);
+  off = align_up(off + sizeof(float) * 3 * nb, 256);
+  w.pcnt = (int*)(b + off);
+  off = align_up(off + sizeof(int) * nb, 256);
+  w.count = (int64_t*)(b + off);
+  w.mtot = w.count + 1;
+  off = align_up(off + 2 * sizeof(int64_t), 256);
+  w.mcnt = (int*)(b + off);
+  off = align_up(off + sizeof(int) * MR_LOSS_BLOCKS, 256);
+  w.bytes = off;
+  return w;
+}
+
+size_t mr_pose_loss_workspace(int64_t npix) { return carve_loss(nullptr, npix).bytes; }
+
+// The loss (and, with gradient buffers, its gradients for dL/dtotal = 1): mask count, one pass over the
+// pixels, final reduction.
+static int32_t pose_loss_run(const PoseLossParams& P, float* total, float* terms, void* ws, float* g_depth,
+                             float* g_sil, float* g_rgb, hipStream_t st) {
+  LossWS w = carve_loss(ws, P.npix);
+  const int64_t nb = ceil_div(P.npix, 256);
+  if (nb >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "npix too large");
+  const bool grads = g_depth != nullptr;
+  if (grads) {
+    const int nm = (int)std::min<int64_t>(MR_LOSS_BLOCKS, nb);
+    k_mask_count<<<nm, 256, 0, st>>>(P.mask, P.npix, w.mcnt);
+    MR_CHECK_LAUNCH("k_mask_count");
+    k_mask_total<<<1, 256, 0, st>>>(w.mcnt, nm, w.mtot);
+    MR_CHECK_LAUNCH("k_mask_total");
+    k_pose_loss_fused<true><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, g_depth, g_sil, g_rgb);
+  } else {
+    k_pose_loss_fused<false><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, nullptr, nullptr, nullptr);
+  }
+  MR_CHECK_LAUNCH("k_pose_loss_fused");
+  k_pose_loss_final<<<1, 1024, 0, st>>>(P, w.part, w.pcnt, (int)nb, total, terms, w.count);
+  MR_CHECK_LAUNCH("k_pose_loss_final");
+  return MR_OK;
 }
 
 int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_stride, const float* rgb,
@@ -1292,17 +1340,7 @@ int32_t mr_pose_loss_forward(const float* depth, const float* sil, int64_t sil_s
   if (rc) return rc;
   if (!out || !ws) return set_err(MR_EINVAL, "NULL output / workspace");
   if (ws_bytes < mr_pose_loss_workspace(npix)) return set_err(MR_EWORKSPACE, "loss workspace too small");
-  char* w = (char*)ws;
-  float* part = (float*)w;
-  int* pcnt = (int*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256));
-  int64_t* count = (int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
-  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
-  hipStream_t st = (hipStream_t)stream;
-  k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
-  MR_CHECK_LAUNCH("k_pose_loss_partial");
-  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, out, out + 1, count);
-  MR_CHECK_LAUNCH("k_pose_loss_final");
-  return MR_OK;
+  return pose_loss_run(P, out, out + 1, ws, nullptr, nullptr, nullptr, (hipStream_t)stream);
 }
 
 // The forward writing the gradients for dL/dtotal = 1 too (see k_pose_loss_fused); mr_pose_loss_scale
@@ -1318,30 +1356,9 @@ int32_t mr_pose_loss_forward_grad(const float* depth, const float* sil, int64_t 
   const bool grads = g_depth || g_sil || g_rgb;
   if (grads && !(g_depth && g_sil && g_rgb)) return set_err(MR_EINVAL, "gradient buffers: all three or none");
   if (ws_bytes < mr_pose_loss_workspace(npix)) return set_err(MR_EWORKSPACE, "loss workspace too small");
-  if ((sil_stride == 4 && ((uintptr_t)g_sil & 15)) || (rgb_stride == 4 && ((uintptr_t)g_rgb & 15)))
+  if (grads && ((sil_stride == 4 && ((uintptr_t)g_sil & 15)) || (rgb_stride == 4 && ((uintptr_t)g_rgb & 15))))
     return set_err(MR_EINVAL, "RGBA gradient buffers must be 16-byte aligned");
-  char* w = (char*)ws;
-  float* part = (float*)w;
-  int* pcnt = (int*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256));
-  int64_t* count = (int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) + align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
-  int* mcnt = (int*)((char*)count + 256);
-  hipStream_t st = (hipStream_t)stream;
-  if (!grads) {  // the loss alone
-    const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
-    k_pose_loss_partial<<<nb, 256, 0, st>>>(P, part, pcnt);
-    MR_CHECK_LAUNCH("k_pose_loss_partial");
-    k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, total, terms, count);
-    MR_CHECK_LAUNCH("k_pose_loss_final");
-    return MR_OK;
-  }
-  const int nb = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(npix, 256));
-  k_mask_count<<<nb, 256, 0, st>>>(mask, npix, mcnt);
-  MR_CHECK_LAUNCH("k_mask_count");
-  k_pose_loss_fused<<<nb, 256, 0, st>>>(P, mcnt, nb, part, pcnt, g_depth, g_sil, g_rgb);
-  MR_CHECK_LAUNCH("k_pose_loss_fused");
-  k_pose_loss_final<<<1, 256, 0, st>>>(P, part, pcnt, nb, total, terms, count);
-  MR_CHECK_LAUNCH("k_pose_loss_final");
-  return MR_OK;
+  return pose_loss_run(P, total, terms, ws, g_depth, g_sil, g_rgb, (hipStream_t)stream);
 }
 
 int32_t mr_pose_loss_scale(const float* g_total, int64_t npix, int64_t sil_stride, int64_t rgb_stride, float* g_depth,
@@ -1364,9 +1381,7 @@ int32_t mr_pose_loss_backward(const float* depth, const float* sil, int64_t sil_
   int rc = pose_loss_params(P, depth, sil, sil_stride, rgb, rgb_stride, mask, depth_ref, rgb_ref, npix, delta, w_color);
   if (rc) return rc;
   if (!g_total || !fwd_ws || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL gradient argument");
-  const char* w = (const char*)fwd_ws;
-  const int64_t* count = (const int64_t*)(w + align_up(sizeof(float) * 3 * MR_LOSS_BLOCKS, 256) +
-                                          align_up(sizeof(int) * MR_LOSS_BLOCKS, 256));
+  const int64_t* count = carve_loss((void*)fwd_ws, npix).count;
   if ((sil_stride == 4 && ((uintptr_t)g_sil & 15)) || (rgb_stride == 4 && ((uintptr_t)g_rgb & 15)))
     return set_err(MR_EINVAL, "RGBA gradient buffers must be 16-byte aligned");
   k_pose_loss_bwd<<<(unsigned)ceil_div(npix, 256), 256, 0, (hipStream_t)stream>>>(P, g_total, count, g_depth, g_sil, g_rgb);

@@ -213,7 +213,14 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   return w;
 }
 // The fused path's gradient rows are addressed with 32-bit row numbers (else: float atomics).
-static bool rows_fit(const RasterWS& w) { return w.ovf0 + w.ovf_cap < (1ll << 31) - 1; }
+static bool rows_fit(const RasterWS& w) {
+#ifdef MR_EXP_NOROWS  // experiment builds only: float atomics (the round-3 backward) for A/B
+  (void)w;
+  return false;
+#else
+  return w.ovf0 + w.ovf_cap < (1ll << 31) - 1;
+#endif
+}
 // Bytes to clear from w.ctr before a forward: the counters and, on the count -> scan path, the
 // per-tile counts and per-view totals.
 static size_t zero_bytes(int64_t N, const BinGeom& g, bool view_path) {

@@ -922,6 +922,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   __shared__ long long base[3];
   __shared__ int rows_base;
   __shared__ int nmulti;
+  __shared__ int any_ovf;  // a record of this workgroup needs pool rows
   __shared__ int multi_slot[MR_SCAN_MULTI];
   const int blk = blockIdx.x, t = threadIdx.x;
   const int B = P.bands;
@@ -948,7 +949,10 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   for (int i = t; i < Tb + (Tb >> 6); i += 1024) hist[i] = 0;
-  if (t == 0) nmulti = 0;
+  if (t == 0) {
+    nmulti = 0;
+    any_ovf = 0;
+  }
   lds_barrier();
   const int nq = P.clipz ? 2 : 1;
   uint32_t rr[MR_VIEW_RPT][2];
@@ -968,8 +972,10 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
-      for (int q = 0; q < 2; ++q)
+      for (int q = 0; q < 2; ++q) {
         rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
+        if (P.rbase && k % B == b && ovf_rows(rr[k][q]) > 0) any_ovf = 1;
+      }
   }
   lds_barrier();
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
@@ -991,7 +997,8 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // a fourth allocation overlapping the other three (see the rows block below)
   const bool one = vcount <= 1024 * MR_VIEW_RPT;
   int rows_mine = 0, rows_incl = 0, rows_tot = 0;
-  if (P.rbase && one) {
+  const bool rows = P.rbase && any_ovf;  // (most views: no record exceeds its fixed row slots)
+  if (rows && one) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
       if (k % B == b)
@@ -1000,7 +1007,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     rows_incl = block_incl_sum<true>(rows_mine, part, rows_tot);
   }
   // the allocations from separate waves: their round trips overlap instead of queueing
-  if (t == 192 && P.rbase && one) {
+  if (t == 192 && rows && one) {
     rows_base = rows_tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], rows_tot) : 0;
   } else if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
@@ -1057,7 +1064,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
-  if (P.rbase) {
+  if (rows) {
     // Overflow gradient rows (fused render path): a record of more than MR_ROW_SLOTS tiles gets
     // consecutive pool rows, its k-th tile (row-major inside the rectangle) at rbase[rid] + k (the
     // others use their fixed slots); the backward writes the row of every (record, tile) it shades and

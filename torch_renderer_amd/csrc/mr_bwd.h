@@ -184,6 +184,21 @@ template <int CTRL, int ROW_MASK>
 MR_DEV float dppf(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
 }
+// Sum of v over the wave in a fixed order: DPP butterflies inside each 16-lane row (quad xor 1, quad
+// xor 2, half-row mirror, row mirror), then the four row sums in lane order. Uniform result; no LDS
+// round trips (a __shfl_xor tree is six dependent ds_bpermute per value).
+MR_DEV float wave_sum_f(float v) {
+  v += dppf<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v += dppf<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v += dppf<0x141, 0xf>(v);  // row_half_mirror
+  v += dppf<0x140, 0xf>(v);  // row_mirror
+  const int b = __builtin_bit_cast(int, v);
+  return ((__builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 0)) +
+           __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 16))) +
+          __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 32))) +
+         __builtin_bit_cast(float, __builtin_amdgcn_readlane(b, 48));
+}
+
 // Segmented inclusive sum over lanes: d = distance from the lane to the first lane of its run.
 // row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31 carry a run across rows
 // (the structure of wave_incl_sum, each step gated on the run reaching that far back).
@@ -827,9 +842,15 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
       }
     }
   }
+  if (G == 64) {  // one face per wave: DPP butterflies (fixed order)
 #pragma unroll
-  for (int i = 0; i < ACC; ++i)
-    for (int o = 1; o < G; o <<= 1) acc[i] += __shfl_xor(acc[i], o, 64);  // fixed order inside the group
+    for (int i = 0; i < ACC; ++i) acc[i] = wave_sum_f(acc[i]);
+  } else {  // a fixed xor tree inside each group of G lanes, every component's shuffle of a level together
+    for (int o = 1; o < G; o <<= 1) {
+#pragma unroll
+      for (int i = 0; i < ACC; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
+    }
+  }
   if (j == 0 && f < F) {
 #pragma unroll
     for (int i = 0; i < ACC; ++i) gout[f * ACC + i] = acc[i] + gatom[f * ACC + i];

@@ -163,54 +163,85 @@ __global__ void __launch_bounds__(256) k_mask_total(const int* __restrict__ pcnt
 
 MR_DEV float sgnf(float e) { return e > 0.0f ? 1.0f : (e < 0.0f ? -1.0f : 0.0f); }
 
-// One pixel per thread, one launch over the image (GRAD: also the gradients for dL/dtotal = 1); per-block
-// partial sums for k_pose_loss_final. (A grid-stride version over 2048 workgroups took 323-384 us for the
-// 16.7M-pixel C3 batch against this shape's ~220: its loop issues each iteration's loads only after the
-// previous iteration's stores.)
+// Four pixels per thread (a workgroup's 1024 consecutive pixels, each load instruction lane-contiguous),
+// one launch over the image (GRAD: also the gradients for dL/dtotal = 1); per-workgroup partial sums for
+// k_pose_loss_final, reduced with DPP (fixed order). (A grid-stride loop over 2048 workgroups took 323-384
+// us for the 16.7M-pixel C3 batch: it issues each iteration's loads after the previous iteration's
+// stores; one pixel per thread with __shfl_xor block sums 295 us.)
+#define MR_LOSS_PPT 4
 template <bool GRAD>
 __global__ void __launch_bounds__(256) k_pose_loss_fused(PoseLossParams P, const int64_t* __restrict__ mtot,
                                                          float* __restrict__ part, int* __restrict__ pcnt,
                                                          float* __restrict__ g_depth, float* __restrict__ g_sil,
                                                          float* __restrict__ g_rgb) {
-  __shared__ float sm[4];
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  float l1 = 0.0f, h = 0.0f, mse = 0.0f;
-  int cnt = 0;
-  if (i < P.npix) {
-    const bool m = P.mask[i] != 0;
-    const float e = P.sil[i * P.sil_stride] - (m ? 1.0f : 0.0f);
-    l1 = fabsf(e);
-    const float dd = P.depth[i] - P.depth_ref[i];
-    if (m) {
-      h = huber_val(dd, P.delta);
-      cnt = 1;
+  __shared__ float sm[4][4];
+  const float* __restrict__ depth = P.depth;
+  const float* __restrict__ dref = P.depth_ref;
+  const float* __restrict__ sil = P.sil;
+  const float* __restrict__ rgb = P.rgb;
+  const float* __restrict__ rref = P.rgb_ref;
+  const uint8_t* __restrict__ mask = P.mask;
+  const int64_t i0 = (int64_t)blockIdx.x * (256 * MR_LOSS_PPT) + threadIdx.x;
+  bool m[MR_LOSS_PPT], ok[MR_LOSS_PPT];
+  float sv[MR_LOSS_PPT], dd[MR_LOSS_PPT], e[MR_LOSS_PPT][3];
+#pragma unroll
+  for (int u = 0; u < MR_LOSS_PPT; ++u) {  // every load first
+    const int64_t i = i0 + u * 256;
+    ok[u] = i < P.npix;
+    const int64_t k = ok[u] ? i : 0;
+    m[u] = mask[k] != 0;
+    sv[u] = sil[k * P.sil_stride];
+    dd[u] = depth[k] - dref[k];
+    const float* c = rgb + k * P.rgb_stride;
+    const float* r = rref + 3 * k;
+    e[u][0] = c[0] - r[0];
+    e[u][1] = c[1] - r[1];
+    e[u][2] = c[2] - r[2];
+  }
+  float l1 = 0.0f, h = 0.0f, mse = 0.0f, cnt = 0.0f;
+  const float cs = P.w_color * (2.0f / (float)(3 * P.npix));
+#pragma unroll
+  for (int u = 0; u < MR_LOSS_PPT; ++u) {
+    if (!ok[u]) continue;
+    const int64_t i = i0 + u * 256;
+    const float es = sv[u] - (m[u] ? 1.0f : 0.0f);
+    l1 += fabsf(es);
+    if (m[u]) {
+      h += huber_val(dd[u], P.delta);
+      cnt += 1.0f;
     }
-    const float* c = P.rgb + i * P.rgb_stride;
-    const float* r = P.rgb_ref + 3 * i;
-    const float e0 = c[0] - r[0], e1 = c[1] - r[1], e2 = c[2] - r[2];
-    mse = (e0 * e0 + e1 * e1) + e2 * e2;
+    mse += (e[u][0] * e[u][0] + e[u][1] * e[u][1]) + e[u][2] * e[u][2];
     if (GRAD) {
-      const float gs = 1.0f * (sgnf(e) / (float)P.npix);
+      const float gs = 1.0f * (sgnf(es) / (float)P.npix);
       if (P.sil_stride == 4) ((float4*)g_sil)[i] = make_float4(0.0f, 0.0f, 0.0f, gs);
       else g_sil[i] = gs;
-      g_depth[i] = m ? 1.0f * (huber_grad(dd, P.delta) / (float)*mtot) : 0.0f;
-      const float cs = P.w_color * (2.0f / (float)(3 * P.npix));
+      g_depth[i] = m[u] ? 1.0f * (huber_grad(dd[u], P.delta) / (float)*mtot) : 0.0f;
       if (P.rgb_stride == 4) {
-        ((float4*)g_rgb)[i] = make_float4(cs * e0, cs * e1, cs * e2, 0.0f);
+        ((float4*)g_rgb)[i] = make_float4(cs * e[u][0], cs * e[u][1], cs * e[u][2], 0.0f);
       } else {
-        g_rgb[3 * i] = cs * e0;
-        g_rgb[3 * i + 1] = cs * e1;
-        g_rgb[3 * i + 2] = cs * e2;
+        g_rgb[3 * i] = cs * e[u][0];
+        g_rgb[3 * i + 1] = cs * e[u][1];
+        g_rgb[3 * i + 2] = cs * e[u][2];
       }
     }
   }
-  const float a = block_sum_256(l1, sm), b = block_sum_256(h, sm), cc = block_sum_256(mse, sm);
-  const float n = block_sum_256((float)cnt, sm);
+  const int w = threadIdx.x >> 6;
+  l1 = wave_sum_f(l1);
+  h = wave_sum_f(h);
+  mse = wave_sum_f(mse);
+  cnt = wave_sum_f(cnt);  // exact: <= 256 per wave
+  if ((threadIdx.x & 63) == 0) {
+    sm[0][w] = l1;
+    sm[1][w] = h;
+    sm[2][w] = mse;
+    sm[3][w] = cnt;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    part[3 * blockIdx.x] = a;
-    part[3 * blockIdx.x + 1] = b;
-    part[3 * blockIdx.x + 2] = cc;
-    pcnt[blockIdx.x] = (int)n;
+    part[3 * blockIdx.x] = ((sm[0][0] + sm[0][1]) + sm[0][2]) + sm[0][3];
+    part[3 * blockIdx.x + 1] = ((sm[1][0] + sm[1][1]) + sm[1][2]) + sm[1][3];
+    part[3 * blockIdx.x + 2] = ((sm[2][0] + sm[2][1]) + sm[2][2]) + sm[2][3];
+    pcnt[blockIdx.x] = (int)(((sm[3][0] + sm[3][1]) + sm[3][2]) + sm[3][3]);
   }
 }
 

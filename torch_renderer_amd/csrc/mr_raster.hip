@@ -124,7 +124,7 @@ extern "C++" {
 // workloads, profiles/r2e_bg_ab.txt): beyond these the stores slow the view workgroups' binning
 // more than they shorten the raster.
 #ifndef MR_BG_CPW_RENDER
-#define MR_BG_CPW_RENDER 8  // 5 KB chunks (depth, silhouette, RGB)
+#define MR_BG_CPW_RENDER 12  // 5 KB chunks (depth, silhouette, RGB); 8 -> 12: render 259.0k -> 260.4k, 260.7k -> 263.1k frames/s (profiles/r4k_ab.txt)
 #endif
 #ifndef MR_BG_CPW_FRAG
 #define MR_BG_CPW_FRAG 8    // 7 KB chunks (PyTorch3D fragments; 4 -> 8: fragment pass 166 -> 162 us)
@@ -1288,7 +1288,7 @@ struct LossWS {
   size_t bytes;
 };
 static LossWS carve_loss(void* ws, int64_t npix) {
-  const size_t nb = (size_t)std::max<int64_t>(ceil_div(npix, 256), 1);
+  const size_t nb = (size_t)std::max<int64_t>(ceil_div(npix, 256 * MR_LOSS_PPT), 1);
   LossWS w;
   char* b = (char*)ws;
   size_t off = 0;
@@ -1312,11 +1312,11 @@ size_t mr_pose_loss_workspace(int64_t npix) { return carve_loss(nullptr, npix).b
 static int32_t pose_loss_run(const PoseLossParams& P, float* total, float* terms, void* ws, float* g_depth,
                              float* g_sil, float* g_rgb, hipStream_t st) {
   LossWS w = carve_loss(ws, P.npix);
-  const int64_t nb = ceil_div(P.npix, 256);
+  const int64_t nb = ceil_div(P.npix, 256 * MR_LOSS_PPT);
   if (nb >= (1ll << 31)) return set_err(MR_EUNSUPPORTED, "npix too large");
   const bool grads = g_depth != nullptr;
   if (grads) {
-    const int nm = (int)std::min<int64_t>(MR_LOSS_BLOCKS, nb);
+    const int nm = (int)std::min<int64_t>(MR_LOSS_BLOCKS, ceil_div(P.npix, 256));
     k_mask_count<<<nm, 256, 0, st>>>(P.mask, P.npix, w.mcnt);
     MR_CHECK_LAUNCH("k_mask_count");
     k_mask_total<<<1, 256, 0, st>>>(w.mcnt, nm, w.mtot);

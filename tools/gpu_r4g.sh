@@ -34,3 +34,7 @@ python -c "import json,sys; d=json.loads(open('gpurun_out/c5_${TAG}.json').read(
 [ -n "$AB_R" ] && { bash tools/gpu_ab_r4.sh ${TAG}r "" $AB_R || exit 1; }
 [ -n "$AB_F" ] && { bash tools/gpu_ab_r4.sh ${TAG}f "--mode fragments" $AB_F || exit 1; }
 echo done
+if [ -n "$CPROF" ]; then
+  MR_BENCH_CPROFILE=gpurun_out/pose_cprof_${TAG}.txt timeout -k 10 300 python bench.py --mode pose --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/pose_cp_${TAG}.json 2> gpurun_out/pose_cp_${TAG}.err || { tail -20 gpurun_out/pose_cp_${TAG}.err; exit 1; }
+  head -60 gpurun_out/pose_cprof_${TAG}.txt
+fi

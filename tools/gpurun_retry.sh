@@ -6,7 +6,7 @@ out=$1; to=$2; cmd=$3
 for i in $(seq 1 40); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$out" 2>&1
   rc=$?
-  if [ $rc -ne 3 ] && ! grep -q "no free box right now\|backing off" "$out"; then echo "rc=$rc"; exit $rc; fi
+  if [ $rc -ne 3 ] && ! grep -q "no free box right now\|backing off\|status=transient" "$out"; then echo "rc=$rc"; exit $rc; fi
   sleep 120
 done
 echo "gave up (no box)"; exit 3

@@ -24,6 +24,8 @@ struct SetupParams {
   uint32_t* rects;  // k_bin_view path: per-record tile rectangles
   float* fv_out;    // k_bin_rect_world: face_verts (N*F,3,3) written beside the records (NULL: none)
   const int64_t* vff;  // world mode, distinct meshes: first union face of each view (N+1); NULL: shared mesh
+  int* bcnt;  // band-list counts cleared by the record launch (nbcnt of them)
+  int nbcnt;
 };
 
 // Face-major slot of record rid (its MR_ROW_SLOTS gradient rows start at row MR_ROW_SLOTS * slot): a
@@ -768,6 +770,7 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
   if (n < 0) {
     const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
+    for (int64_t i = v; i < P.nbcnt; i += (int64_t)gridDim.x * blockDim.x) P.bcnt[i] = 0;
     for (int64_t i = v; i < NA.nzero4; i += (int64_t)gridDim.x * blockDim.x) NA.zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int64_t i = v; i < NA.nztag; i += (int64_t)gridDim.x * blockDim.x) NA.ztag[i] = make_uint4(0u, 0u, 0u, 0u);
     if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
@@ -889,7 +892,15 @@ struct ViewBinParams {
   int* rbase;
   uint8_t* rtag;
   int64_t rows_cap;
+  // bands > 1: the records of each (view, band) listed by k_band_bucket (blist[(n B + b) bcap + e],
+  // bcnt[n B + b] of them); NULL: every band reads all of the view's rectangles
+  const int* blist;
+  const int* bcnt;
+  int64_t bcap;
 };
+
+// The band holding tile row ty (bands b hold rows [b TY / B, (b + 1) TY / B)).
+MR_DEV int band_of(int ty, int TY, int B) { return ((ty + 1) * B - 1) / TY; }
 
 
 // Tiles of a rectangle (0 for MR_RECT_NONE).
@@ -901,6 +912,44 @@ MR_DEV int rect_size(uint32_t r) {
 MR_DEV int ovf_rows(uint32_t r) {
   const int sz = rect_size(r);
   return sz > MR_ROW_SLOTS ? sz : 0;
+}
+
+// Band lists for the banded per-view binning of one shared mesh: every record of view n (one thread per
+// face, both triangles of a split face) is appended to the list of each band its tile rectangle meets,
+// one global atomic per (band, workgroup) — so a band's workgroup in k_bin_view reads its ~F / B records
+// instead of all F rectangles of the view (C5: 81,920 faces, one view, 32 bands). The order inside a list
+// is arbitrary; nothing downstream depends on it (the raster's keys are order-free, the backward groups a
+// tile's pixels by record, slots stay in tile order).
+__global__ void __launch_bounds__(1024) k_band_bucket(const uint32_t* __restrict__ rects, int64_t F, int64_t NF, int nq,
+                                                       int TY, int B, int* __restrict__ bcnt, int* __restrict__ blist,
+                                                       int64_t bcap) {
+  __shared__ int lcnt[MR_BANDS_MAX], lbase[MR_BANDS_MAX];
+  const int n = blockIdx.y, t = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * 1024 + t;
+  if (t < B) lcnt[t] = 0;
+  __syncthreads();
+  int rid[2], b0[2], b1[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    rid[q] = (int)((q ? NF : 0) + (int64_t)n * F + i);
+    const uint32_t r = (q < nq && i < F) ? rects[rid[q]] : MR_RECT_NONE;
+    const bool any = rect_size(r) > 0;
+    b0[q] = any ? band_of((int)((r >> 16) & 255), TY, B) : 1;
+    b1[q] = any ? band_of((int)(r >> 24), TY, B) : 0;
+    for (int b = b0[q]; b <= b1[q]; ++b) atomicAdd(&lcnt[b], 1);
+  }
+  __syncthreads();
+  if (t < B) {
+    lbase[t] = lcnt[t] > 0 ? atomicAdd(&bcnt[n * B + t], lcnt[t]) : 0;
+    lcnt[t] = 0;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+    for (int b = b0[q]; b <= b1[q]; ++b) {
+      const int pos = lbase[b] + atomicAdd(&lcnt[b], 1);
+      if (pos < bcap) blist[(int64_t)(n * B + b) * bcap + pos] = rid[q];
+    }
 }
 
 // The band-local tiles (ty - by0) * TX + tx of rectangle r inside tile rows [by0, by1).
@@ -955,26 +1004,50 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   }
   lds_barrier();
   const int nq = P.clipz ? 2 : 1;
+  // the entries this workgroup bins: the view's records (both triangles of a split face per entry), or
+  // with band lists the records k_band_bucket listed for this band (one per entry)
+  const bool lists = P.blist != nullptr;
+  const int* bl = lists ? P.blist + (int64_t)blk * P.bcap : nullptr;
+  const int nent = lists ? (int)min((int64_t)P.bcnt[blk], P.bcap) : vcount;
   uint32_t rr[MR_VIEW_RPT][2];
+  int rid_[MR_VIEW_RPT][2];
   auto load_chunk = [&](int i0) {
+    if (lists) {
+#pragma unroll
+      for (int k = 0; k < MR_VIEW_RPT; ++k) {
+        const int i = i0 + k * 1024 + j;
+        rid_[k][0] = i < nent ? bl[i] : 0;
+        rid_[k][1] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < MR_VIEW_RPT; ++k) {
+        rr[k][0] = i0 + k * 1024 + j < nent ? P.rects[rid_[k][0]] : MR_RECT_NONE;
+        rr[k][1] = MR_RECT_NONE;
+      }
+      return;
+    }
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         const int i = i0 + k * 1024 + j;
-        rr[k][q] = (q < nq && i < vcount) ? P.rects[(q ? P.NF : 0) + f0 + i] : MR_RECT_NONE;
+        rid_[k][q] = (int)((q ? P.NF : 0) + f0 + i);
+        rr[k][q] = (q < nq && i < vcount) ? P.rects[rid_[k][q]] : MR_RECT_NONE;
       }
   };
+  // the entry's record is this workgroup's to allocate pool rows for: with band lists the band holding
+  // the record's first tile row, else chunk slot k's band k % bands
+  auto owns = [&](int k, uint32_t r) { return lists ? band_of((int)((r >> 16) & 255), P.TY, B) == b : k % B == b; };
   // count
 #pragma unroll 1
-  for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+  for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
     load_chunk(i0);
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
-        if (P.rbase && k % B == b && ovf_rows(rr[k][q]) > 0) any_ovf = 1;
+        if (P.rbase && ovf_rows(rr[k][q]) > 0 && owns(k, rr[k][q])) any_ovf = 1;
       }
   }
   lds_barrier();
@@ -995,15 +1068,14 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int is = block_incl_sum<true>(my_s, part, as);
   // a view of one chunk (rectangles still in registers): its gradient rows are allocated here too,
   // a fourth allocation overlapping the other three (see the rows block below)
-  const bool one = vcount <= 1024 * MR_VIEW_RPT;
+  const bool one = nent <= 1024 * MR_VIEW_RPT;
   int rows_mine = 0, rows_incl = 0, rows_tot = 0;
   const bool rows = P.rbase && any_ovf;  // (most views: no record exceeds its fixed row slots)
   if (rows && one) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
-      if (k % B == b)
 #pragma unroll
-        for (int q = 0; q < 2; ++q) rows_mine += ovf_rows(rr[k][q]);
+      for (int q = 0; q < 2; ++q) rows_mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
     rows_incl = block_incl_sum<true>(rows_mine, part, rows_tot);
   }
   // the allocations from separate waves: their round trips overlap instead of queueing
@@ -1073,16 +1145,15 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     // workgroup and chunk (a view of one chunk: made with the list allocations above, none when no
     // record overflows); the allocated rows' tags are cleared here.
 #pragma unroll 1
-    for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+    for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
       int mine = rows_mine, incl = rows_incl, tot = rows_tot;
       if (!one) {
         load_chunk(i0);
         mine = 0;
 #pragma unroll
         for (int k = 0; k < MR_VIEW_RPT; ++k)
-          if (k % B == b)
 #pragma unroll
-            for (int q = 0; q < 2; ++q) mine += ovf_rows(rr[k][q]);
+          for (int q = 0; q < 2; ++q) mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
         incl = block_incl_sum<true>(mine, part, tot);
         if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
         lds_barrier();
@@ -1091,16 +1162,14 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       long long rb = wb + incl - mine;
 #pragma unroll
       for (int k = 0; k < MR_VIEW_RPT; ++k)
-        if (k % B == b)
 #pragma unroll
-          for (int q = 0; q < 2; ++q) {
-            const int i = i0 + k * 1024 + j;
-            const int sz = ovf_rows(rr[k][q]);
-            if (q < nq && i < vcount && sz > 0) {
-              P.rbase[(q ? P.NF : 0) + f0 + i] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
-              rb += sz;
-            }
+        for (int q = 0; q < 2; ++q) {
+          const int sz = owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;  // (0 for entries past the end)
+          if (sz > 0) {
+            P.rbase[rid_[k][q]] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
+            rb += sz;
           }
+        }
       for (int i = t; i < tot; i += 1024)
         if (wb + i < P.rows_cap) P.rtag[wb + i] = 0;
       lds_barrier();  // rows_base is rewritten by the next chunk
@@ -1112,13 +1181,13 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   int* stage = hist + ((Tb + (Tb >> 6) + 3) & ~3);
   const int lst = min(te, P.stage_cap);
 #pragma unroll 1
-  for (int i0 = 0; i0 < vcount; i0 += 1024 * MR_VIEW_RPT) {
+  for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
     if (!one) load_chunk(i0);
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        const int rid = (int)((q ? P.NF : 0) + f0 + i0 + k * 1024 + j);
+        const int rid = rid_[k][q];
         rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) {
           // an overflowing tile's cursor starts at MR_CURSOR_OFF >= list_cap: no store, and no
           // read of the cursor before the atomic

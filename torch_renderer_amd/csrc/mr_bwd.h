@@ -875,30 +875,34 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
   // result does not depend on how many bands (i.e. on the batch size: a view's gradient is bitwise the same
   // in any batch). Four positions' rows are loaded together (a single-view batch has thousands of slots:
   // one dependent load per 256 slots made k_rt_reduce 24 us at C5), then added in sequence order.
-  __shared__ int bfirst[MR_BANDS_MAX], bpre[MR_BANDS_MAX + 1];
+  __shared__ int bfirst[MR_BANDS_MAX], bcount[MR_BANDS_MAX], bpre[MR_BANDS_MAX + 1];
+  if ((int)threadIdx.x < bands) {  // the bands' ranges, loaded in parallel
+    bfirst[threadIdx.x] = vslot[n * bands + threadIdx.x];
+    bcount[threadIdx.x] = vslot[N * bands + n * bands + threadIdx.x];
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
     int tot = 0;
     for (int b = 0; b < bands; ++b) {
-      bfirst[b] = vslot[n * bands + b];
       bpre[b] = tot;
-      tot += vslot[N * bands + n * bands + b];
+      tot += bcount[b];
     }
     bpre[bands] = tot;
   }
   __syncthreads();
   const int total = bpre[bands];
+  int cb = 0;  // this thread's positions only increase: the band pointer advances with them
   auto slot_at = [&](int p) {  // sequence position -> slot
-    int b = 0;
-    while (b + 1 < bands && bpre[b + 1] <= p) ++b;
-    return bfirst[b] + (p - bpre[b]);
+    while (cb + 1 < bands && bpre[cb + 1] <= p) ++cb;
+    return bfirst[cb] + (p - bpre[cb]);
   };
 #pragma unroll 1
   for (int p0 = threadIdx.x; p0 < total; p0 += 4 * 256) {
     float4 r[4][3];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + u * 256;
-      const float4* q = (const float4*)(part + (int64_t)slot_at(p < total ? p : p0) * 12);
+      const int p = p0 + u * 256 < total ? p0 + u * 256 : total - 1;
+      const float4* q = (const float4*)(part + (int64_t)slot_at(p) * 12);
       r[u][0] = q[0];
       r[u][1] = q[1];
       r[u][2] = q[2];

@@ -99,6 +99,8 @@ static SetupParams make_setup(const mr_raster_settings_t* s, const BinGeom& g, c
   P.rects = w.rects;
   P.fv_out = nullptr;
   P.vff = nullptr;
+  P.bcnt = w.bcnt;
+  P.nbcnt = w.nbcnt;
   return P;
 }
 
@@ -151,30 +153,6 @@ static size_t view_lds_bytes() {
   }
   return b;
 }
-static int num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  }
-  return cus;
-}
-// Workgroups (bands of tile rows) per view of the per-view binning: enough for the views to cover
-// 1 / MR_BAND_CU_DIV of the CUs (1 view -> 32 bands, 16 views -> 4, 64 views -> 1 on 256 CUs), at
-// most MR_BANDS_MAX and one tile row per band. The CUs left over stream the background beside the
-// binning: banding 64 views 4 ways starved that share (fragment pass 421k -> 363k frames/s, render
-// 240k -> 223k, profiles/r4f_bands_ab.txt). A pure function of the batch geometry: the backward's
-// R/T reduction walks the same (view, band) ranges.
-#ifndef MR_BAND_CU_DIV
-#define MR_BAND_CU_DIV 4
-#endif
-static int bin_bands(int64_t N, const BinGeom& g) {
-  int64_t b = (int64_t)num_cus() / ((N > 0 ? N : 1) * MR_BAND_CU_DIV);
-  if (b > MR_BANDS_MAX) b = MR_BANDS_MAX;
-  if (b > g.TY) b = g.TY;
-  return b < 1 ? 1 : (int)b;
-}
 // Background workgroups of the k_bin_view launch: the workgroup slots the binning (nbin = views x bands
 // workgroups) and the ShadeRec packing (sb) leave free — one per CU with one workgroup per view (98 KB
 // of LDS each), MR_BG_WG_PER_CU per CU with bands (64 KB: two fit a CU, so a background workgroup can
@@ -226,6 +204,15 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
   V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
   V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
   V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
+  if (B > 1 && !first && !view_count && w.nbcnt == N * B && F > 0) {
+    // one shared mesh: each band's records listed first (the record launch cleared the counts)
+    k_band_bucket<<<dim3((unsigned)ceil_div(F, 1024), (unsigned)N), 1024, 0, st>>>(w.rects, F, SP.NF, SP.clipz ? 2 : 1,
+                                                                                   g.TY, B, w.bcnt, w.blist, w.bcap);
+    MR_CHECK_LAUNCH("k_band_bucket");
+    V.blist = w.blist;
+    V.bcnt = w.bcnt;
+    V.bcap = w.bcap;
+  }
   const int Tb = ((g.TY + B - 1) / B) * g.TX;  // tiles of the largest band
   const size_t hist_b = sizeof(int) * (size_t)((Tb + (Tb >> 6) + 3) & ~3);
   const size_t shm = std::max(hist_b, B > 1 ? (size_t)MR_VIEW_LDS_BANDED : view_lds_bytes());

@@ -113,6 +113,30 @@ static BinGeom bin_geom(int H, int W, int64_t N, int64_t Ftot, int32_t mfpb) {
   return g;
 }
 
+static int num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus;
+}
+// Workgroups (bands of tile rows) per view of the per-view binning: enough for the views to cover
+// 1 / MR_BAND_CU_DIV of the CUs (1 view -> 32 bands, 16 views -> 4, 64 views -> 1 on 256 CUs), at
+// most MR_BANDS_MAX and one tile row per band. The CUs left over stream the background beside the
+// binning: banding 64 views 4 ways starved that share (fragment pass 421k -> 363k frames/s, render
+// 240k -> 223k, profiles/r4f_bands_ab.txt). A pure function of the batch geometry: the backward's
+// R/T reduction walks the same (view, band) ranges.
+#ifndef MR_BAND_CU_DIV
+#define MR_BAND_CU_DIV 4
+#endif
+static int bin_bands(int64_t N, const BinGeom& g) {
+  int64_t b = (int64_t)num_cus() / ((N > 0 ? N : 1) * MR_BAND_CU_DIV);
+  if (b > MR_BANDS_MAX) b = MR_BANDS_MAX;
+  if (b > g.TY) b = g.TY;
+  return b < 1 ? 1 : (int)b;
+}
 struct RasterWS {
   FaceRec* recs;
   int* ctr;    // (CTR_COUNT) units / slots emitted by the scan, covered pixels, entries (u64)
@@ -144,6 +168,13 @@ struct RasterWS {
   float* rrows;    // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) rows of MR_ROW_STRIDE(acc) floats
   int64_t ovf0;    // first pool row (= MR_ROW_SLOTS * 2 Ftot)
   int64_t ovf_cap; // pool rows
+  // banded per-view binning of one shared mesh (bands > 1): each (view, band)'s records, listed by
+  // k_band_bucket (bcap = 2 Ftot / N: both triangles of every face of the view), and their counts
+  // (cleared by the record launch)
+  int* bcnt;
+  int* blist;
+  int64_t bcap;
+  int nbcnt;       // N * bands (0: no lists)
   size_t bytes;
 };
 // Gradient rows of `acc` floats are stored 16-B aligned (stride MR_ROW_STRIDE(acc) floats: whole float4
@@ -209,6 +240,13 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + nrows, 256);
   w.rrows = (float*)(b + off);
   off = align_up(off + sizeof(float) * MR_ROW_STRIDE(27) * nrows, 256);
+  const int B = bin_bands(N, g);
+  w.nbcnt = B > 1 ? (int)(N * B) : 0;
+  w.bcap = B > 1 ? 2 * ((Ftot > 0 ? Ftot : 1) + N - 1) / N : 0;
+  w.bcnt = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)w.nbcnt, 256);
+  w.blist = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (size_t)w.nbcnt * (size_t)w.bcap, 256);
   w.bytes = off;
   return w;
 }

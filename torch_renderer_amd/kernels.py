@@ -353,6 +353,20 @@ def _vertex_normals(v, f, vptr, vadj):
 
 
 # --------------------------------------------------------------------------- fused render
+_STRUCT_CACHE: dict = {}  # ShadeConfig values -> its ctypes structs (per-call host work of the eager loops)
+_WS_CACHE: dict = {}      # workspace-size queries by their arguments
+
+
+def _ws_size(fn, *args):
+    k = (fn.__name__,) + args
+    v = _WS_CACHE.get(k)
+    if v is None:
+        if len(_WS_CACHE) > 256:
+            _WS_CACHE.clear()
+        v = _WS_CACHE[k] = int(fn(*args))
+    return v
+
+
 @dataclass
 class ShadeConfig:
     """Static (non-differentiable) configuration of one fused render call."""
@@ -389,11 +403,28 @@ class ShadeConfig:
     frag_sorted: bool = False  # fragment shading: empty slots follow the filled ones (MR_FRAG_SORTED)
     zbuf: bool = False  # depth output = zbuf[..., 0] of K = 1 fragments (background -1), not relu of it
 
+    def key(self):
+        """The configuration's values (field order is the dataclass's): the struct caches' key."""
+        return tuple(self.__dict__.values())
+
     def raster_struct(self):
-        return raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip, self.cull,
-                                      self.max_faces_per_bin, self.z_clip)
+        k = ("r", self.key())
+        hit = _STRUCT_CACHE.get(k)
+        if hit is None:
+            hit = _STRUCT_CACHE[k] = raster_settings_struct(self.H, self.W, 1, self.blur, self.persp, self.clip,
+                                                            self.cull, self.max_faces_per_bin, self.z_clip)
+        return MrRasterSettings.from_buffer_copy(hit)  # a copy: callers set flags on it
 
     def shade_struct(self):
+        k = ("s", self.key())
+        hit = _STRUCT_CACHE.get(k)
+        if hit is None:
+            if len(_STRUCT_CACHE) > 256:
+                _STRUCT_CACHE.clear()
+            hit = _STRUCT_CACHE[k] = self._shade_struct()
+        return MrShadeParams.from_buffer_copy(hit)
+
+    def _shade_struct(self):
         sp = MrShadeParams()
         sp.light_kind = int(self.light_kind)
         for name in ("light_location", "light_ambient", "light_diffuse", "light_specular", "mat_ambient",
@@ -462,7 +493,7 @@ def _tsig(t):
 
 
 def _shade_sig(cfg):
-    return tuple(sorted((k, v) for k, v in cfg.__dict__.items()))
+    return cfg.key()
 
 
 def _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges):
@@ -517,7 +548,7 @@ class RenderViews(torch.autograd.Function):
         rgb = torch.empty((N, H, W, cfg.rgb_channels), device=dev) if cfg.want_rgb else None
         p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
         wsq = L.mr_render_workspace_meshes if ranges is not None else L.mr_render_workspace
-        wsb = wsq(N, f.shape[0], H, W, rs.max_faces_per_bin)
+        wsb = _ws_size(wsq, N, f.shape[0], H, W, rs.max_faces_per_bin)
         geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges)
         ent = _RESHADE["entry"]
         ssig = _shade_sig(cfg)
@@ -578,14 +609,14 @@ class RenderViews(torch.autograd.Function):
         if cfg.want_rgb:
             gC = grads[gi]
             gi += 1
-        cfg2 = ShadeConfig(**{**cfg.__dict__})
-        cfg2.want_depth = gD is not None
-        cfg2.want_sil = gS is not None
-        cfg2.want_rgb = gC is not None
         mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None,
                             ctx.ranges)
-        rs = cfg2.raster_struct()
-        sp = cfg2.shade_struct()
+        rs = cfg.raster_struct()
+        sp = cfg.shade_struct()
+        # the outputs whose gradients arrived (absent ones: NULL, no zero tensors)
+        sp.out_flags &= ~((0 if gD is not None else _lib.MR_OUT_DEPTH | _lib.MR_OUT_ZBUF) |
+                          (0 if gS is not None else _lib.MR_OUT_SIL | _lib.MR_OUT_SIL_RGBA) |
+                          (0 if gC is not None else _lib.MR_OUT_RGB))
         sp.out_flags |= ctx.slot << _lib.MR_SREC_SLOT_SHIFT  # the ShadeRecs this node's forward packed
         ent = _RESHADE["entry"]
         if ent is not None and ent["ws"] is ws:  # a backward over the workspace ends its reuse
@@ -596,7 +627,7 @@ class RenderViews(torch.autograd.Function):
         gverts = torch.empty_like(v)
         gviews = torch.empty((N, 12), device=dev)
         gcol = torch.empty_like(v) if ctx.has_vcol else None
-        bwb = L.mr_render_backward_workspace(N, v.shape[0], f.shape[0], cfg.H, cfg.W)
+        bwb = _ws_size(L.mr_render_backward_workspace, N, v.shape[0], f.shape[0], cfg.H, cfg.W)
         bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
         c = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
         if ctx.pose_cv:  # pose grads straight in the OpenCV frame (no separate conversion launch)

@@ -790,6 +790,9 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
+  // one wave per face (G = 64): lane i < ACC fetches the face's float-atomic row entry i now and stores
+  // total i at the end (one coalesced load and store instead of ACC dependent single-lane ones)
+  const float gat = (G == 64 && lane < ACC && f < F) ? gatom[f * ACC + lane] : 0.0f;
   auto add4 = [&](const float4 (&x4)[RS / 4]) {
     const float* x = (const float*)x4;
 #pragma unroll
@@ -842,9 +845,15 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
       }
     }
   }
-  if (G == 64) {  // one face per wave: DPP butterflies (fixed order)
+  if (G == 64) {  // one face per wave: DPP butterflies (fixed order), lane i stores total i
+    float mine = 0.0f;
 #pragma unroll
-    for (int i = 0; i < ACC; ++i) acc[i] = wave_sum_f(acc[i]);
+    for (int i = 0; i < ACC; ++i) {
+      const float t = wave_sum_f(acc[i]);
+      mine = lane == i ? t : mine;
+    }
+    if (lane < ACC && f < F) gout[f * ACC + lane] = mine + gat;
+    return;
   } else {  // a fixed xor tree inside each group of G lanes, every component's shuffle of a level together
     for (int o = 1; o < G; o <<= 1) {
 #pragma unroll

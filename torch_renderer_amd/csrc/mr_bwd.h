@@ -470,7 +470,13 @@ MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__
       if (j < tot) {
         const float x = lrow[j];
         const int q = lq[r];
-        if (q >= 0) rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
+        if (q >= 0) {
+#ifdef MR_ROWS_NT  // experiment: rows stored past the L2 (no dirty lines to write back at the kernel's end)
+          __builtin_nontemporal_store(x, rows + (int64_t)q * MR_ROW_STRIDE(ACC) + c);
+#else
+          rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
+#endif
+        }
         else if (x != 0.0f) atomicAdd(gface + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
       }
     }
@@ -507,9 +513,10 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
   r = load_rec(P.recs, f < 0 ? 0 : f);
   fr = P.frec[(int64_t)slot * 64 + lane];
-  const int* pr = P.rbase ? P.rbase + (f < 0 ? 0 : f) : (const int*)g_zero4;
+  // the record's tile rectangle (its row slots); the pool base rbase is read only for the rare record of
+  // more than MR_ROW_SLOTS tiles, where the row is computed
   const uint32_t* pt = P.rbase ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
-  rb = *pr;
+  rb = 0;
   rect = *pt;
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
@@ -745,9 +752,12 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         const int slot0 = MR_ROW_SLOTS * (int)(P.F ? ((f >= P.NF ? P.F : 0) + face) * P.N + n : f);
         if ((rx1 - rx0 + 1) * (ry1 - ry0 + 1) <= MR_ROW_SLOTS) {
           q = slot0 + k;
-        } else if (rb >= 0) {
-          q = (int)P.ovf0 + rb + k;
-          qf = slot0;
+        } else {
+          const int rbo = P.rbase[f];
+          if (rbo >= 0) {
+            q = (int)P.ovf0 + rbo + k;
+            qf = slot0;
+          }
         }
       }
     }

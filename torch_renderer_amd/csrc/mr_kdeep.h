@@ -402,16 +402,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     int4* ent = P.sent + base + (incl - cnt);
     float alpha_nz = 1.0f;
     int nzero = 0, kzero = -1;
+    // the keys leave the list through q[0]; the next key's record is loaded while this one is evaluated
+    // (unconditional load of record 0 for an empty key: a guarded load would be waited on at once)
+    unsigned long long key_n = q[0];
+    FaceRec r_n = load_rec(P.recs, key_n < MR_KEY_EMPTY ? code_rec((unsigned)(key_n & 0xffffffffull), P.NF) : 0);
 #pragma unroll 1
     for (int k = 0; k < K; ++k) {
-      if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
-      const unsigned long long key = q[0];
+      if (__ballot(key_n < MR_KEY_EMPTY) == 0ull) break;
+      const unsigned long long key = key_n;
+      const FaceRec r = r_n;
 #pragma unroll
       for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
       q[KP - 1] = MR_KEY_EMPTY;
+      key_n = q[0];
+      r_n = load_rec(P.recs, key_n < MR_KEY_EMPTY ? code_rec((unsigned)(key_n & 0xffffffffull), P.NF) : 0);
       if (!in_img || !(key < MR_KEY_EMPTY)) continue;
       const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
-      const FaceRec r = P.recs[id];
       FragEval ev;
       eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
       const float prob = frag_prob(ev.sdist, P.isig);
@@ -437,16 +443,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const float xf = col_ndc(px, H, W), yf = row_ndc(py, H, W);
   // only the filled slots (k_fill wrote the background of every slot); keys shifted out through q[0]
   // (constant indices only: the array stays in registers)
+  unsigned long long key_n = q[0];  // (the next key's record in flight, as in the SIL tail above)
+  FaceRec r_n = load_rec(P.recs, key_n < MR_KEY_EMPTY ? code_rec((unsigned)(key_n & 0xffffffffull), P.NF) : 0);
 #pragma unroll 1
   for (int k = 0; k < K; ++k) {
-    if (__ballot(q[0] < MR_KEY_EMPTY) == 0ull) break;
-    const unsigned long long key = q[0];
+    if (__ballot(key_n < MR_KEY_EMPTY) == 0ull) break;
+    const unsigned long long key = key_n;
+    const FaceRec r = r_n;
 #pragma unroll
     for (int i = 0; i + 1 < KP; ++i) q[i] = q[i + 1];
     q[KP - 1] = MR_KEY_EMPTY;
+    key_n = q[0];
+    r_n = load_rec(P.recs, key_n < MR_KEY_EMPTY ? code_rec((unsigned)(key_n & 0xffffffffull), P.NF) : 0);
     if (!(key < MR_KEY_EMPTY)) continue;
     const int id = code_rec((unsigned)(key & 0xffffffffull), P.NF);
-    const FaceRec r = P.recs[id];
     FragEval ev;
     eval_face(r, xf, yf, pad, blur, persp, clipb, ev);  // kept by construction
     if (r.flags & FR_CLIP) clip_unconvert(P.crec[id], ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);

@@ -206,8 +206,8 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
   V.units = w.units; V.ctr = w.ctr; V.tkey = w.tkey; V.list = w.list;
   if (B > 1 && !first && !view_count && w.nbcnt == N * B && F > 0) {
     // one shared mesh: each band's records listed first (the record launch cleared the counts)
-    k_band_bucket<<<dim3((unsigned)ceil_div(F, 1024), (unsigned)N), 1024, 0, st>>>(w.rects, F, SP.NF, SP.clipz ? 2 : 1,
-                                                                                   g.TY, B, w.bcnt, w.blist, w.bcap);
+    MR_TIMED(KID_BAND_BUCKET, st, (k_band_bucket<<<dim3((unsigned)ceil_div(F, 1024), (unsigned)N), 1024, 0, st>>>(
+                                       w.rects, F, SP.NF, SP.clipz ? 2 : 1, g.TY, B, w.bcnt, w.blist, w.bcap)));
     MR_CHECK_LAUNCH("k_band_bucket");
     V.blist = w.blist;
     V.bcnt = w.bcnt;

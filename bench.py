@@ -1028,6 +1028,7 @@ def bench_c5(args, dev, world, rank):
 
     elapsed = _time_steps(step, args, dev, world)
     kt = _kernel_times(step, min(args.steps, 10))
+    _host_profile(step, dev)
     # work counters of one view's forward (render_stats reads the live workspace)
     norm = torch.nn.functional.hardtanh(verts_rgb, 0.0, 1.0).detach()
     keep = renderer(Meshes([verts0], [faces], TexturesVertex(verts_features=norm)), cameras=target_cameras[0],

@@ -240,3 +240,66 @@ def test_c3_three_calls_share_one_raster():
     assert served == 2 and served_off == 1
     for nm, a, b in zip(("depth", "silhouette", "colour", "pose grad"), shared, indep):
         assert torch.equal(a, b), f"{nm} differs between the shared raster and three passes"
+
+
+def _icosahedron():
+    """12 vertices, 20 faces (outward winding), slightly perturbed so no two faces tie exactly."""
+    p = (1.0 + 5 ** 0.5) / 2.0
+    v = torch.tensor([[-1, p, 0], [1, p, 0], [-1, -p, 0], [1, -p, 0], [0, -1, p], [0, 1, p], [0, -1, -p],
+                      [0, 1, -p], [p, 0, -1], [p, 0, 1], [-p, 0, -1], [-p, 0, 1]], dtype=torch.float32)
+    f = torch.tensor([[0, 11, 5], [0, 5, 1], [0, 1, 7], [0, 7, 10], [0, 10, 11], [1, 5, 9], [5, 11, 4], [11, 10, 2],
+                      [10, 7, 6], [7, 1, 8], [3, 9, 4], [3, 4, 2], [3, 2, 6], [3, 6, 8], [3, 8, 9], [4, 9, 5],
+                      [2, 4, 11], [6, 2, 10], [8, 6, 7], [9, 8, 1]], dtype=torch.int64)
+    g = torch.Generator().manual_seed(5)
+    return v + (torch.rand(v.shape, generator=g) - 0.5) * 0.05, f
+
+
+def test_large_faces_take_pool_rows_deterministic_vs_oracle():
+    """Faces far larger than a tile (an icosahedron filling a 128x128 image: ~20 tiles per face) have their
+    gradient rows in k_bin_view's overflow pool instead of the 4 fixed slots (read from the workspace's
+    pool counter): vertex and pose gradients against the oracle within the per-entry bars, and bitwise
+    equal over two runs (the pool's allocation order varies with the atomics, the sums do not)."""
+    from tests.helpers import canonical_views
+    from torch_renderer_amd import kernels as Kn
+
+    verts, faces = _icosahedron()
+    N, H, W = 3, 128, 128
+    R, T, intr, _ = canonical_views(verts, N, H, W, dist=4.0)
+    gen = torch.Generator().manual_seed(2)
+    gD = torch.rand(N, H, W, generator=gen) * 2 - 1
+    gS = torch.rand(N, H, W, generator=gen) * 2 - 1
+    gC = torch.rand(N, H, W, 3, generator=gen) * 2 - 1
+    light = dict(O.DEFAULT_LIGHT)
+
+    def flat(precision):
+        vr, Rr, Tr = (x.clone().requires_grad_(True) for x in (verts, R, T))
+        ref = O.render_ref(vr, faces, Rr, Tr, intr, H, W, light=light, precision=precision)
+        dt = ref["rgba"].dtype
+        ((ref["depth"] * gD.to(dt)).sum() + (ref["sil"] * gS.to(dt)).sum() +
+         (ref["rgba"][..., :3] * gC.to(dt)).sum()).backward()
+        return ref["depth"].detach(), ref["rgba"][..., :3].detach(), vr.grad, Rr.grad, Tr.grad
+
+    ref, r64, sp = oracle_runs(flat)
+
+    def gpu():
+        cfg = Kn.ShadeConfig(H=H, W=W)
+        vg, Rg, Tg = (x.to(DEV).requires_grad_(True) for x in (verts, R, T))
+        out = Kn.render_views(vg, Rg, Tg, faces.to(DEV), intr.to(DEV), torch.zeros(1, 3, device=DEV), cfg)
+        ws = out["depth"].grad_fn.saved_tensors[5]
+        ctr = (ctypes.c_int32 * 8)()
+        _lib.check(_lib.load().mr_workspace_counters(_lib.ptr(ws), N, N * faces.shape[0], H, W, 0,
+                                                     ctypes.cast(ctr, ctypes.c_void_p), _lib.stream_handle(DEV)))
+        ((out["depth"] * gD.to(DEV)).sum() + (out["sil"] * gS.to(DEV)).sum() + (out["rgb"] * gC.to(DEV)).sum()).backward()
+        torch.cuda.synchronize()
+        return out, (vg.grad, Rg.grad, Tg.grad), ctr[7]
+
+    out, g1, pool_rows = gpu()
+    print(f"[large faces] pool rows allocated: {pool_rows}")
+    assert pool_rows > 0, "no record took the overflow pool"
+    report("large faces depth", out["depth"], ref[0], rel_above_one=False, ref64=r64[0], sens=sp[0])
+    report("large faces rgb", out["rgb"], ref[1], rel_above_one=False, ref64=r64[1], sens=sp[1])
+    for i, nm in enumerate(("verts", "R", "T")):
+        report(f"large faces grad {nm}", g1[i], ref[2 + i], ref64=r64[2 + i], sens=sp[2 + i])
+    _, g2, _ = gpu()
+    for a, b, nm in zip(g1, g2, ("verts", "R", "T")):
+        assert torch.equal(a, b), f"{nm} gradient differs between two runs"

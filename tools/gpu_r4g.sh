@@ -38,3 +38,7 @@ if [ -n "$CPROF" ]; then
   MR_BENCH_CPROFILE=gpurun_out/pose_cprof_${TAG}.txt timeout -k 10 300 python bench.py --mode pose --no-cpu-baseline --steps 10 --warmup 3 > gpurun_out/pose_cp_${TAG}.json 2> gpurun_out/pose_cp_${TAG}.err || { tail -20 gpurun_out/pose_cp_${TAG}.err; exit 1; }
   head -60 gpurun_out/pose_cprof_${TAG}.txt
 fi
+if [ -n "$CPROF5" ]; then
+  MR_BENCH_CPROFILE=gpurun_out/c5_cprof_${TAG}.txt timeout -k 10 300 python bench.py --mode c5 --no-cpu-baseline --steps 5 --warmup 2 > gpurun_out/c5_cp_${TAG}.json 2> gpurun_out/c5_cp_${TAG}.err || { tail -20 gpurun_out/c5_cp_${TAG}.err; exit 1; }
+  head -70 gpurun_out/c5_cprof_${TAG}.txt
+fi

@@ -515,7 +515,7 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
   fr = P.frec[(int64_t)slot * 64 + lane];
   // the record's tile rectangle (its row slots); the pool base rbase is read only for the rare record of
   // more than MR_ROW_SLOTS tiles, where the row is computed
-  const uint32_t* pt = P.rbase ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
+  const uint32_t* pt = P.rtag ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
   rb = 0;
   rect = *pt;
   const float* pD = P.gD ? P.gD + pix : g_zero4;
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         const int slot0 = MR_ROW_SLOTS * (int)(P.F ? ((f >= P.NF ? P.F : 0) + face) * P.N + n : f);
         if ((rx1 - rx0 + 1) * (ry1 - ry0 + 1) <= MR_ROW_SLOTS) {
           q = slot0 + k;
-        } else {
+        } else if (P.rbase) {
           const int rbo = P.rbase[f];
           if (rbo >= 0) {
             q = (int)P.ovf0 + rbo + k;
@@ -775,12 +775,13 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
 // are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) whose tag
-// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 64), lane j
-// taking views j, j + G, ...: per view one 32-bit load of the record's four tags, then its tagged rows,
-// two loads in flight (a record whose slot 0 holds 2 walks its pool rows instead); the G partial sums
-// are then added by a fixed xor tree. Two dependent round trips per (face, view) — per-slot tag loads
-// spread over four rounds measured 29 us per render step, 16-slot lanes walking their rows one by one 41.
-// Workgroups are dispatched round-robin over the 8 XCDs: block b takes faces from XCD-contiguous ranges.
+// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 16), lane j
+// taking views j, j + G, ... in that order, four views' 32-bit tag words loaded together, then their
+// tagged rows two loads in flight (a record whose slot 0 holds 2 walks its pool rows instead); the G
+// partial sums are then added by a fixed DPP tree inside each 16-lane row. Four faces per wave at 64
+// views: a wave per face made the launch dispatch-bound (5,856 short waves; PMC: 2.3 us of life per
+// wave against a 20-us kernel). Workgroups are dispatched round-robin over the 8 XCDs: block b takes
+// faces from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
                                                      int64_t ovf0, const int* __restrict__ rbase,
@@ -800,9 +801,6 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
   for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
   const int nv = F_shared ? N : 1;
-  // one wave per face (G = 64): lane i < ACC fetches the face's float-atomic row entry i now and stores
-  // total i at the end (one coalesced load and store instead of ACC dependent single-lane ones)
-  const float gat = (G == 64 && lane < ACC && f < F) ? gatom[f * ACC + lane] : 0.0f;
   auto add4 = [&](const float4 (&x4)[RS / 4]) {
     const float* x = (const float*)x4;
 #pragma unroll
@@ -818,53 +816,61 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
       // the face's record in view 0: its rec_slot (the views' records follow)
       const int64_t r0 = F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f;
 #pragma unroll 1
-      for (int n = j; n < nv; n += G) {
-        const uint32_t tw = ((const uint32_t*)rtag)[r0 + n];
-        if (tw == 0u) continue;
-        if ((tw & 255u) == 2u) {  // the record's rows are in the pool
-          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
-          const int rb = rbase[rid];
-          const int sz = rect_size(rects[rid]);
-#pragma unroll 1
-          for (int k = 0; k < sz; ++k)
-            if (rtag[ovf0 + rb + k]) {
-              float4 x4[RS / 4];
-              load4(ovf0 + rb + k, x4);
-              add4(x4);
-            }
-          continue;
-        }
-        uint32_t m = 0;  // bit k: tile k's row tagged
+      for (int n0 = j; n0 < nv; n0 += 4 * G) {
+        uint32_t tw[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) m |= (((tw >> (8 * k)) & 255u) == 1u ? 1u : 0u) << k;
-        const int64_t row0 = (r0 + n) * MR_ROW_SLOTS;
+        for (int u = 0; u < 4; ++u) tw[u] = n0 + u * G < nv ? ((const uint32_t*)rtag)[r0 + n0 + u * G] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (tw[u] == 0u) continue;
+          const int n = n0 + u * G;
+          if ((tw[u] & 255u) == 2u) {  // the record's rows are in the pool
+            const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
+            const int rb = rbase[rid];
+            const int sz = rect_size(rects[rid]);
 #pragma unroll 1
-        while (m) {
-          const int k1 = __builtin_ctz(m);
-          m &= m - 1u;
-          const int k2 = m ? __builtin_ctz(m) : k1;
-          float4 xa[RS / 4], xb[RS / 4];
-          load4(row0 + k1, xa);
-          load4(row0 + k2, xb);
-          add4(xa);
-          if (m) {
+            for (int k = 0; k < sz; ++k)
+              if (rtag[ovf0 + rb + k]) {
+                float4 x4[RS / 4];
+                load4(ovf0 + rb + k, x4);
+                add4(x4);
+              }
+            continue;
+          }
+          uint32_t m = 0;  // bit k: tile k's row tagged
+#pragma unroll
+          for (int k = 0; k < 4; ++k) m |= (((tw[u] >> (8 * k)) & 255u) == 1u ? 1u : 0u) << k;
+          const int64_t row0 = (r0 + n) * MR_ROW_SLOTS;
+#pragma unroll 1
+          while (m) {
+            const int k1 = __builtin_ctz(m);
             m &= m - 1u;
-            add4(xb);
+            const int k2 = m ? __builtin_ctz(m) : k1;
+            float4 xa[RS / 4], xb[RS / 4];
+            load4(row0 + k1, xa);
+            load4(row0 + k2, xb);
+            add4(xa);
+            if (m) {
+              m &= m - 1u;
+              add4(xb);
+            }
           }
         }
       }
     }
   }
-  if (G == 64) {  // one face per wave: DPP butterflies (fixed order), lane i stores total i
-    float mine = 0.0f;
+  // the G partial sums of each face: a fixed DPP tree inside the 16-lane row (G = 16), else a fixed xor tree
+  if (G == 16) {
 #pragma unroll
     for (int i = 0; i < ACC; ++i) {
-      const float t = wave_sum_f(acc[i]);
-      mine = lane == i ? t : mine;
+      float v = acc[i];
+      v += dppf<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+      v += dppf<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+      v += dppf<0x141, 0xf>(v);  // row_half_mirror
+      v += dppf<0x140, 0xf>(v);  // row_mirror
+      acc[i] = v;
     }
-    if (lane < ACC && f < F) gout[f * ACC + lane] = mine + gat;
-    return;
-  } else {  // a fixed xor tree inside each group of G lanes, every component's shuffle of a level together
+  } else {
     for (int o = 1; o < G; o <<= 1) {
 #pragma unroll
       for (int i = 0; i < ACC; ++i) acc[i] += __shfl_xor(acc[i], o, 64);

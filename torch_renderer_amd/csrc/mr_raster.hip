@@ -189,7 +189,11 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.Fs = F;
     sb = ceil_div(F, 1024);
     // the fused render path: pool rows of the records too large for their fixed gradient-row slots
+#ifdef MR_EXP_NOPOOL  // experiment builds only: no pool (records of > 4 tiles take float atomics)
+    if (false) {
+#else
     if (rows_fit(w)) {
+#endif
       V.rbase = w.rbase;
       V.rtag = w.rtag + w.ovf0;
       V.rows_cap = w.ovf_cap;
@@ -993,7 +997,9 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   // per-view binning (k_bin_view) allocates; the count -> scan path has none (float atomics into gface)
   const bool vpath = view_binning(g, N, NF) && rows_fit(w);
   if (vpath) {
+#ifndef MR_EXP_NOPOOL
     P.rbase = w.rbase;
+#endif
     P.rects = w.rects;
     P.rtag = w.rtag;
     P.rrows = w.rrows;
@@ -1019,8 +1025,8 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   {
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 64)
-    while (G < 64 && G < (multi ? 1 : (int)N)) G <<= 1;
+    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 16)
+    while (G < 16 && G < (multi ? 1 : (int)N)) G <<= 1;
     int nb = ceil_div(m->F, 256 / G);
     nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {

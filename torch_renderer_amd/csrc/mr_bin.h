@@ -657,9 +657,6 @@ __global__ void __launch_bounds__(1024) k_bin_scan(ScanParams P) {
 #define MR_RECT_NONE 0x000000ffu        // tx0 = 255 > tx1 = 0: an empty rectangle
 #define MR_CURSOR_OFF 0x40000000        // fill cursor of a tile whose list is not filled (list_cap <= it)
 #define MR_VIEW_RPT 8                   // rectangles per thread per chunk
-#ifndef MR_HIST_COPIES
-#define MR_HIST_COPIES 1                // LDS histogram copies of k_bin_view (lane % copies)
-#endif
 MR_DEV uint32_t rec_rect(const SetupParams& P, const FaceRec& r) {
   int tx0, tx1, ty0, ty1;
   if (!rec_tiles(P, r, tx0, tx1, ty0, ty1)) return MR_RECT_NONE;
@@ -993,19 +990,11 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // band tile lt lives at hist[lt + lt / 64] (the scan's per-thread runs of C tiles spread over the
   // banks); a view's rectangles are read in chunks of MR_VIEW_RPT per thread, all loads of a
   // chunk in flight together, and a view of one chunk keeps them in registers for the fill.
-#ifdef MR_VIEW_PERM  // experiment: a wave's lanes on faces 16 apart (mesh-order neighbours hit the same tiles)
-  const int j = (t & 63) * 16 + (t >> 6);
-#else
   const int j = t;
-#endif
   const int64_t f0 = P.first ? P.first[n] : (int64_t)n * P.F;
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
-  // MR_HIST_COPIES histograms: lane l counts (and later fills) through copy l % copies, so neighbouring
-  // faces of the mesh order — which hit the same tiles — no longer serialise on one LDS address
-  const int HS = (Tb + (Tb >> 6) + 3) & ~3;  // one copy's ints
-  const int cp = (t & 63) % MR_HIST_COPIES;
-  int* hc = hist + cp * HS;                  // this lane's copy
-  for (int i = t; i < MR_HIST_COPIES * HS; i += 1024) hist[i] = 0;
+  const int HS = (Tb + (Tb >> 6) + 3) & ~3;  // the histogram's ints (padded)
+  for (int i = t; i < HS; i += 1024) hist[i] = 0;
   if (t == 0) {
     nmulti = 0;
     any_ovf = 0;
@@ -1054,7 +1043,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
-        rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hc[tt + (tt >> 6)], 1); });
+        rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
         if (P.rbase && ovf_rows(rr[k][q]) > 0 && owns(k, rr[k][q])) any_ovf = 1;
       }
   }
@@ -1064,9 +1053,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int t0 = min(t * C, Tb), t1 = min(t0 + C, Tb);
   int le = 0, my_u = 0, my_s = 0;
   for (int tt = t0; tt < t1; ++tt) {
-    int cc = 0;
-#pragma unroll
-    for (int c = 0; c < MR_HIST_COPIES; ++c) cc += hist[c * HS + tt + (tt >> 6)];
+    const int cc = hist[tt + (tt >> 6)];
     le += cc;
     const bool mo = P.mfpb > 0 && cc > P.mfpb;  // PyTorch3D's per-bin cap: the whole-view path
     my_u += cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
@@ -1109,9 +1096,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   if (t == 0 && b == 0) P.vbase[n] = 0;
   int u0 = (int)base[0] + iu - my_u, slot = (int)base[1] + is - my_s;
   for (int tt = t0, ex = ex0; tt < t1; ++tt) {
-    int cc = 0;
-#pragma unroll
-    for (int c = 0; c < MR_HIST_COPIES; ++c) cc += hist[c * HS + tt + (tt >> 6)];
+    const int cc = hist[tt + (tt >> 6)];
     const int gt = n * P.T + T0 + tt;
     if (P.ranges) {
       P.cnt[gt] = cc;
@@ -1140,12 +1125,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       else
         for (int i = 0; i < 64; ++i) P.tkey[(int64_t)slot * 64 + i] = MR_KEY_EMPTY;
     }
-    // fill cursors: copy c's entries of the tile follow copies 0 .. c-1's (overflowing lists are not filled)
-    for (int c = 0, cur = (int)(vb + ex); c < MR_HIST_COPIES; ++c) {
-      const int n_c = hist[c * HS + tt + (tt >> 6)];
-      hist[c * HS + tt + (tt >> 6)] = ovf ? MR_CURSOR_OFF : cur;
-      cur += n_c;
-    }
+    hist[tt + (tt >> 6)] = ovf ? MR_CURSOR_OFF : (int)(vb + ex);  // fill cursor (overflowing lists are not filled)
     u0 += nu;
     slot += cc > 0 ? 1 : 0;
     ex += cc;
@@ -1195,7 +1175,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   // fill: the band's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
   // staged in LDS and stored as consecutive lines afterwards (scattered 4-B stores issue one
   // lane per cycle), the rest (a band larger than the stage) go straight to the pool
-  int* stage = hist + MR_HIST_COPIES * HS;
+  int* stage = hist + HS;
   const int lst = min(te, P.stage_cap);
 #pragma unroll 1
   for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
@@ -1208,7 +1188,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
         rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) {
           // an overflowing tile's cursor starts at MR_CURSOR_OFF >= list_cap: no store, and no
           // read of the cursor before the atomic
-          const int pos = atomicAdd(&hc[tt + (tt >> 6)], 1);
+          const int pos = atomicAdd(&hist[tt + (tt >> 6)], 1);
           if (pos < P.list_cap) {
             const int rel = (int)(pos - vb);
             if (rel < lst) stage[rel] = rid;

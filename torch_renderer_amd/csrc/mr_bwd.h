@@ -470,13 +470,7 @@ MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__
       if (j < tot) {
         const float x = lrow[j];
         const int q = lq[r];
-        if (q >= 0) {
-#ifdef MR_ROWS_NT  // experiment: rows stored past the L2 (no dirty lines to write back at the kernel's end)
-          __builtin_nontemporal_store(x, rows + (int64_t)q * MR_ROW_STRIDE(ACC) + c);
-#else
-          rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
-#endif
-        }
+        if (q >= 0) rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
         else if (x != 0.0f) atomicAdd(gface + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
       }
     }

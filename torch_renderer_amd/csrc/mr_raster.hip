@@ -218,7 +218,7 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.bcap = w.bcap;
   }
   const int Tb = ((g.TY + B - 1) / B) * g.TX;  // tiles of the largest band
-  const size_t hist_b = sizeof(int) * MR_HIST_COPIES * (size_t)((Tb + (Tb >> 6) + 3) & ~3);
+  const size_t hist_b = sizeof(int) * (size_t)((Tb + (Tb >> 6) + 3) & ~3);
   const size_t shm = std::max(hist_b, B > 1 ? (size_t)MR_VIEW_LDS_BANDED : view_lds_bytes());
   V.stage_cap = (int)((shm - hist_b) / sizeof(int));
   if constexpr (MODE >= 0) {

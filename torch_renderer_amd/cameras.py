@@ -132,7 +132,15 @@ class FoVPerspectiveCameras(CamerasBase):
 
 
 def _param_key(cameras):
-    return tuple((k, v.data_ptr(), v._version) for k, v in sorted(vars(cameras).items()) if torch.is_tensor(v))
+    """(name, storage, version) of the camera's tensor attributes — the caches' key. The attribute names
+    are listed once per set of attribute names (an eager loop calls this several times per render)."""
+    d = vars(cameras)
+    keys = tuple(k for k in d if k != "_pk_names")
+    names = d.get("_pk_names")
+    if names is None or names[0] != keys:
+        names = (keys, tuple(k for k in sorted(keys) if torch.is_tensor(d[k])))
+        d["_pk_names"] = names
+    return tuple((k, d[k].data_ptr(), d[k]._version) for k in names[1] if torch.is_tensor(d[k]))
 
 
 def cached_ndc_affine(cameras: CamerasBase, image_size, device):

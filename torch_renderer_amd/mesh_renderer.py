@@ -597,8 +597,8 @@ class MeshRenderer(torch.nn.Module):
         H, W = rs.hw()
         cfg = self._config(cameras, rs, H, W, kwargs)
         cfg.sil_rgba = not cfg.want_rgb  # SoftSilhouetteShader's (1, 1, 1, alpha) straight from the kernels
-        R, T, _ = _views(meshes, cameras, (H, W), kwargs)
+        R, T, intr = _views(meshes, cameras, (H, W), kwargs)
         # specular camera position: cameras.get_camera_center() without the R/T kwargs (upstream
         # shading.py), i.e. from the camera object's own R, T
-        out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg)
+        out = render_mesh_batch(meshes, cameras, (H, W), R, T, cfg, views=(R, T, intr))
         return out["rgb"] if cfg.want_rgb else out["sil"]

@@ -129,14 +129,18 @@ def textures_need_modular(meshes: Meshes) -> bool:
 
 
 def render_mesh_batch(meshes: Meshes, cameras, image_size, R, T, cfg: ShadeConfig, cam_center=None,
-                      pose_cv=False):
+                      pose_cv=False, views=None):
     """Render every view of `meshes` (shared mesh or per-view meshes) with the fused kernels.
     Returns dict(depth, sil, rgb[, pix_to_face32 if cfg.want_p2f]) with tensors of batch N.
     pose_cv: R, T are OpenCV poses; the PyTorch3D conversion of torch_renderer.py:73-80 runs
     on the GPU inside the render (mr_views_from_opencv) and gradients come back in kind."""
     H, W = image_size
-    n = max(len(meshes), R.reshape(-1, 3, 3).shape[0], T.reshape(-1, 3).shape[0])
-    Rb, Tb, intr = view_batch(cameras, (H, W), R, T, n_views=n)
+    if views is not None:  # (R, T, intr) already broadcast by the caller's view_batch
+        Rb, Tb, intr = views
+        n = Rb.shape[0]
+    else:
+        n = max(len(meshes), R.reshape(-1, 3, 3).shape[0], T.reshape(-1, 3).shape[0])
+        Rb, Tb, intr = view_batch(cameras, (H, W), R, T, n_views=n)
     if cam_center is None:
         cam_center = cached_camera_center(cameras, Rb.device)
     need_color = cfg.want_rgb

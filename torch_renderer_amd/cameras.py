@@ -132,15 +132,23 @@ class FoVPerspectiveCameras(CamerasBase):
 
 
 def _param_key(cameras):
-    """(name, storage, version) of the camera's tensor attributes — the caches' key. The attribute names
-    are listed once per set of attribute names (an eager loop calls this several times per render)."""
+    """The caches' key: (name, storage, version) of the camera's tensor attributes and (name, value) of its
+    scalar ones (FoV cameras keep fov / aspect_ratio / znear as floats). The attribute names are listed
+    once per set of names (an eager loop calls this several times per render)."""
     d = vars(cameras)
-    keys = tuple(k for k in d if k != "_pk_names")
+    keys = tuple(k for k in d if not k.startswith("_") or k == "_in_ndc")
     names = d.get("_pk_names")
     if names is None or names[0] != keys:
-        names = (keys, tuple(k for k in sorted(keys) if torch.is_tensor(d[k])))
+        names = (keys, tuple(sorted(keys)))
         d["_pk_names"] = names
-    return tuple((k, d[k].data_ptr(), d[k]._version) for k in names[1] if torch.is_tensor(d[k]))
+    out = []
+    for k in names[1]:
+        v = d[k]
+        if torch.is_tensor(v):
+            out.append((k, v.data_ptr(), v._version))
+        elif isinstance(v, (bool, int, float, str)):
+            out.append((k, v))
+    return tuple(out)
 
 
 def cached_ndc_affine(cameras: CamerasBase, image_size, device):

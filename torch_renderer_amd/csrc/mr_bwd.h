@@ -501,7 +501,7 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // phi copies wait on the load right away, which defeats the prefetch.
 __device__ float g_zero4[4];
 MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
-                             float4& fr, int& rb, uint32_t& rect) {
+                             float4& fr, uint32_t& rect) {
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
@@ -510,7 +510,6 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
   // the record's tile rectangle (its row slots); the pool base rbase is read only for the rare record of
   // more than MR_ROW_SLOTS tiles, where the row is computed
   const uint32_t* pt = P.rtag ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
-  rb = 0;
   rect = *pt;
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
@@ -608,11 +607,10 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   FaceRec r_c;
   float g_c[5];
   float4 fr_c;
-  int rb_c;
   uint32_t rect_c;
   // lane -> tile pixel p_c of the slot in flight (pixels grouped by record, sort_slot_pixels)
   int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
-  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rb_c, rect_c);
+  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rect_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
   for (; s < send; s += G) {
@@ -620,7 +618,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c, p = p_c;
     const FaceRec r = r_c;
     const float4 frag = fr_c;
-    const int rb = rb_c;
     const uint32_t rect = rect_c;
     float gin[5];
 #pragma unroll
@@ -629,7 +626,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     f_c = f_n;
     sl_c = sl_n;
     p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
-    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rb_c, rect_c);
+    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rect_c);
     sc = min(s + 2 * G, slast);
     sl_n = sc;
     gt_n = P.stile[sc + lz];

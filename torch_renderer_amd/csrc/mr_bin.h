@@ -110,6 +110,28 @@ MR_DEV int block_incl_sum(int v, int* part16, int& tot) {
   return w + (wave > 0 ? before : 0);
 }
 
+// Four inclusive scans over a 1024-thread workgroup in one pass: the four DPP wave scans, ONE LDS exchange
+// of the 4 x 16 wave totals, two LDS-only barriers (three block_incl_sum calls take six). Uniform call only.
+MR_DEV void block_incl_sum4(const int (&v)[4], int (*part4)[16], int (&incl)[4], int (&tot)[4]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = wave_incl_sum(v[k]);
+  if (lane == 63) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part4[k][wave] = w[k];
+  }
+  lds_barrier();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int ws = wave_incl_sum(lane < 16 ? part4[k][lane] : 0);
+    tot[k] = __builtin_amdgcn_readlane(ws, 15);
+    const int before = __shfl(ws, wave > 0 ? wave - 1 : 0, 64);
+    incl[k] = w[k] + (wave > 0 ? before : 0);
+  }
+  lds_barrier();  // part4 is reused by the next call
+}
+
 // Inverse of col_ndc/row_ndc (approximate, widened by 0.05 px; the raster
 // kernel repeats the exact per-pixel bbox test, so a superset is all we need).
 MR_DEV void ndc_range_to_pix(float lo, float hi, int S1, int S2, int& p0, int& p1) {
@@ -968,6 +990,7 @@ MR_DEV void rect_tiles(uint32_t r, int TX, int by0, int by1, Fn&& fn) {
 MR_DEV void bin_view_body(const ViewBinParams& P) {
   extern __shared__ __attribute__((aligned(16))) int hist[];  // Tb (+ Tb/64 pad): counts, then fill cursors
   __shared__ int part[16];
+  __shared__ int part4[4][16];
   __shared__ long long base[3];
   __shared__ int rows_base;
   __shared__ int nmulti;
@@ -1059,22 +1082,22 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     my_u += cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
     my_s += cc > 0 ? 1 : 0;
   }
-  int te, au, as;
-  const int ex0 = block_incl_sum<true>(le, part, te) - le;
-  const int iu = block_incl_sum<true>(my_u, part, au);
-  const int is = block_incl_sum<true>(my_s, part, as);
-  // a view of one chunk (rectangles still in registers): its gradient rows are allocated here too,
-  // a fourth allocation overlapping the other three (see the rows block below)
+  // a view of one chunk (rectangles still in registers): its overflow gradient rows are counted here too,
+  // a fourth scan and allocation beside the list / unit / slot ones (see the rows block below)
   const bool one = nent <= 1024 * MR_VIEW_RPT;
-  int rows_mine = 0, rows_incl = 0, rows_tot = 0;
+  int rows_mine = 0;
   const bool rows = P.rbase && any_ovf;  // (most views: no record exceeds its fixed row slots)
   if (rows && one) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
       for (int q = 0; q < 2; ++q) rows_mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
-    rows_incl = block_incl_sum<true>(rows_mine, part, rows_tot);
   }
+  int sc_in[4] = {le, my_u, my_s, rows_mine}, sc_incl[4], sc_tot[4];
+  block_incl_sum4(sc_in, part4, sc_incl, sc_tot);
+  const int te = sc_tot[0], au = sc_tot[1], as = sc_tot[2];
+  const int ex0 = sc_incl[0] - le, iu = sc_incl[1], is = sc_incl[2];
+  const int rows_incl = sc_incl[3], rows_tot = sc_tot[3];
   // the allocations from separate waves: their round trips overlap instead of queueing
   if (t == 192 && rows && one) {
     rows_base = rows_tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], rows_tot) : 0;

@@ -766,12 +766,13 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
 // are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) whose tag
-// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 16), lane j
-// taking views j, j + G, ... in that order, four views' 32-bit tag words loaded together, then their
-// tagged rows two loads in flight (a record whose slot 0 holds 2 walks its pool rows instead); the G
-// partial sums are then added by a fixed DPP tree inside each 16-lane row. Four faces per wave at 64
-// views: a wave per face made the launch dispatch-bound (5,856 short waves; PMC: 2.3 us of life per
-// wave against a 20-us kernel). Workgroups are dispatched round-robin over the 8 XCDs: block b takes
+// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 16) take its
+// views in batches of 4G: the 4G tag words are loaded together (lane j: views j, j + G, j + 2G, j + 3G),
+// the tagged fixed-slot rows are compacted in LDS and dealt round-robin to the G lanes (four loads in
+// flight), and each lane then walks the pool rows of its records whose slot 0 holds 2 (eight tag bytes at
+// a time). The G partial sums are added by a fixed DPP tree inside each 16-lane row. Four faces per wave
+// at 64 views: a wave per face made the launch dispatch-bound (5,856 short waves; PMC: 2.3 us of life
+// per wave against a 20-us kernel). Workgroups are dispatched round-robin over the 8 XCDs: block b takes
 // faces from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
@@ -802,50 +803,104 @@ __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F
 #pragma unroll
     for (int i = 0; i < RS / 4; ++i) x4[i] = src[i];
   };
-  if (f < F) {
-    for (int q = 0; q <= clip; ++q) {
-      // the face's record in view 0: its rec_slot (the views' records follow)
-      const int64_t r0 = F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f;
+  // the tagged rows of pool mask m in bit order (bit b: row base + b), four loads in flight
+  auto walk = [&](uint32_t m, int64_t base) {
 #pragma unroll 1
-      for (int n0 = j; n0 < nv; n0 += 4 * G) {
-        uint32_t tw[4];
+    while (m) {
+      int k[4];
+      bool v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) tw[u] = n0 + u * G < nv ? ((const uint32_t*)rtag)[r0 + n0 + u * G] : 0u;
+      for (int i = 0; i < 4; ++i) {
+        v[i] = m != 0u;
+        k[i] = v[i] ? __builtin_ctz(m) : k[0];
+        m &= m - 1u;
+      }
+      float4 x[4][RS / 4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          if (tw[u] == 0u) continue;
-          const int n = n0 + u * G;
-          if ((tw[u] & 255u) == 2u) {  // the record's rows are in the pool
-            const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)n * F_shared : 0) + f;
-            const int rb = rbase[rid];
-            const int sz = rect_size(rects[rid]);
+      for (int i = 0; i < 4; ++i) load4(base + k[i], x[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (v[i]) add4(x[i]);
+    }
+  };
+  // A face's tagged fixed-slot rows of one batch of 4G views, compacted in LDS in a fixed order (lane
+  // j's views j, j + G, j + 2G, j + 3G, tiles ascending, lanes in order) and dealt round-robin to its G
+  // lanes: every lane of a face loads about the same number of rows (per-view lanes waited on the
+  // face's most covered views).
+  __shared__ uint16_t lst[256 * 16];
+  uint16_t* my = lst + ((wave * 64 + lane) / G) * 16 * G;
+#ifndef MR_FR_INFL
+#define MR_FR_INFL 4
+#endif
+  constexpr int INFL = ACC == 27 ? 4 : MR_FR_INFL;  // rows in flight per lane
+  for (int q = 0; q <= clip; ++q) {
+    // the face's record in view 0: its rec_slot (the views' records follow)
+    const int64_t r0 = F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f;
 #pragma unroll 1
-            for (int k = 0; k < sz; ++k)
-              if (rtag[ovf0 + rb + k]) {
-                float4 x4[RS / 4];
-                load4(ovf0 + rb + k, x4);
-                add4(x4);
-              }
-            continue;
-          }
-          uint32_t m = 0;  // bit k: tile k's row tagged
+    for (int nb = 0; nb < nv; nb += 4 * G) {
+      uint32_t tw[4];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) m |= (((tw[u] >> (8 * k)) & 255u) == 1u ? 1u : 0u) << k;
-          const int64_t row0 = (r0 + n) * MR_ROW_SLOTS;
+      for (int u = 0; u < 4; ++u) {
+        const int n = nb + j + u * G;
+        tw[u] = f < F && n < nv ? ((const uint32_t*)rtag)[r0 + n] : 0u;
+      }
+      // the pool records among the four (slot 0 tagged 2): their pool base and size
+      int rb[4], sz[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        rb[u] = sz[u] = 0;
+        if ((tw[u] & 255u) == 2u) {
+          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)(nb + j + u * G) * F_shared : 0) + f;
+          rb[u] = rbase[rid];
+          sz[u] = rect_size(rects[rid]);
+        }
+      }
+      // bit 4u + k: view nb + j + uG, tile k
+      uint32_t m = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m |= (((tw[u] >> (8 * k)) & 255u) == 1u ? 1u : 0u) << (4 * u + k);
+      const int c = __builtin_popcount(m);
+      int x = c;  // inclusive scan of the counts over the face's G lanes
+      for (int o = 1; o < G; o <<= 1) {
+        const int t = __shfl_up(x, o, G);
+        if (j >= o) x += t;
+      }
+      const int tot = __shfl(x, G - 1, G);
+      for (int o = x - c; m; m &= m - 1u, ++o) {
+        const int b = __builtin_ctz(m);
+        my[o] = (uint16_t)((j + (b >> 2) * G) * MR_ROW_SLOTS + (b & 3));
+      }
+      __syncthreads();
+      const int64_t R0 = (r0 + nb) * MR_ROW_SLOTS;
 #pragma unroll 1
-          while (m) {
-            const int k1 = __builtin_ctz(m);
-            m &= m - 1u;
-            const int k2 = m ? __builtin_ctz(m) : k1;
-            float4 xa[RS / 4], xb[RS / 4];
-            load4(row0 + k1, xa);
-            load4(row0 + k2, xb);
-            add4(xa);
-            if (m) {
-              m &= m - 1u;
-              add4(xb);
-            }
-          }
+      for (int i0 = j; i0 < tot; i0 += INFL * G) {
+        int e[INFL];
+        bool v[INFL];
+#pragma unroll
+        for (int t = 0; t < INFL; ++t) {
+          v[t] = i0 + t * G < tot;
+          e[t] = my[v[t] ? i0 + t * G : i0];
+        }
+        float4 xr[INFL][RS / 4];
+#pragma unroll
+        for (int t = 0; t < INFL; ++t) load4(R0 + e[t], xr[t]);
+#pragma unroll
+        for (int t = 0; t < INFL; ++t)
+          if (v[t]) add4(xr[t]);
+      }
+      __syncthreads();
+      // then this lane's pool records' rows, eight tag bytes at a time
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+#pragma unroll 1
+        for (int k0 = 0; k0 < sz[u]; k0 += 8) {
+          const int64_t base = ovf0 + rb[u] + k0;
+          uint32_t pm = 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) pm |= (k0 + k < sz[u] && rtag[base + k] ? 1u : 0u) << k;
+          walk(pm, base);
         }
       }
     }

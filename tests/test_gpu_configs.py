@@ -462,3 +462,32 @@ def test_large_image_count_scan_fill_path():
         report(f"1040 grad {nm}", a, ref[3 + i], ref64=r64[3 + i], sens=sp[3 + i])
     assert torch.equal(out["pix_to_face32"].long(), _modular_p2f(verts, faces, R_cv, t_cv, K, H, W))
     _check_background(out, out["pix_to_face32"], (1.0, 1.0, 1.0))
+
+
+def test_vertex_grads_additive_over_view_batches():
+    """k_face_reduce deals a face's views to G lanes in batches of 4G views (G = 16 at >= 16 views, 8 at
+    5 views): the shared vertex gradient of 80 views in one call (two view batches) equals the sum of
+    three calls over 5, 16 and 59 of those views (G = 8, 16, 16; one batch each) within float reordering,
+    and each view's R / t gradient is bitwise the same in any batch (its slots' partial rows are summed as
+    one sequence whatever the band split)."""
+    H = W = 128
+    N = 80
+    verts, faces, d = mesh_arrays("cow")
+    img, vuv, fuv = _uv_texture(d)
+    tex = TexturesUV(maps=[img.to(DEV)], faces_uvs=[fuv.to(DEV)], verts_uvs=[vuv.to(DEV)])
+    _, _, _, (R_cv, t_cv, K) = canonical_views(verts, N, H, W, dist=0.5)
+    grads = _upstream(N, H, W, seed=3)
+    out, (gv, gR, gt) = _gpu_views(verts, faces, tex, R_cv, t_cv, K, H, W, grads)
+    acc = torch.zeros_like(gv)
+    for a, b in ((0, 5), (5, 21), (21, 80)):
+        texs = TexturesUV(maps=[img.to(DEV)], faces_uvs=[fuv.to(DEV)], verts_uvs=[vuv.to(DEV)])
+        o, (sv, sR, st) = _gpu_views(verts, faces, texs, R_cv[a:b], t_cv[a:b], K, H, W,
+                                     tuple(g[a:b] for g in grads))
+        p = o["pix_to_face32"]  # packed ids: view n's faces are n * F + f
+        assert torch.equal(torch.where(p >= 0, p + a * faces.shape[0], p), out["pix_to_face32"][a:b])
+        assert torch.equal(sR, gR[a:b]) and torch.equal(st, gt[a:b]), (a, b)
+        acc += sv
+    scale = gv.abs().max().item()
+    err = (acc - gv).abs().max().item()
+    print(f"[view batches] vertex grad |sum of 5+16+59 views - 80 views| max {err:.3e} (scale {scale:.3e})")
+    assert err <= 1e-4 * scale

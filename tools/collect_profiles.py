@@ -16,7 +16,7 @@ ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 def short(name):
     n = name.replace("void ", "").split("(")[0].strip()
-    m = re.match(r"(k_bwd_fused|k_rt_vgrad_a|k_bwd_geom|k_vgrad_a|k_vgrad_b|k_tile_raster|k_bin_count_world|k_bin_fill_world|k_bin_view|k_bin_rect_world|k_bin_rect_fv)<.*>", n)
+    m = re.match(r"(k_bwd_fused|k_face_reduce|k_rt_vgrad_a|k_bwd_geom|k_vgrad_a|k_vgrad_b|k_tile_raster|k_bin_count_world|k_bin_fill_world|k_bin_view|k_bin_rect_world|k_bin_rect_fv)<.*>", n)
     if m:
         return {"k_bin_count_world": "k_bin_count", "k_bin_fill_world": "k_bin_fill", "k_bin_rect_world": "k_bin_rect", "k_bin_rect_fv": "k_bin_rect"}.get(m.group(1), m.group(1))
     m = re.match(r"k_shade<(\d+), *\d+>", n)

@@ -1156,45 +1156,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
-  if (rows) {
-    // Overflow gradient rows (fused render path): a record of more than MR_ROW_SLOTS tiles gets
-    // consecutive pool rows, its k-th tile (row-major inside the rectangle) at rbase[rid] + k (the
-    // others use their fixed slots); the backward writes the row of every (record, tile) it shades and
-    // k_face_reduce sums a face's rows in a fixed order (deterministic vertex gradients, no float
-    // atomics). The records of chunk slot k belong to band k % bands; one pool allocation per
-    // workgroup and chunk (a view of one chunk: made with the list allocations above, none when no
-    // record overflows); the allocated rows' tags are cleared here.
-#pragma unroll 1
-    for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
-      int mine = rows_mine, incl = rows_incl, tot = rows_tot;
-      if (!one) {
-        load_chunk(i0);
-        mine = 0;
-#pragma unroll
-        for (int k = 0; k < MR_VIEW_RPT; ++k)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
-        incl = block_incl_sum<true>(mine, part, tot);
-        if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
-        lds_barrier();
-      }
-      const long long wb = rows_base;
-      long long rb = wb + incl - mine;
-#pragma unroll
-      for (int k = 0; k < MR_VIEW_RPT; ++k)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int sz = owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;  // (0 for entries past the end)
-          if (sz > 0) {
-            P.rbase[rid_[k][q]] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
-            rb += sz;
-          }
-        }
-      for (int i = t; i < tot; i += 1024)
-        if (wb + i < P.rows_cap) P.rtag[wb + i] = 0;
-      lds_barrier();  // rows_base is rewritten by the next chunk
-    }
-  }
   // fill: the band's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
   // staged in LDS and stored as consecutive lines afterwards (scattered 4-B stores issue one
   // lane per cycle), the rest (a band larger than the stage) go straight to the pool
@@ -1223,5 +1184,46 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   for (int i = t; i < lst; i += 1024)
     if (vb + i < P.list_cap) P.list[vb + i] = stage[i];
+  if (rows) {
+    // Overflow gradient rows (fused render path): a record of more than MR_ROW_SLOTS tiles gets
+    // consecutive pool rows, its k-th tile (row-major inside the rectangle) at rbase[rid] + k (the
+    // others use their fixed slots); the backward writes the row of every (record, tile) it shades and
+    // k_face_reduce sums a face's rows in a fixed order (deterministic vertex gradients, no float
+    // atomics). The records of chunk slot k belong to band k % bands; one pool allocation per
+    // workgroup and chunk (a view of one chunk: made with the list allocations above, none when no
+    // record overflows); the allocated rows' tags are cleared here. Done last, after the list stores:
+    // between the scan and the fill these few scattered stores cost the binning 6 us, here 4
+    // (profiles/r4w_pool_ab.txt).
+#pragma unroll 1
+    for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
+      int mine = rows_mine, incl = rows_incl, tot = rows_tot;
+      if (!one) {
+        load_chunk(i0);
+        mine = 0;
+#pragma unroll
+        for (int k = 0; k < MR_VIEW_RPT; ++k)
+#pragma unroll
+          for (int q = 0; q < 2; ++q) mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
+        incl = block_incl_sum<true>(mine, part, tot);
+        if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
+        lds_barrier();
+      }
+      const long long wb = rows_base;
+      for (int i = t; i < tot; i += 1024)
+        if (wb + i < P.rows_cap) P.rtag[wb + i] = 0;
+      long long rb = wb + incl - mine;
+#pragma unroll
+      for (int k = 0; k < MR_VIEW_RPT; ++k)
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int sz = owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;  // (0 for entries past the end)
+          if (sz > 0) {
+            P.rbase[rid_[k][q]] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
+            rb += sz;
+          }
+        }
+      if (!one) lds_barrier();  // rows_base is rewritten by the next chunk
+    }
+  }
 }
 __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) { bin_view_body(P); }

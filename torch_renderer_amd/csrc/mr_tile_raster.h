@@ -573,6 +573,9 @@ __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __rest
 
 // CLIP: near-plane clipping on (split faces may be present); the CLIP = false instantiation
 // carries none of their code, so the common launch keeps its register budget.
+#ifndef MR_TR_BGFIRST_FRAG
+#define MR_TR_BGFIRST_FRAG 4
+#endif
 #ifndef MR_RASTER_WAVES
 #define MR_RASTER_WAVES 4  // waves / SIMD: 5 -> <= 96 VGPRs, 4 -> <= 128
 #endif
@@ -601,9 +604,47 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
   const int jw = (blockIdx.x / parts) * 4 + wave, Gp = (gridDim.x / parts) * 4;
   const int Cp = (nunits + parts - 1) / parts;
+#ifdef MR_EXP_TR_NOUNITS
+  const int ub = 0, ue = 0;
+#else
   const int ub = (blockIdx.x % parts) * Cp, ue = ub + Cp < nunits ? ub + Cp : nunits;
+#endif
   const Bg bg = background<MODE>(P);
+#ifdef MR_EXP_TR_NOBG
+  int chunk = nchunks;
+#else
   int chunk = P.fill_first + gw;
+#endif
+  // the wave's background chunks c = chunk, chunk + G, ... (view, chunk) stepped incrementally: no
+  // integer division per chunk
+  auto background_chunks = [&]() {
+    const int gn = G / cpv, gc = G - gn * cpv;
+    int cn = chunk / cpv, cc = chunk - cn * cpv;
+    if (MODE == 0 && P.emit_frag) {
+#pragma unroll 1
+      for (; chunk < nchunks; chunk += G) {
+        fill_frag_unlisted(P, cn, cc);
+        cn += gn;
+        cc += gc;
+        if (cc >= cpv) { cc -= cpv; ++cn; }
+      }
+    } else {
+#pragma unroll 1
+      for (; chunk < nchunks; chunk += G) {
+        fill_chunk<MODE, CH>(P, bg, cn, cc, vec);
+        cn += gn;
+        cc += gc;
+        if (cc >= cpv) { cc -= cpv; ++cn; }
+      }
+    }
+  };
+  // Fragments (K = 1): one wave in MR_TR_BGFIRST_FRAG (alternating over workgroups, so each SIMD holds
+  // both kinds) streams its background first, overlapping the other waves' latency-bound raster
+  // (alone: units 59 us, background 53 us, together 92; one in 4 first: 89, one in 2: 94 — the
+  // fused render loses 2-3 % with either, profiles/r4y_bgfirst_ab.txt)
+  if (MODE == 0 && MR_TR_BGFIRST_FRAG > 0 &&
+      (blockIdx.x + wave) % (MR_TR_BGFIRST_FRAG > 0 ? MR_TR_BGFIRST_FRAG : 1) == 0)
+    background_chunks();
   // Software pipeline over the wave's units u, u + Gp, u + 2Gp, ...: while unit u is
   // rasterised, the face records of u + Gp, the list entries of u + 2Gp and the unit record of
   // u + 3Gp are in flight (unit records are wave-uniform scalar loads). Each link of the
@@ -782,26 +823,7 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
     }
     wave_lds_sync();
   }
-  // (view, chunk) stepped incrementally: no integer division per chunk
-  const int gn = G / cpv, gc = G - gn * cpv;
-  int cn = chunk / cpv, cc = chunk - cn * cpv;
-  if (MODE == 0 && P.emit_frag) {
-#pragma unroll 1
-    for (; chunk < nchunks; chunk += G) {
-      fill_frag_unlisted(P, cn, cc);
-      cn += gn;
-      cc += gc;
-      if (cc >= cpv) { cc -= cpv; ++cn; }
-    }
-  } else {
-#pragma unroll 1
-    for (; chunk < nchunks; chunk += G) {
-      fill_chunk<MODE, CH>(P, bg, cn, cc, vec);
-      cn += gn;
-      cc += gc;
-      if (cc >= cpv) { cc -= cpv; ++cn; }
-    }
-  }
+  background_chunks();
 }
 
 // Per-face shading records of the shared mesh (one thread per face).

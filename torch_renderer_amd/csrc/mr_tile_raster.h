@@ -604,17 +604,9 @@ __global__ void __launch_bounds__(256, MR_RASTER_WAVES) k_tile_raster(FwdParams 
   const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
   const int jw = (blockIdx.x / parts) * 4 + wave, Gp = (gridDim.x / parts) * 4;
   const int Cp = (nunits + parts - 1) / parts;
-#ifdef MR_EXP_TR_NOUNITS
-  const int ub = 0, ue = 0;
-#else
   const int ub = (blockIdx.x % parts) * Cp, ue = ub + Cp < nunits ? ub + Cp : nunits;
-#endif
   const Bg bg = background<MODE>(P);
-#ifdef MR_EXP_TR_NOBG
-  int chunk = nchunks;
-#else
   int chunk = P.fill_first + gw;
-#endif
   // the wave's background chunks c = chunk, chunk + G, ... (view, chunk) stepped incrementally: no
   // integer division per chunk
   auto background_chunks = [&]() {

@@ -766,13 +766,13 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
 // with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
 // are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) whose tag
-// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 16) take its
+// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 32) take its
 // views in batches of 4G: the 4G tag words are loaded together (lane j: views j, j + G, j + 2G, j + 3G),
 // the tagged fixed-slot rows are compacted in LDS and dealt round-robin to the G lanes (four loads in
 // flight), and each lane then walks the pool rows of its records whose slot 0 holds 2 (eight tag bytes at
-// a time). The G partial sums are added by a fixed DPP tree inside each 16-lane row. Four faces per wave
-// at 64 views: a wave per face made the launch dispatch-bound (5,856 short waves; PMC: 2.3 us of life
-// per wave against a 20-us kernel). Workgroups are dispatched round-robin over the 8 XCDs: block b takes
+// a time). The G partial sums are added by a fixed DPP tree inside each 16-lane row (G = 16) or a fixed
+// xor-shuffle tree. Two faces per wave at 64 views (G = 32; one wave per face, G = 64, measured slower).
+// Workgroups are dispatched round-robin over the 8 XCDs: block b takes
 // faces from XCD-contiguous ranges.
 template <int ACC>
 __global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,

@@ -1025,8 +1025,12 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   {
     const int clip = s->clip_z ? 1 : 0;
     const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 16)
-    while (G < 16 && G < (multi ? 1 : (int)N)) G <<= 1;
+    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 32; 16: face
+                // reduction 23.5 -> 21.3 us at 64 views, 64: 23.0, profiles/r4y_face_lanes_ab.txt)
+#ifndef MR_FR_GMAX
+#define MR_FR_GMAX 32
+#endif
+    while (G < MR_FR_GMAX && G < (multi ? 1 : (int)N)) G <<= 1;
     int nb = ceil_div(m->F, 256 / G);
     nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
     if (vpath) {

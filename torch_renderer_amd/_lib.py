@@ -205,7 +205,15 @@ def strided_ptr(t):
 
 
 def stream_handle(device=None):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    """The current HIP stream of `device` (torch.device, index or None: the current device) as a handle:
+    the raw stream pointer, without building a torch Stream object per launch."""
+    if isinstance(device, torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+    elif isinstance(device, int):
+        idx = device
+    else:
+        idx = torch.cuda.current_device()
+    return ctypes.c_void_p(torch._C._cuda_getCurrentRawStream(idx))
 
 
 def timing_enable(on: bool = True) -> None:

@@ -488,6 +488,17 @@ def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol, ranges=None):
 _RESHADE = {"entry": None, "enabled": True}
 
 
+_EMPTY0 = {}
+
+
+def _empty0(dev):
+    """A cached empty tensor on `dev` (the placeholder saved for absent optional inputs)."""
+    t = _EMPTY0.get(dev)
+    if t is None:
+        t = _EMPTY0[dev] = torch.empty(0, device=dev)
+    return t
+
+
 def _tsig(t):
     return (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), str(t.device), t.dtype)
 
@@ -580,9 +591,9 @@ class RenderViews(torch.autograd.Function):
             check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
                                       ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
                                       _lib.stream_handle(dev)))
-        ctx.save_for_backward(v, f, vcol if vcol is not None else torch.empty(0, device=dev), views, cc, ws,
-                              vn if vn is not None else torch.empty(0, device=dev),
-                              raw if raw is not None else torch.empty(0, device=dev), vptr, vadj)
+        e0 = _empty0(dev)
+        ctx.save_for_backward(v, f, vcol if vcol is not None else e0, views, cc, ws, vn if vn is not None else e0,
+                              raw if raw is not None else e0, vptr, vadj)
         ctx.cfg, ctx.tex, ctx.has_vcol, ctx.pose_cv, ctx.ranges = cfg, tex, vcolors is not None, pose_cv, ranges
         ctx.slot = slot
         outs = [x for x in (depth, sil, rgb) if x is not None]

@@ -500,7 +500,7 @@ def _empty0(dev):
 
 
 def _tsig(t):
-    return (t.data_ptr(), t._version, tuple(t.shape), tuple(t.stride()), str(t.device), t.dtype)
+    return (t.data_ptr(), t._version, t.shape, t.stride(), t.device, t.dtype)
 
 
 def _shade_sig(cfg):

@@ -78,7 +78,7 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
         * the nearest fragment's Phong colour or the background, alpha = 1 where a face covers the
         * pixel; gradients reach the colour of the nearest fragment only */
        MR_OUT_HARD = 8,
-       /* mr_render_backward[_opencv] only: the forward workspace's face-gradient rows are as the
+       /* mr_render_backward[_opencv] only: the forward workspace's per-face gradient totals are as the
         * forward left them (cleared), i.e. this is the first backward over that forward; the
         * backward then skips clearing them. Leave it unset for any later backward over the same
         * forward workspace (e.g. autograd retain_graph). */
@@ -97,8 +97,9 @@ enum { MR_OUT_DEPTH = 1, MR_OUT_SIL = 2, MR_OUT_RGB = 4,
        MR_SREC_SLOT_SHIFT = 8,
        /* mr_shade_fragments_* only: every pixel's empty slots (pix_to_face = -1) follow its filled
         * ones, as mr_rasterize_meshes[_world] (and PyTorch3D's rasterizer) write them; the kernels
-        * then stop at a pixel's first empty slot instead of reading all K (same results) */
-       MR_FRAG_SORTED = 64 };
+        * then stop at a pixel's first empty slot instead of reading all K (same results).
+        * Bit 10 since mr_version() 5 (it was 64, the value of MR_OUT_ZBUF, before). */
+       MR_FRAG_SORTED = 1024 };
 
 /* One triangle mesh shared by all N views (Meshes.extend(N)) — or, with
  * view_face_first set, a batch of N distinct meshes (renderer.py:78-80: N OBJ files in one Meshes),

@@ -35,8 +35,9 @@ def test_all_header_symbols_exported(lib):
 
 
 def test_version_and_workspace_queries(lib):
-    assert lib.mr_version() == 4  # 2: mr_raster_settings_t gained clip_z / z_clip_value; 3: mr_mesh_t vnormals_out;
-    # 4: mr_pose_loss_* take sil_stride (RGBA slices read in place), MR_OUT_ZBUF, quaternion kernels
+    assert lib.mr_version() == 5  # 2: mr_raster_settings_t gained clip_z / z_clip_value; 3: mr_mesh_t vnormals_out;
+    # 4: mr_pose_loss_* take sil_stride (RGBA slices read in place), MR_OUT_ZBUF, quaternion kernels;
+    # 5: MR_FRAG_SORTED moved to bit 10 (it shared 64 with MR_OUT_ZBUF)
     a = lib.mr_render_workspace(64, 5856, 512, 512, 0)
     b = lib.mr_render_workspace(8, 5856, 512, 512, 0)
     assert a > b > 0
@@ -97,3 +98,26 @@ def test_world_rasterizer_validation_and_workspace(lib):
     w = lib.mr_rasterize_meshes_world_workspace(64, 5856, 512, 512, 0)
     assert w >= lib.mr_rasterize_meshes_workspace(64, 64 * 5856, 512, 512, 0) + 16 * 64
     assert ctypes.sizeof(_lib.MrPoses) == ctypes.sizeof(_lib.MrOpencvPoses) == 48
+
+
+def header_enum(names_prefix=("MR_OUT_", "MR_GRAD_", "MR_FRAG_", "MR_SREC_")):
+    src = open(os.path.join(ROOT, "include", "mi355r.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return {k: int(v) for k, v in re.findall(r"\b(MR_[A-Z_0-9]+)\s*=\s*(\d+)", src) if k.startswith(names_prefix)}
+
+
+def test_out_flags_are_distinct_bits():
+    """Every out_flags value the header publishes is its own bit, none overlaps another or the ShadeRec
+    slot field (bits MR_SREC_SLOT_SHIFT .. +1), and the Python binding uses the header's values."""
+    vals = header_enum()
+    shift = vals.pop("MR_SREC_SLOT_SHIFT")
+    assert shift == _lib.MR_SREC_SLOT_SHIFT == 8
+    slot_bits = 3 << shift
+    seen = 0
+    for name, v in vals.items():
+        assert v > 0 and v & (v - 1) == 0, (name, v)
+        assert not (v & seen), f"{name} = {v} overlaps another flag"
+        assert not (v & slot_bits), f"{name} = {v} overlaps the ShadeRec slot bits"
+        seen |= v
+        assert getattr(_lib, name) == v, name
+    assert {"MR_OUT_ZBUF", "MR_FRAG_SORTED", "MR_GRAD_ROWS_CLEARED"} <= set(vals)

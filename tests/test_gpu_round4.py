@@ -254,11 +254,11 @@ def _icosahedron():
     return v + (torch.rand(v.shape, generator=g) - 0.5) * 0.05, f
 
 
-def test_large_faces_take_pool_rows_deterministic_vs_oracle():
-    """Faces far larger than a tile (an icosahedron filling a 128x128 image: ~20 tiles per face) have their
-    gradient rows in k_bin_view's overflow pool instead of the 4 fixed slots (read from the workspace's
-    pool counter): vertex and pose gradients against the oracle within the per-entry bars, and bitwise
-    equal over two runs (the pool's allocation order varies with the atomics, the sums do not)."""
+def test_large_faces_deterministic_vs_oracle():
+    """Faces far larger than a tile (an icosahedron filling a 128x128 image: ~20 tiles per face, so each
+    face total is the sum of ~60 (record, tile) runs whose fixed-point atomics arrive in a different order
+    every run): vertex and pose gradients against the oracle within the per-entry bars, and bitwise equal
+    over two runs. (Round 4 gave such faces rows in an overflow pool; round 5 sums in fixed point.)"""
     from tests.helpers import canonical_views
     from torch_renderer_amd import kernels as Kn
 
@@ -285,21 +285,15 @@ def test_large_faces_take_pool_rows_deterministic_vs_oracle():
         cfg = Kn.ShadeConfig(H=H, W=W)
         vg, Rg, Tg = (x.to(DEV).requires_grad_(True) for x in (verts, R, T))
         out = Kn.render_views(vg, Rg, Tg, faces.to(DEV), intr.to(DEV), torch.zeros(1, 3, device=DEV), cfg)
-        ws = out["depth"].grad_fn.saved_tensors[5]
-        ctr = (ctypes.c_int32 * 8)()
-        _lib.check(_lib.load().mr_workspace_counters(_lib.ptr(ws), N, N * faces.shape[0], H, W, 0,
-                                                     ctypes.cast(ctr, ctypes.c_void_p), _lib.stream_handle(DEV)))
         ((out["depth"] * gD.to(DEV)).sum() + (out["sil"] * gS.to(DEV)).sum() + (out["rgb"] * gC.to(DEV)).sum()).backward()
         torch.cuda.synchronize()
-        return out, (vg.grad, Rg.grad, Tg.grad), ctr[7]
+        return out, (vg.grad, Rg.grad, Tg.grad)
 
-    out, g1, pool_rows = gpu()
-    print(f"[large faces] pool rows allocated: {pool_rows}")
-    assert pool_rows > 0, "no record took the overflow pool"
+    out, g1 = gpu()
     report("large faces depth", out["depth"], ref[0], rel_above_one=False, ref64=r64[0], sens=sp[0])
     report("large faces rgb", out["rgb"], ref[1], rel_above_one=False, ref64=r64[1], sens=sp[1])
     for i, nm in enumerate(("verts", "R", "T")):
         report(f"large faces grad {nm}", g1[i], ref[2 + i], ref64=r64[2 + i], sens=sp[2 + i])
-    _, g2, _ = gpu()
+    _, g2 = gpu()
     for a, b, nm in zip(g1, g2, ("verts", "R", "T")):
         assert torch.equal(a, b), f"{nm} gradient differs between two runs"

@@ -27,8 +27,8 @@ MR_OUT_HARD = 8  # hard_rgb_blend (HardPhongShader), fragment-shader path only
 MR_OUT_SIL_RGBA = 32  # silhouette as (N,H,W,4) RGBA (1, 1, 1, alpha), fused render path
 MR_OUT_ZBUF = 64  # depth output = MeshRasterizer's zbuf[..., 0] (background -1), fused render path
 MR_SREC_SLOT_SHIFT = 8  # out_flags bits 8-9: the workspace's ShadeRec slot (mr_render_reshade)
-MR_FRAG_SORTED = 64  # mr_shade_fragments_*: empty slots follow the filled ones (this library's rasterizer)
-MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its gradient rows are still clear)
+MR_FRAG_SORTED = 1024  # mr_shade_fragments_*: empty slots follow the filled ones (this library's rasterizer)
+MR_GRAD_ROWS_CLEARED = 16  # mr_render_backward: first backward over a forward (its face totals are still clear)
 
 
 class MrView(ctypes.Structure):

@@ -28,16 +28,6 @@ struct SetupParams {
   int nbcnt;
 };
 
-// Face-major slot of record rid (its MR_ROW_SLOTS gradient rows start at row MR_ROW_SLOTS * slot): a
-// shared mesh's face f has its N views' records side by side (second triangles of split faces after
-// every first one), so k_face_reduce reads a face's rows as one block; distinct meshes: the record id.
-MR_DEV int64_t rec_slot(int64_t rid, int64_t NF, int64_t F, int N) {
-  if (F == 0) return rid;
-  const int64_t q = rid >= NF ? 1 : 0, r = rid - q * NF;
-  const int64_t n = r / F, f = r - n * F;
-  return (q * F + f) * N + n;
-}
-
 // Wave-wide inclusive scans on DPP: row_shr 1/2/4/8 inside each 16-lane row, then
 // row_bcast:15 / row_bcast:31 carry row totals across rows (GFX9 DPP). Full EXEC required.
 MR_DEV int wave_incl_sum(int v) {
@@ -701,10 +691,10 @@ struct NormalsArgs {
   const int32_t* adj;
   float* vn;    // NULL: no normals to compute
   float* vraw;
-  float4* zero4;   // the fused backward's face-gradient rows, cleared here (nzero4 float4s; NULL: none)
+  float4* zero4;   // the fused backward's fixed-point face totals, cleared here (nzero4 16-B words; NULL: none)
   int64_t nzero4;
-  uint4* ztag;     // the gradient rows' slot tags, cleared here (nztag 16-B words; NULL: none)
-  int64_t nztag;
+  float4* zero4b;  // ... and their float remainder rows (nzero4b 16-B words)
+  int64_t nzero4b;
 };
 // OpenCV poses converted on the fly (mr_render_forward_opencv): element k of view n's record,
 // as k_views_from_opencv writes it (torch_renderer.py:73-80; bitwise the torch conversion).
@@ -794,7 +784,7 @@ __global__ void __launch_bounds__(256) k_bin_rect_world(SetupParams P, const flo
     if (blockIdx.x == 0 && threadIdx.x < CTR_COUNT) ctr[threadIdx.x] = 0;
     for (int64_t i = v; i < P.nbcnt; i += (int64_t)gridDim.x * blockDim.x) P.bcnt[i] = 0;
     for (int64_t i = v; i < NA.nzero4; i += (int64_t)gridDim.x * blockDim.x) NA.zero4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int64_t i = v; i < NA.nztag; i += (int64_t)gridDim.x * blockDim.x) NA.ztag[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (int64_t i = v; i < NA.nzero4b; i += (int64_t)gridDim.x * blockDim.x) NA.zero4b[i] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (NA.vn && v < NA.V) vertex_normal(verts, faces, NA.ptr, NA.adj, v, NA.vn, NA.vraw);
     return;
   }
@@ -909,11 +899,6 @@ struct ViewBinParams {
   int64_t Fs;
   int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
   int stage_cap;  // list entries of a view staged in LDS (after the histogram)
-  // fused path: overflow gradient rows (records of more than MR_ROW_SLOTS tiles) for the deterministic
-  // backward (rbase NULL: none); rtag = the pool's tags, rows_cap = its rows
-  int* rbase;
-  uint8_t* rtag;
-  int64_t rows_cap;
   // bands > 1: the records of each (view, band) listed by k_band_bucket (blist[(n B + b) bcap + e],
   // bcnt[n B + b] of them); NULL: every band reads all of the view's rectangles
   const int* blist;
@@ -929,11 +914,6 @@ MR_DEV int band_of(int ty, int TY, int B) { return ((ty + 1) * B - 1) / TY; }
 MR_DEV int rect_size(uint32_t r) {
   const int tx0 = r & 255, tx1 = (r >> 8) & 255, ty0 = (r >> 16) & 255, ty1 = r >> 24;
   return tx1 < tx0 ? 0 : (tx1 - tx0 + 1) * (ty1 - ty0 + 1);
-}
-// Pool rows of a record: its tiles when they exceed the record's fixed slots.
-MR_DEV int ovf_rows(uint32_t r) {
-  const int sz = rect_size(r);
-  return sz > MR_ROW_SLOTS ? sz : 0;
 }
 
 // Band lists for the banded per-view binning of one shared mesh: every record of view n (one thread per
@@ -992,9 +972,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   __shared__ int part[16];
   __shared__ int part4[4][16];
   __shared__ long long base[3];
-  __shared__ int rows_base;
   __shared__ int nmulti;
-  __shared__ int any_ovf;  // a record of this workgroup needs pool rows
   __shared__ int multi_slot[MR_SCAN_MULTI];
   const int blk = blockIdx.x, t = threadIdx.x;
   const int B = P.bands;
@@ -1018,10 +996,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int vcount = (int)(P.view_count ? (P.view_count[n] < 0x7fffffffll ? P.view_count[n] : 0x7fffffffll) : P.F);
   const int HS = (Tb + (Tb >> 6) + 3) & ~3;  // the histogram's ints (padded)
   for (int i = t; i < HS; i += 1024) hist[i] = 0;
-  if (t == 0) {
-    nmulti = 0;
-    any_ovf = 0;
-  }
+  if (t == 0) nmulti = 0;
   lds_barrier();
   const int nq = P.clipz ? 2 : 1;
   // the entries this workgroup bins: the view's records (both triangles of a split face per entry), or
@@ -1055,9 +1030,6 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
         rr[k][q] = (q < nq && i < vcount) ? P.rects[rid_[k][q]] : MR_RECT_NONE;
       }
   };
-  // the entry's record is this workgroup's to allocate pool rows for: with band lists the band holding
-  // the record's first tile row, else chunk slot k's band k % bands
-  auto owns = [&](int k, uint32_t r) { return lists ? band_of((int)((r >> 16) & 255), P.TY, B) == b : k % B == b; };
   // count
 #pragma unroll 1
   for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
@@ -1065,10 +1037,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
 #pragma unroll
     for (int k = 0; k < MR_VIEW_RPT; ++k)
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
-        if (P.rbase && ovf_rows(rr[k][q]) > 0 && owns(k, rr[k][q])) any_ovf = 1;
-      }
+      for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
   }
   lds_barrier();
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
@@ -1082,26 +1051,14 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     my_u += cc == 0 ? 0 : mo ? 1 : (cc + MR_UE - 1) / MR_UE;
     my_s += cc > 0 ? 1 : 0;
   }
-  // a view of one chunk (rectangles still in registers): its overflow gradient rows are counted here too,
-  // a fourth scan and allocation beside the list / unit / slot ones (see the rows block below)
+  // a view of one chunk keeps its rectangles in registers for the fill
   const bool one = nent <= 1024 * MR_VIEW_RPT;
-  int rows_mine = 0;
-  const bool rows = P.rbase && any_ovf;  // (most views: no record exceeds its fixed row slots)
-  if (rows && one) {
-#pragma unroll
-    for (int k = 0; k < MR_VIEW_RPT; ++k)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) rows_mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
-  }
-  int sc_in[4] = {le, my_u, my_s, rows_mine}, sc_incl[4], sc_tot[4];
+  int sc_in[4] = {le, my_u, my_s, 0}, sc_incl[4], sc_tot[4];
   block_incl_sum4(sc_in, part4, sc_incl, sc_tot);
   const int te = sc_tot[0], au = sc_tot[1], as = sc_tot[2];
   const int ex0 = sc_incl[0] - le, iu = sc_incl[1], is = sc_incl[2];
-  const int rows_incl = sc_incl[3], rows_tot = sc_tot[3];
   // the allocations from separate waves: their round trips overlap instead of queueing
-  if (t == 192 && rows && one) {
-    rows_base = rows_tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], rows_tot) : 0;
-  } else if (t == 0) {
+  if (t == 0) {
     base[0] = atomicAdd(&P.ctr[CTR_UNITS], au);
   } else if (t == 64) {
     // slot range of (view, band): the R/T reduction walks a view's bands in order
@@ -1184,46 +1141,5 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   lds_barrier();
   for (int i = t; i < lst; i += 1024)
     if (vb + i < P.list_cap) P.list[vb + i] = stage[i];
-  if (rows) {
-    // Overflow gradient rows (fused render path): a record of more than MR_ROW_SLOTS tiles gets
-    // consecutive pool rows, its k-th tile (row-major inside the rectangle) at rbase[rid] + k (the
-    // others use their fixed slots); the backward writes the row of every (record, tile) it shades and
-    // k_face_reduce sums a face's rows in a fixed order (deterministic vertex gradients, no float
-    // atomics). The records of chunk slot k belong to band k % bands; one pool allocation per
-    // workgroup and chunk (a view of one chunk: made with the list allocations above, none when no
-    // record overflows); the allocated rows' tags are cleared here. Done last, after the list stores:
-    // between the scan and the fill these few scattered stores cost the binning 6 us, here 4
-    // (profiles/r4w_pool_ab.txt).
-#pragma unroll 1
-    for (int i0 = 0; i0 < nent; i0 += 1024 * MR_VIEW_RPT) {
-      int mine = rows_mine, incl = rows_incl, tot = rows_tot;
-      if (!one) {
-        load_chunk(i0);
-        mine = 0;
-#pragma unroll
-        for (int k = 0; k < MR_VIEW_RPT; ++k)
-#pragma unroll
-          for (int q = 0; q < 2; ++q) mine += owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;
-        incl = block_incl_sum<true>(mine, part, tot);
-        if (t == 0) rows_base = tot > 0 ? atomicAdd(&P.ctr[CTR_ROWS], tot) : 0;
-        lds_barrier();
-      }
-      const long long wb = rows_base;
-      for (int i = t; i < tot; i += 1024)
-        if (wb + i < P.rows_cap) P.rtag[wb + i] = 0;
-      long long rb = wb + incl - mine;
-#pragma unroll
-      for (int k = 0; k < MR_VIEW_RPT; ++k)
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int sz = owns(k, rr[k][q]) ? ovf_rows(rr[k][q]) : 0;  // (0 for entries past the end)
-          if (sz > 0) {
-            P.rbase[rid_[k][q]] = rb + sz <= P.rows_cap ? (int)rb : -1;  // -1: pool full (atomics)
-            rb += sz;
-          }
-        }
-      if (!one) lds_barrier();  // rows_base is rewritten by the next chunk
-    }
-  }
 }
 __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P) { bin_view_body(P); }

@@ -362,17 +362,13 @@ struct RenderBwdParams {
   const ClipRec* crec;
   float zc;      // z_clip_value (clipped records only)
   const ViewRec* views;
-  float* gface;  // (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows] (float atomics: the
-                 // count -> scan path, and records whose rows did not fit)
+  // per-face gradient totals (F, ACC): 9 position rows, 9 normal rows [, 9 vertex-colour rows], in
+  // fixed point (gfix, 64-bit integer atomics: order-independent, deterministic) plus the float
+  // remainder gface of the rare component >= MR_FIX_MAX
+  unsigned long long* gfix;
+  float* gface;
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
   const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
-  // deterministic face gradients (rtag NULL: float atomics into gface): a record's fixed rows at
-  // MR_ROW_SLOTS * rec_slot(rid) + k, or (more than MR_ROW_SLOTS tiles) pool rows ovf0 + rbase[rid] + k
-  const int* rbase;
-  const uint32_t* rects;
-  uint8_t* rtag;
-  float* rrows;
-  int64_t ovf0;
 };
 
 // Order the 64 pixels of a slot by winning record (groups in order of first appearance, pixels of a
@@ -401,13 +397,11 @@ MR_DEV int sort_slot_pixels(int& f, int lane, int* lperm) {
   return src;
 }
 
-// seg_stage for the row path: key = record id (runs are whole (tile, record) groups after
-// sort_slot_pixels), q = the run's gradient row (-1: float atomics into gface row `face`), qf = the
-// record's slot-0 tag when q is a pool row (-1 otherwise). The run totals are staged in LDS with their
-// row / face; the row's tag is set by the emitting lane.
+// seg_stage for the fused backward: key = record id (runs are whole (tile, record) groups after
+// sort_slot_pixels), face = the record's face (the accumulator row every view's records add into).
+// The run totals are staged in LDS with their face.
 template <int ACC>
-MR_DEV int seg_stage_rows(int key, int face, int q, int qf, float (&v)[ACC], float* lrow, int* lkey, int* lq,
-                          uint8_t* __restrict__ rtag) {
+MR_DEV int seg_stage_face(int key, int face, float (&v)[ACC], float* lrow, int* lkey) {
   const int lane = threadIdx.x & 63;
   const int prev = dpp_wave_shr1(key, -2);
   const bool head = lane == 0 || key != prev;
@@ -444,20 +438,19 @@ MR_DEV int seg_stage_rows(int key, int face, int q, int qf, float (&v)[ACC], flo
   if (emit) {
     const int slot = __popcll(m & ((1ull << lane) - 1ull));
     lkey[slot] = face;
-    lq[slot] = q;
-    if (q >= 0) rtag[q] = 1;
-    if (qf >= 0) rtag[qf] = 2;  // the record's rows are in the pool (its slot 0 says so)
 #pragma unroll
     for (int i = 0; i < ACC; ++i) lrow[slot * ACC + i] = v[i];
   }
   wave_lds_sync();
   return __popcll(m);
 }
-// seg_flush for the row path: plain stores of whole rows (every component: the rows are not
-// cleared), float atomics for the runs without a row. Straight-line, as seg_flush.
+// seg_flush for the fused backward: each nonzero run component is added into its face's fixed-point
+// total with a 64-bit integer atomic (order-independent: the totals are deterministic), lanes covering
+// consecutive components of consecutive runs; a component of magnitude >= MR_FIX_MAX takes a float
+// atomic into the face's float row. Straight-line, as seg_flush.
 template <int ACC>
-MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__ gface, const float* lrow,
-                           const int* lkey, const int* lq) {
+MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* __restrict__ gface, const float* lrow,
+                          const int* lkey) {
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int tot = nt * ACC;
@@ -469,9 +462,12 @@ MR_DEV void seg_flush_rows(int nt, float* __restrict__ rows, float* __restrict__
       const int j = 64 * i + lane;
       if (j < tot) {
         const float x = lrow[j];
-        const int q = lq[r];
-        if (q >= 0) rows[(int64_t)q * MR_ROW_STRIDE(ACC) + c] = x;
-        else if (x != 0.0f) atomicAdd(gface + ((uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c), x);
+        const uint32_t e = (uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c;
+        if (fabsf(x) < MR_FIX_MAX) {
+          if (x != 0.0f) atomicAdd(gfix + e, (unsigned long long)fix_of(x));
+        } else {
+          atomicAdd(gface + e, x);
+        }
       }
     }
     c += m;
@@ -501,16 +497,12 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // phi copies wait on the load right away, which defeats the prefetch.
 __device__ float g_zero4[4];
 MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
-                             float4& fr, uint32_t& rect) {
+                             float4& fr) {
   int n, px, py;
   slot_pixel(P, gt, lane, n, px, py);
   const int64_t pix = n * (int64_t)P.H * P.W + (int64_t)py * P.W + px;
   r = load_rec(P.recs, f < 0 ? 0 : f);
   fr = P.frec[(int64_t)slot * 64 + lane];
-  // the record's tile rectangle (its row slots); the pool base rbase is read only for the rare record of
-  // more than MR_ROW_SLOTS tiles, where the row is computed
-  const uint32_t* pt = P.rtag ? P.rects + (f < 0 ? 0 : f) : (const uint32_t*)g_zero4;
-  rect = *pt;
   const float* pD = P.gD ? P.gD + pix : g_zero4;
   const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
   const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
@@ -581,7 +573,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   const RenderBwdParams& P = P0;
   __shared__ float lrow[4][64 * ACC];
   __shared__ int lkey[4][64];
-  __shared__ int lq[4][64];
   __shared__ int lperm[4][64];
   __shared__ float4 lrec[4][MR_BWD_REC][64];
   const bool lut = stage_tex_lut(P.S);  // the u8 texture table in LDS
@@ -607,10 +598,9 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   FaceRec r_c;
   float g_c[5];
   float4 fr_c;
-  uint32_t rect_c;
   // lane -> tile pixel p_c of the slot in flight (pixels grouped by record, sort_slot_pixels)
   int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
-  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rect_c);
+  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev = 0.0f;
   for (; s < send; s += G) {
@@ -618,7 +608,6 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c, p = p_c;
     const FaceRec r = r_c;
     const float4 frag = fr_c;
-    const uint32_t rect = rect_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
@@ -626,7 +615,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     f_c = f_n;
     sl_c = sl_n;
     p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
-    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c, rect_c);
+    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
     sc = min(s + 2 * G, slast);
     sl_n = sc;
     gt_n = P.stile[sc + lz];
@@ -686,7 +675,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
-      seg_flush_rows<ACC>(nt_prev, P.rrows, P.gface, lrow[wave], lkey[wave], lq[wave]);
+      seg_flush_fix<ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
       if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -729,202 +718,13 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         }
       }
     }
-    // the run's gradient row: tile (tx, ty) is the k-th of the record's rectangle (row-major), its row
-    // the record's slot row k (rectangles of <= MR_ROW_SLOTS tiles) or pool row rbase + k; -1 (float
-    // atomics) without rows, when the pool was full, or for a tile outside the rectangle (not expected:
-    // a winning pixel lies inside the record's padded bbox)
-    int q = -1, qf = -1;
-    if (P.rtag && f >= 0) {
-      const int t = gt - n * P.T;
-      const int ty = t / P.TX, tx = t - ty * P.TX;
-      const int rx0 = rect & 255, rx1 = (rect >> 8) & 255, ry0 = (rect >> 16) & 255, ry1 = rect >> 24;
-      if (tx >= rx0 && tx <= rx1 && ty >= ry0 && ty <= ry1) {
-        const int k = (ty - ry0) * (rx1 - rx0 + 1) + (tx - rx0);
-        const int slot0 = MR_ROW_SLOTS * (int)(P.F ? ((f >= P.NF ? P.F : 0) + face) * P.N + n : f);
-        if ((rx1 - rx0 + 1) * (ry1 - ry0 + 1) <= MR_ROW_SLOTS) {
-          q = slot0 + k;
-        } else if (P.rbase) {
-          const int rbo = P.rbase[f];
-          if (rbo >= 0) {
-            q = (int)P.ovf0 + rbo + k;
-            qf = slot0;
-          }
-        }
-      }
-    }
-    nt_prev = seg_stage_rows<ACC>(f >= 0 ? f : -1, key, q, qf, row, lrow[wave], lkey[wave], lq[wave], P.rtag);
+    nt_prev = seg_stage_face<ACC>(f >= 0 ? f : -1, key, row, lrow[wave], lkey[wave]);
     rt_prev = rt_partial(gR, gT, lane);
     s_prev = s;
   }
   if (nt_prev >= 0) {
-    seg_flush_rows<ACC>(nt_prev, P.rrows, P.gface, lrow[wave], lkey[wave], lq[wave]);
+    seg_flush_fix<ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
     if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
-  }
-}
-
-// Deterministic per-face gradient rows: face f's total = the sum, in a fixed order, of the rows the
-// backward tagged for its records (view by view, tile by tile) plus whatever the backward had to add
-// with float atomics (gatom: rows of records without a row, zero otherwise). A face's fixed row slots
-// are one block (rec_slot: N views x MR_ROW_SLOTS tiles, second triangles in a second block) whose tag
-// bytes are contiguous. G lanes per face (the views rounded up to a power of two, at most 32) take its
-// views in batches of 4G: the 4G tag words are loaded together (lane j: views j, j + G, j + 2G, j + 3G),
-// the tagged fixed-slot rows are compacted in LDS and dealt round-robin to the G lanes (four loads in
-// flight), and each lane then walks the pool rows of its records whose slot 0 holds 2 (eight tag bytes at
-// a time). The G partial sums are added by a fixed DPP tree inside each 16-lane row (G = 16) or a fixed
-// xor-shuffle tree. Two faces per wave at 64 views (G = 32; one wave per face, G = 64, measured slower).
-// Workgroups are dispatched round-robin over the 8 XCDs: block b takes
-// faces from XCD-contiguous ranges.
-template <int ACC>
-__global__ void __launch_bounds__(256) k_face_reduce(int64_t F, int N, int64_t F_shared, int64_t NF, int clip, int G,
-                                                     int64_t ovf0, const int* __restrict__ rbase,
-                                                     const uint32_t* __restrict__ rects, const uint8_t* __restrict__ rtag,
-                                                     const float* __restrict__ rows, const float* __restrict__ gatom,
-                                                     float* __restrict__ gout) {
-  static_assert(MR_ROW_SLOTS == 4, "one 32-bit tag word per record");
-  constexpr int RS = MR_ROW_STRIDE(ACC);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int fpb = 256 / G;  // faces per workgroup
-  const int parts = (gridDim.x & 7) == 0 ? 8 : 1;
-  const int per = (int)gridDim.x / parts;
-  const int64_t blk = (int64_t)(blockIdx.x % parts) * per + blockIdx.x / parts;
-  const int64_t f = blk * fpb + (int64_t)((wave * 64 + lane) / G);
-  const int j = lane & (G - 1);
-  float acc[ACC];
-#pragma unroll
-  for (int i = 0; i < ACC; ++i) acc[i] = 0.0f;
-  const int nv = F_shared ? N : 1;
-  auto add4 = [&](const float4 (&x4)[RS / 4]) {
-    const float* x = (const float*)x4;
-#pragma unroll
-    for (int i = 0; i < ACC; ++i) acc[i] += x[i];
-  };
-  auto load4 = [&](int64_t row, float4 (&x4)[RS / 4]) {
-    const float4* src = (const float4*)(rows + row * RS);
-#pragma unroll
-    for (int i = 0; i < RS / 4; ++i) x4[i] = src[i];
-  };
-  // the tagged rows of pool mask m in bit order (bit b: row base + b), four loads in flight
-  auto walk = [&](uint32_t m, int64_t base) {
-#pragma unroll 1
-    while (m) {
-      int k[4];
-      bool v[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = m != 0u;
-        k[i] = v[i] ? __builtin_ctz(m) : k[0];
-        m &= m - 1u;
-      }
-      float4 x[4][RS / 4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) load4(base + k[i], x[i]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (v[i]) add4(x[i]);
-    }
-  };
-  // A face's tagged fixed-slot rows of one batch of 4G views, compacted in LDS in a fixed order (lane
-  // j's views j, j + G, j + 2G, j + 3G, tiles ascending, lanes in order) and dealt round-robin to its G
-  // lanes: every lane of a face loads about the same number of rows (per-view lanes waited on the
-  // face's most covered views).
-  __shared__ uint16_t lst[256 * 16];
-  uint16_t* my = lst + ((wave * 64 + lane) / G) * 16 * G;
-#ifndef MR_FR_INFL
-#define MR_FR_INFL 4
-#endif
-  constexpr int INFL = ACC == 27 ? 4 : MR_FR_INFL;  // rows in flight per lane
-  for (int q = 0; q <= clip; ++q) {
-    // the face's record in view 0: its rec_slot (the views' records follow)
-    const int64_t r0 = F_shared ? (q * F_shared + f) * N : (q ? NF : 0) + f;
-#pragma unroll 1
-    for (int nb = 0; nb < nv; nb += 4 * G) {
-      uint32_t tw[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int n = nb + j + u * G;
-        tw[u] = f < F && n < nv ? ((const uint32_t*)rtag)[r0 + n] : 0u;
-      }
-      // the pool records among the four (slot 0 tagged 2): their pool base and size
-      int rb[4], sz[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        rb[u] = sz[u] = 0;
-        if ((tw[u] & 255u) == 2u) {
-          const int64_t rid = (q ? NF : 0) + (F_shared ? (int64_t)(nb + j + u * G) * F_shared : 0) + f;
-          rb[u] = rbase[rid];
-          sz[u] = rect_size(rects[rid]);
-        }
-      }
-      // bit 4u + k: view nb + j + uG, tile k
-      uint32_t m = 0;
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int k = 0; k < 4; ++k) m |= (((tw[u] >> (8 * k)) & 255u) == 1u ? 1u : 0u) << (4 * u + k);
-      const int c = __builtin_popcount(m);
-      int x = c;  // inclusive scan of the counts over the face's G lanes
-      for (int o = 1; o < G; o <<= 1) {
-        const int t = __shfl_up(x, o, G);
-        if (j >= o) x += t;
-      }
-      const int tot = __shfl(x, G - 1, G);
-      for (int o = x - c; m; m &= m - 1u, ++o) {
-        const int b = __builtin_ctz(m);
-        my[o] = (uint16_t)((j + (b >> 2) * G) * MR_ROW_SLOTS + (b & 3));
-      }
-      __syncthreads();
-      const int64_t R0 = (r0 + nb) * MR_ROW_SLOTS;
-#pragma unroll 1
-      for (int i0 = j; i0 < tot; i0 += INFL * G) {
-        int e[INFL];
-        bool v[INFL];
-#pragma unroll
-        for (int t = 0; t < INFL; ++t) {
-          v[t] = i0 + t * G < tot;
-          e[t] = my[v[t] ? i0 + t * G : i0];
-        }
-        float4 xr[INFL][RS / 4];
-#pragma unroll
-        for (int t = 0; t < INFL; ++t) load4(R0 + e[t], xr[t]);
-#pragma unroll
-        for (int t = 0; t < INFL; ++t)
-          if (v[t]) add4(xr[t]);
-      }
-      __syncthreads();
-      // then this lane's pool records' rows, eight tag bytes at a time
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-#pragma unroll 1
-        for (int k0 = 0; k0 < sz[u]; k0 += 8) {
-          const int64_t base = ovf0 + rb[u] + k0;
-          uint32_t pm = 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) pm |= (k0 + k < sz[u] && rtag[base + k] ? 1u : 0u) << k;
-          walk(pm, base);
-        }
-      }
-    }
-  }
-  // the G partial sums of each face: a fixed DPP tree inside the 16-lane row (G = 16), else a fixed xor tree
-  if (G == 16) {
-#pragma unroll
-    for (int i = 0; i < ACC; ++i) {
-      float v = acc[i];
-      v += dppf<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
-      v += dppf<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
-      v += dppf<0x141, 0xf>(v);  // row_half_mirror
-      v += dppf<0x140, 0xf>(v);  // row_mirror
-      acc[i] = v;
-    }
-  } else {
-    for (int o = 1; o < G; o <<= 1) {
-#pragma unroll
-      for (int i = 0; i < ACC; ++i) acc[i] += __shfl_xor(acc[i], o, 64);
-    }
-  }
-  if (j == 0 && f < F) {
-#pragma unroll
-    for (int i = 0; i < ACC; ++i) gout[f * ACC + i] = acc[i] + gatom[f * ACC + i];
   }
 }
 

@@ -30,6 +30,21 @@ MR_DEV float fexp(float x) { return __builtin_amdgcn_exp2f(x * 1.442695040888963
 // a^b for a >= 0 (a = 0 -> 0 for b > 0, the only use: Phong's specular power)
 MR_DEV float fpow(float a, float b) { return a > 0.0f ? __builtin_amdgcn_exp2f(b * __builtin_amdgcn_logf(a)) : (b == 0.0f ? 1.0f : 0.0f); }
 
+// Fixed-point gradient accumulation (the fused backward's per-face totals): a value is stored as the
+// two's-complement integer round(x * 2^MR_FIX_SHIFT) and summed with 64-bit integer atomics. Integer
+// addition is associative, so a total is the same bits whatever order the addends arrive in
+// (deterministic without a fixed-order reduction pass); wrap-around in intermediate sums cancels, so
+// only the final total must lie within +-2^(63 - MR_FIX_SHIFT). Resolution 2^-32 = 2.3e-10 absolute,
+// far below the 1e-4 bar; an addend of magnitude >= MR_FIX_MAX takes a float atomic instead.
+#define MR_FIX_SHIFT 32
+#define MR_FIX_MAX 1073741824.0f  // 2^30: |x| * 2^32 < 2^62
+MR_DEV long long fix_of(float x) { return __float2ll_rn(x * 4294967296.0f); }
+MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)v * (1.0 / 4294967296.0)); }
+// Per-face total component i: the fixed-point sum plus the float-atomic remainder.
+MR_DEV float fix_total(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i) {
+  return gfix ? fix_to_f(gfix[i]) + gflt[i] : gflt[i];
+}
+
 // std::max/std::min semantics (a < b ? b : a) — NaN handling follows the CPU code.
 MR_DEV float smax(float a, float b) { return (a < b) ? b : a; }
 MR_DEV float smin(float a, float b) { return (b < a) ? b : a; }

@@ -48,7 +48,7 @@ extern "C" {
 const char* mr_last_error(void) { return g_err; }
 
 
-int32_t mr_version(void) { return 4; }
+int32_t mr_version(void) { return 5; }
 
 int32_t mr_struct_size(int32_t which) {
   switch (which) {
@@ -188,16 +188,6 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.srec = Pf ? (ShadeRec*)Pf->srec : w.srec;  // the call's ShadeRec slot
     V.Fs = F;
     sb = ceil_div(F, 1024);
-    // the fused render path: pool rows of the records too large for their fixed gradient-row slots
-#ifdef MR_EXP_NOPOOL  // experiment builds only: no pool (records of > 4 tiles take float atomics)
-    if (false) {
-#else
-    if (rows_fit(w)) {
-#endif
-      V.rbase = w.rbase;
-      V.rtag = w.rtag + w.ovf0;
-      V.rows_cap = w.ovf_cap;
-    }
   }
   V.nsrec_wg = (int)sb;
   V.T = g.T; V.TX = g.TX; V.TY = g.TY; V.mfpb = g.mfpb; V.clipz = SP.clipz;
@@ -787,12 +777,12 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     NA.V = m->V; NA.ptr = m->vadj_ptr; NA.adj = m->vadj;
     NA.vn = vb ? m->vnormals_out : nullptr;
     NA.vraw = m->vraw_out;
-    NA.zero4 = (float4*)w.grows;
-    NA.nzero4 = (27 * m->F + 3) / 4;
-    if (rows_fit(w)) {  // the gradient rows' slot tags (second triangles' too when clipping), 256-B aligned
-      NA.ztag = (uint4*)w.rtag;
-      NA.nztag = (int64_t)MR_ROW_SLOTS * NF * (SP.clipz ? 2 : 1) / 16 + 1;
-    }
+    // the backward's face totals (ACC components per face: the backward's ACC for this mesh)
+    const int64_t nacc = (int64_t)(m->tex_kind == 1 ? 27 : 18) * m->F;
+    NA.zero4 = (float4*)w.gfix;
+    NA.nzero4 = (nacc + 1) / 2;
+    NA.zero4b = (float4*)w.gflt;
+    NA.nzero4b = (nacc + 3) / 4;
     const int64_t bx = std::max<int64_t>(ceil_div(maxvf, 256), ceil_div(m->V, 256));
     dim3 rgrid((unsigned)(bx > 0 ? bx : 1), (unsigned)N + 1);  // row 0: normals + counter clear
     if (SP.clipz) MR_TIMED(KID_BIN_RECT, st, (k_bin_rect_world<true><<<rgrid, 256, 0, st>>>(SP, m->verts, m->faces, m->F, (const ViewRec*)views, NA, w.ctr, C, FragBg{})));
@@ -805,7 +795,8 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     if ((rc = launch_bin_view<1, 3>(SP, w, g, N, m->view_face_first, m->view_face_count, m->F, false, st, &P.S, &P))) return rc;
     return launch_raster_and_shade<1, 3>(P, g, N, st, s->clip_z != 0);
   }
-  if (hipMemsetAsync(w.grows, 0, sizeof(float) * 27 * (size_t)m->F, st) != hipSuccess)
+  if (hipMemsetAsync(w.gfix, 0, sizeof(unsigned long long) * 27 * (size_t)m->F, st) != hipSuccess ||
+      hipMemsetAsync(w.gflt, 0, sizeof(float) * 27 * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   if (C.R) {  // count -> scan path: the view records first
     k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C.R, C.sR, C.t, C.sT, C.intr, C.sI, N, C.out);
@@ -900,7 +891,6 @@ size_t mr_render_backward_workspace(int64_t N, int64_t V, int64_t F, int32_t H, 
   const int64_t NT = N * (int64_t)ceil_div(W, MR_TS) * ceil_div(H, MR_TS);
   size_t off = align_up(sizeof(float) * 3 * (size_t)V, 256);                   // gnu
   off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);                  // rt_part
-  off = align_up(off + sizeof(float) * 27 * (size_t)(F > 0 ? F : 1), 256);     // per-face gradient totals
   return off;
 }
 
@@ -959,14 +949,14 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   float* gnu = (float*)(b + off);
   off = align_up(off + sizeof(float) * 3 * (size_t)m->V, 256);
   float* rt_part = (float*)(b + off);
-  off = align_up(off + sizeof(float) * 12 * (size_t)NT, 256);
-  float* gtot = (float*)(b + off);  // per-face totals (k_face_reduce) read by the vertex gathers
-  // float-atomic face rows (records without gradient rows) live in the forward's workspace, which
-  // the forward cleared; a second backward over the same forward (MR_GRAD_ROWS_CLEARED not set)
-  // clears them again
-  float* gface = w.grows;
+  // the per-face totals (fixed point + float remainder) live in the forward's workspace, which the
+  // forward cleared; a second backward over the same forward (MR_GRAD_ROWS_CLEARED not set) clears
+  // them again
+  unsigned long long* gfix = w.gfix;
+  float* gface = w.gflt;
   if (!(sp->out_flags & MR_GRAD_ROWS_CLEARED) &&
-      hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess)
+      (hipMemsetAsync(gfix, 0, sizeof(unsigned long long) * ACC * (size_t)m->F, st) != hipSuccess ||
+       hipMemsetAsync(gface, 0, sizeof(float) * ACC * (size_t)m->F, st) != hipSuccess))
     return set_err(MR_ELAUNCH, "memset failed");
   RenderBwdParams P;
   memset(&P, 0, sizeof(P));
@@ -990,21 +980,10 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.crec = w.crec;
   P.zc = s->z_clip_value;
   P.views = (const ViewRec*)views;
+  P.gfix = gfix;
   P.gface = gface;
   P.rt_part = rt_part;
   P.frec = w.frec;
-  // per-(record, tile) gradient rows: fixed slots (tags cleared by k_bin_rect_world) and the pool the
-  // per-view binning (k_bin_view) allocates; the count -> scan path has none (float atomics into gface)
-  const bool vpath = view_binning(g, N, NF) && rows_fit(w);
-  if (vpath) {
-#ifndef MR_EXP_NOPOOL
-    P.rbase = w.rbase;
-#endif
-    P.rects = w.rects;
-    P.rtag = w.rtag;
-    P.rrows = w.rrows;
-    P.ovf0 = w.ovf0;
-  }
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
@@ -1022,36 +1001,18 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false><<<cap(f18), 256, 0, st>>>(P)));
   }
   MR_CHECK_LAUNCH("k_bwd_fused");
-  {
-    const int clip = s->clip_z ? 1 : 0;
-    const int64_t Fs = multi ? 0 : m->F;
-    int G = 1;  // lanes per face: the views of one face, rounded up to a power of two (<= 32; 16: face
-                // reduction 23.5 -> 21.3 us at 64 views, 64: 23.0, profiles/r4y_face_lanes_ab.txt)
-#ifndef MR_FR_GMAX
-#define MR_FR_GMAX 32
-#endif
-    while (G < MR_FR_GMAX && G < (multi ? 1 : (int)N)) G <<= 1;
-    int nb = ceil_div(m->F, 256 / G);
-    nb = (nb + 7) / 8 * 8;  // XCD-contiguous face ranges (k_face_reduce)
-    if (vpath) {
-      if (vcol) MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<27><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.ovf0, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
-      else MR_TIMED(KID_FACE_REDUCE, st, (k_face_reduce<18><<<nb, 256, 0, st>>>(m->F, (int)N, Fs, NF, clip, G, w.ovf0, w.rbase, w.rects, w.rtag, w.rrows, gface, gtot)));
-      MR_CHECK_LAUNCH("k_face_reduce");
-      gface = gtot;
-    }
-  }
   const int use_n = sp->light_kind == 0;
   const int vb = ceil_div(m->V * MR_VL, 256);
   // the forward's slot ranges: one per (view, band) on the per-view binning, one per view otherwise
   const int bands = view_binning(g, N, NF) ? bin_bands(N, g) : 1;
   if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv)));
-  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
-  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu)));
+  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
-    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, gnu, use_n, gverts, gcol)));
   } else {
-    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, gverts, gcol)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");
   return MR_OK;
@@ -1159,12 +1120,12 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   const int use_n = sp->light_kind == 0 && !P.sil;
   const int vb = ceil_div(m->V * MR_VL, 256);
   if (use_n) {
-    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
-    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, gface, vraw, gnu);
+    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, vraw, gnu);
+    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, vraw, gnu);
     MR_CHECK_LAUNCH("k_rt_vgrad_a");
   }
-  if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, g_verts, g_vcolors);
-  else k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gface, gnu, use_n, g_verts, g_vcolors);
+  if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, gnu, use_n, g_verts, g_vcolors);
+  else k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, gnu, use_n, g_verts, g_vcolors);
   MR_CHECK_LAUNCH("k_vgrad_b");
   return MR_OK;
 }

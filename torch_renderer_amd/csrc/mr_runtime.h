@@ -39,7 +39,7 @@ static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bi
                                               "k_vertex_normals", "k_project_faces", "k_project_faces_bwd",
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
                                               "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero",
-                                              "k_bin_rect", "k_bin_view", "k_face_reduce", "k_band_bucket"};
+                                              "k_bin_rect", "k_bin_view", "k_face_reduce(unused)", "k_band_bucket"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;
@@ -87,8 +87,7 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
 // ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)
 // ctr[CTR_ZWALK]: tiles the K-deep raster walked near-to-far (its depth-ordered list walk)
-// ctr[CTR_ROWS]: per-(record, tile) gradient rows allocated by the per-view binning (fused path)
-enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_ZWALK = 6, CTR_ROWS = 7,
+enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_ZWALK = 6,
        CTR_COUNT = 8 };
 
 struct BinGeom {
@@ -154,20 +153,16 @@ struct RasterWS {
   unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
   int* sface;  // (N*T*64) per slot, per tile pixel (row-major 8x8): winning face record or -1
   ShadeRec* srec;  // (F) per-face shading inputs (fused path; F = faces of the shared mesh)
-  float* grows;    // (F, 27) the fused backward's per-face gradient rows, cleared by the forward
+  // (F, 27) u64 + (F, 27) f32: the fused backward's per-face gradient totals, cleared by the forward.
+  // Fixed point (MR_FIX_SHIFT fractional bits, two's complement) summed with 64-bit integer atomics:
+  // integer addition is associative, so the totals do not depend on the order the backward's waves
+  // add their per-(record, tile) runs in — bitwise deterministic vertex gradients with one launch
+  // fewer than a fixed-order reduction of stored rows (round 4). The f32 rows take the rare run
+  // component of magnitude >= 2^30 that does not fit the fixed-point range (float atomics).
+  unsigned long long* gfix;
+  float* gflt;
   float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
-  // fused path, deterministic face gradients: the backward writes one gradient row per (record, tile)
-  // it shades (plain stores, no float atomics), k_face_reduce sums each face's rows in a fixed order.
-  // Rows: MR_ROW_SLOTS fixed slots per record, face-major (rec_slot: a face's records of all views
-  // side by side, so the reduction reads each face's rows as one contiguous block), for records of
-  // <= MR_ROW_SLOTS tiles; the rest (larger faces) take rows from an overflow pool allocated by k_bin_view.
-  int* rbase;      // (2 * Ftot) overflow records: first pool row of their tile rectangle (-1: pool full)
-  uint8_t* rtag;   // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) 1 = the backward wrote the row; a record's slot 0 holds
-                   // 2 when its rows are in the pool. Slot tags cleared by k_bin_rect_world (its normals row), pool tags by k_bin_view
-  float* rrows;    // (MR_ROW_SLOTS * 2 Ftot + ovf_cap) rows of MR_ROW_STRIDE(acc) floats
-  int64_t ovf0;    // first pool row (= MR_ROW_SLOTS * 2 Ftot)
-  int64_t ovf_cap; // pool rows
   // banded per-view binning of one shared mesh (bands > 1): each (view, band)'s records, listed by
   // k_band_bucket (bcap = 2 Ftot / N: both triangles of every face of the view), and their counts
   // (cleared by the record launch)
@@ -177,15 +172,6 @@ struct RasterWS {
   int nbcnt;       // N * bands (0: no lists)
   size_t bytes;
 };
-// Gradient rows of `acc` floats are stored 16-B aligned (stride MR_ROW_STRIDE(acc) floats: whole float4
-// loads in k_face_reduce). MR_ROW_SLOTS = 4 fixed rows per record cover a face's 1, 2 (straddling a tile
-// edge) or 4 (a tile corner) tiles; the overflow pool holds list_cap / 2 rows (room for one screen-filling
-// face per view besides ~3 Ftot entries), past which rows fall back to float atomics.
-#define MR_ROW_STRIDE(acc) ((acc) == 27 ? 28 : 20)
-#ifndef MR_ROW_SLOTS
-#define MR_ROW_SLOTS 4
-#endif
-static int64_t row_ovf_cap(const BinGeom& g) { return g.list_cap / 2; }
 static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int W, const BinGeom& g,
                                 int64_t Fshade = 0) {
   (void)H; (void)W;
@@ -225,21 +211,14 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * 64 * NT, 256);
   w.srec = (ShadeRec*)(b + off);  // MR_SREC_SLOTS slots of Fshade records (mr_render_reshade)
   off = align_up(off + sizeof(ShadeRec) * MR_SREC_SLOTS * (size_t)Fshade, 256);
-  w.grows = (float*)(b + off);
+  w.gfix = (unsigned long long*)(b + off);
+  off = align_up(off + sizeof(unsigned long long) * 27 * (size_t)Fshade, 256);
+  w.gflt = (float*)(b + off);
   off = align_up(off + sizeof(float) * 27 * (size_t)Fshade, 256);
   w.frec = (float4*)(b + off);
   off = align_up(off + sizeof(float4) * (Fshade > 0 ? 64 * NT : 0), 256);
   w.crec = (ClipRec*)(b + off);
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
-  w.rbase = (int*)(b + off);
-  off = align_up(off + (Fshade > 0 ? sizeof(int) * 2 * (size_t)(Ftot > 0 ? Ftot : 1) : 0), 256);
-  w.ovf0 = (int64_t)MR_ROW_SLOTS * 2 * (Ftot > 0 ? Ftot : 1);
-  w.ovf_cap = row_ovf_cap(g);
-  const size_t nrows = Fshade > 0 ? (size_t)(w.ovf0 + w.ovf_cap) : 0;
-  w.rtag = (uint8_t*)(b + off);
-  off = align_up(off + nrows, 256);
-  w.rrows = (float*)(b + off);
-  off = align_up(off + sizeof(float) * MR_ROW_STRIDE(27) * nrows, 256);
   const int B = bin_bands(N, g);
   w.nbcnt = B > 1 ? (int)(N * B) : 0;
   w.bcap = B > 1 ? 2 * ((Ftot > 0 ? Ftot : 1) + N - 1) / N : 0;
@@ -249,15 +228,6 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * (size_t)w.nbcnt * (size_t)w.bcap, 256);
   w.bytes = off;
   return w;
-}
-// The fused path's gradient rows are addressed with 32-bit row numbers (else: float atomics).
-static bool rows_fit(const RasterWS& w) {
-#ifdef MR_EXP_NOROWS  // experiment builds only: float atomics (the round-3 backward) for A/B
-  (void)w;
-  return false;
-#else
-  return w.ovf0 + w.ovf_cap < (1ll << 31) - 1;
-#endif
 }
 // Bytes to clear from w.ctr before a forward: the counters and, on the count -> scan path, the
 // per-tile counts and per-view totals.

@@ -54,11 +54,23 @@ def global_view_offset(n_total, rank=None, world_size=None):
 
 
 def allreduce_grads(params, group=None):
-    """Sum the .grad of replicated parameters over ranks in ONE flattened all_reduce."""
+    """Sum the .grad of replicated parameters over ranks in ONE flattened all_reduce.
+
+    Every rank must call the same collective with a buffer of the same size, whatever it rendered: a
+    rank with an empty view shard (``shard_range`` hands them out when there are fewer views than
+    ranks) or a parameter its views did not reach has ``.grad`` None. Such a gradient is materialised as
+    zeros here, so the flattened buffer always holds every gradient-requiring parameter of ``params`` in
+    list order (the list is the same replicated parameters on every rank)."""
     _, w = world()
-    grads = [p.grad for p in params if p is not None and p.grad is not None]
-    if w == 1 or not grads:
+    if w == 1:
         return
+    live = [p for p in params if p is not None and p.requires_grad]
+    if not live:
+        return
+    for p in live:
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
+    grads = [p.grad for p in live]
     if len(grads) == 1 and grads[0].is_contiguous():  # one bucket already: reduce in place (no copies)
         dist.all_reduce(grads[0], op=dist.ReduceOp.SUM, group=group)
         return

@@ -1,4 +1,4 @@
-"""Summarise an interleaved A/B (tools/gpu_ab_r4.sh outputs) into one text table.
+"""Summarise an interleaved A/B (tools/gpu_ab.sh outputs) into one text table.
 python tools/ab_summary.py TAG > profiles/<TAG>_ab.txt"""
 import glob
 import json

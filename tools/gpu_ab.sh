@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of experiment builds (exp/<name>.so) on the render bench, interleaved: base, v1, v2, ..., repeated twice.
-# usage: tools/gpu_ab_r4.sh TAG MODEARGS variant...   (MODEARGS e.g. "--mode fragments")
+# usage: tools/gpu_ab.sh TAG MODEARGS variant...   (MODEARGS e.g. "--mode fragments")
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp

@@ -1,13 +1,13 @@
 #!/bin/bash
-# Round-4 evidence session: GPU parity tests, smoke, every bench line (render with its fragment_pass and CPU
+# Evidence session (tag $1): GPU parity tests, smoke, every bench line (render with its fragment_pass and CPU
 # baseline, fragments, soft, pose, C4 gather, C5), rocprofv3 kernel stats of each, the 2-rank rehearsal.
 # PMC passes: tools/pmc_profile.sh (separate call).
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-TAG=${1:-r4z}
-timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/pytest_${TAG}.log 2>&1
+TAG=${1:-ev}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v -s --timeout 300 --timeout-method thread > gpurun_out/pytest_${TAG}.log 2>&1
 rc=$?
 grep -E "passed|failed" gpurun_out/pytest_${TAG}.log | tail -2
 grep -E "^(FAILED|ERROR)" gpurun_out/pytest_${TAG}.log | head -20

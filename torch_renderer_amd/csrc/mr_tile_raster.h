@@ -172,32 +172,9 @@ MR_DEV bool pair_keep(const FaceRec* __restrict__ recs, int64_t NF, int id, cons
                       float pad, float blur, bool persp, bool clipb, int& cid, float& pz);
 // The pixels of one lane's tile rectangle for a split face's triangle (k_tile_raster, rare path;
 // out of line so that its registers do not weigh on the pixel-pair loop).
-// A wave's staged face records (one per entry lane). MR_STAGE_AOS: records of 16-B words padded to 80 B
-// (5 float4; record m's words on banks 20 m + 4 c mod 64, so records up to 16 apart never share a bank)
-// read with 4 ds_read_b128 instead of 16 ds_read_b32; else structure-of-arrays (field i of record m at
-// rec[i][m]).
-#ifndef MR_STAGE_AOS
-#define MR_STAGE_AOS 0
-#endif
-#if MR_STAGE_AOS
-struct StageRecs {
-  float4 w[64][5];
-};
-MR_DEV void stage_rec_put(StageRecs& S, int lane, const FaceRec& r) {
-  float4 q[4];
-  __builtin_memcpy(q, &r, sizeof(q));
-#pragma unroll
-  for (int i = 0; i < 4; ++i) S.w[lane][i] = q[i];
-}
-MR_DEV FaceRec stage_rec_get(const StageRecs& S, int m) {
-  float4 q[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) q[i] = S.w[m][i];
-  FaceRec r;
-  __builtin_memcpy(&r, q, sizeof(q));
-  return r;
-}
-#else
+// A wave's staged face records (one per entry lane), structure-of-arrays: field i of record m at
+// rec[i][m]. (Measured against 80-B padded array-of-structures records read with ds_read_b128: no gain,
+// profiles/r4f_bands_ab.txt.)
 struct StageRecs {
   float rec[16][64];
 };
@@ -213,7 +190,6 @@ MR_DEV FaceRec stage_rec_get(const StageRecs& S, int m) {
   for (int i = 0; i < 16; ++i) f[i] = S.rec[i][m];
   return r;
 }
-#endif
 __attribute__((noinline)) __device__ void raster_pair_rect(const FaceRec* __restrict__ recs, int64_t NF,
                                                            const StageRecs& srec, const int* sid, const float* xs,
                                                            const float* ys, unsigned long long* key, int lane,

@@ -199,7 +199,8 @@ def test_c3_three_calls_share_one_raster():
 
     H = W = 256
     N = 6
-    meshes = load_asset("cow", device=DEV).extend(N)
+    base = load_asset("cow", device=DEV)
+    v0, f0 = base.shared_verts().detach(), base.shared_faces()
     cams = FoVPerspectiveCameras(device=DEV)
     blend = BlendParams(sigma=1e-4, gamma=1e-4, background_color=(0, 0, 0))
     rs = RasterizationSettings(image_size=H, blur_radius=0.0, faces_per_pixel=1)
@@ -218,6 +219,10 @@ def test_c3_three_calls_share_one_raster():
         Kn._RESHADE["enabled"] = enabled
         Kn._RESHADE["entry"] = None
         try:
+            # the shared vertices require grad too: three backwards accumulate into the one workspace's
+            # face totals (the first over the forward's clear, the later ones clear them again)
+            v = v0.clone().requires_grad_(True)
+            meshes = Meshes([v], [f0], base.textures).extend(N)
             q = q0.clone().requires_grad_(True)
             R = quaternion_to_matrix(q[:, 3:])
             T = q[:, :3]
@@ -229,7 +234,7 @@ def test_c3_three_calls_share_one_raster():
             color = phong(meshes, R=R, T=T)[..., :3]
             ((depth * gd).sum() + (sil * gs).sum() + (color * gc).sum()).backward()
             torch.cuda.synchronize()
-            return (depth.detach(), sil.detach(), color.detach(), q.grad.detach().clone()), reused_after_sil
+            return (depth.detach(), sil.detach(), color.detach(), q.grad.detach().clone(), v.grad.clone()), reused_after_sil
         finally:
             Kn._RESHADE["enabled"] = True
             Kn._RESHADE["entry"] = None
@@ -238,7 +243,8 @@ def test_c3_three_calls_share_one_raster():
     indep, served_off = step(False)
     print(f"[reshade] shadings served by the first raster: {served} (disabled: {served_off})")
     assert served == 2 and served_off == 1
-    for nm, a, b in zip(("depth", "silhouette", "colour", "pose grad"), shared, indep):
+    assert shared[4].abs().max() > 0
+    for nm, a, b in zip(("depth", "silhouette", "colour", "pose grad", "vertex grad"), shared, indep):
         assert torch.equal(a, b), f"{nm} differs between the shared raster and three passes"
 
 

@@ -1,0 +1,103 @@
+"""Round-5 GPU checks:
+
+* The lazy K = 1 Fragments of MeshRasterizer (camera_pose_optimizer.py:244-246) use what the call saw:
+  a zbuf first read inside a no_grad block still carries the call's autograd graph, and an in-place
+  vertex edit between the call and the first read raises instead of rasterizing the edited mesh.
+* The reshade entry (one raster shared by the zbuf / silhouette / Phong calls of one step) never pins a
+  workspace: after an inference render whose outputs are discarded the workspace is freed.
+* Fixed-point face totals: the vertex gradient of a batch is bitwise the same whatever the view order
+  inside the batch (the integer sums are order-independent; the per-view R / T gradients permute with
+  the views).
+"""
+import gc
+
+import pytest
+import torch
+
+from torch_renderer_amd import kernels as Kn
+from torch_renderer_amd.assets import load_asset
+from torch_renderer_amd.cameras import FoVPerspectiveCameras
+from torch_renderer_amd.mesh_renderer import MeshRasterizer, RasterizationSettings, _LazyFragments
+from torch_renderer_amd.structures import Meshes
+from torch_renderer_amd.transforms import look_at_view_transform
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _cow_views(N, dist=0.7):
+    base = load_asset("cow", device=DEV, textures=False)
+    v0, f0 = base.shared_verts().detach(), base.shared_faces()
+    R, T = look_at_view_transform(dist, torch.linspace(5, 60, N), torch.linspace(0, 330, N), device=DEV,
+                                  at=(v0.mean(0).tolist(),))
+    return v0, f0, R, T
+
+
+def test_lazy_fragments_capture_call_state():
+    N, H = 3, 96
+    v0, f0, R, T = _cow_views(N)
+    rast = MeshRasterizer(cameras=FoVPerspectiveCameras(device=DEV),
+                          raster_settings=RasterizationSettings(image_size=H, faces_per_pixel=1))
+    v = v0.clone().requires_grad_(True)
+    frags = rast(meshes_world=Meshes([v], [f0]).extend(N), R=R, T=T)
+    assert isinstance(frags, _LazyFragments)
+    with torch.no_grad():
+        z = frags.zbuf  # first read under no_grad: the call ran with grad enabled
+    assert z.requires_grad and z.grad_fn is not None
+    torch.relu(z[..., 0]).sum().backward()
+    assert v.grad is not None and v.grad.abs().sum() > 0
+    v2 = v0.clone()
+    frags2 = rast(meshes_world=Meshes([v2], [f0]).extend(N), R=R, T=T)
+    v2.add_(0.01)  # in place, before the first access
+    with pytest.raises(RuntimeError, match="modified in place"):
+        _ = frags2.zbuf
+
+
+def test_reshade_entry_does_not_pin_the_workspace():
+    N, H = 4, 128
+    v0, f0, R, T = _cow_views(N)
+    cfg = Kn.ShadeConfig(H=H, W=H)
+    cc = torch.zeros(1, 3, device=DEV)
+    intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
+    Kn._RESHADE["entry"] = None
+    with torch.no_grad():
+        Kn.render_views(v0, R, T, f0, intr, cc, cfg)
+    gc.collect()
+    ent = Kn._RESHADE["entry"]
+    assert ent is not None and ent["ws"]() is None, "an inference render pinned its workspace"
+    # with a graph alive the workspace stays reachable (and reusable) until the backward
+    v = v0.clone().requires_grad_(True)
+    out = Kn.render_views(v, R, T, f0, intr, cc, cfg)
+    ent = Kn._RESHADE["entry"]
+    assert ent["ws"]() is not None
+    out["depth"].sum().backward()
+    assert Kn._RESHADE["entry"] is None
+    Kn._RESHADE["entry"] = None
+
+
+def test_vertex_grad_independent_of_view_order():
+    N, H = 16, 192
+    v0, f0, R, T = _cow_views(N, dist=0.6)
+    intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
+    cfg = Kn.ShadeConfig(H=H, W=H)
+    cc = torch.zeros(1, 3, device=DEV)
+    g = torch.Generator().manual_seed(3)
+    gD, gS, gC = (torch.rand(N, H, H, generator=g).to(DEV) - 0.5, torch.rand(N, H, H, generator=g).to(DEV) - 0.5,
+                  torch.rand(N, H, H, 3, generator=g).to(DEV) - 0.5)
+    perm = torch.randperm(N, generator=g).to(DEV)
+
+    def run(p):
+        v = v0.clone().requires_grad_(True)
+        Rp, Tp = R[p].clone().requires_grad_(True), T[p].clone().requires_grad_(True)
+        Kn._RESHADE["entry"] = None
+        out = Kn.render_views(v, Rp, Tp, f0, intr, cc, cfg)
+        ((out["depth"] * gD[p]).sum() + (out["sil"] * gS[p]).sum() + (out["rgb"] * gC[p]).sum()).backward()
+        torch.cuda.synchronize()
+        return v.grad, Rp.grad, Tp.grad
+
+    ident = torch.arange(N, device=DEV)
+    va, Ra, Ta = run(ident)
+    vb, Rb, Tb = run(perm)
+    print(f"[determinism] vertex grad under a view permutation: max |diff| = {(va - vb).abs().max().item():.3e}")
+    assert torch.equal(va, vb)
+    assert torch.equal(Ra[perm], Rb) and torch.equal(Ta[perm], Tb)

@@ -485,6 +485,10 @@ def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol, ranges=None):
 # with the same geometry but a different shading only re-shades (mr_render_reshade: no projection, binning
 # or rasterization). An entry serves each shading configuration once (a repeated identical call — a
 # benchmark loop, a second step — rasterizes again) and ends when a backward over its workspace starts.
+# The workspace is held by a weak reference: the forward's autograd node keeps it alive while a backward
+# can still run; an inference render (no_grad, nothing requiring grad, discarded outputs) lets it go, so
+# the entry never pins a workspace. The key includes the launch stream (a reshade on another stream would
+# read the workspace unordered).
 _RESHADE = {"entry": None, "enabled": True}
 
 
@@ -507,9 +511,9 @@ def _shade_sig(cfg):
     return cfg.key()
 
 
-def _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges):
+def _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream):
     return (_tsig(v), _tsig(f), _tsig(R), _tsig(T), _tsig(intr), cfg.H, cfg.W, cfg.persp, cfg.blur, cfg.clip, cfg.cull,
-            cfg.max_faces_per_bin, cfg.z_clip, bool(pose_cv), ranges is None)
+            cfg.max_faces_per_bin, cfg.z_clip, bool(pose_cv), ranges is None, stream)
 
 
 class RenderViews(torch.autograd.Function):
@@ -560,21 +564,26 @@ class RenderViews(torch.autograd.Function):
         p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
         wsq = L.mr_render_workspace_meshes if ranges is not None else L.mr_render_workspace
         wsb = _ws_size(wsq, N, f.shape[0], H, W, rs.max_faces_per_bin)
-        geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges)
+        stream = _lib.stream_handle(dev)
+        geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream)
         ent = _RESHADE["entry"]
         ssig = _shade_sig(cfg)
-        reuse = (_RESHADE["enabled"] and ent is not None and ent["geom"] == geom and ssig not in ent["served"] and
-                 len(ent["served"]) < 4 and not cfg.want_p2f)
+        ws = None
+        if (_RESHADE["enabled"] and ent is not None and ent["geom"] == geom and ssig not in ent["served"] and
+                len(ent["served"]) < 4 and not cfg.want_p2f):
+            ws = ent["ws"]()  # None once the workspace's last autograd node is gone
+        reuse = ws is not None
         if reuse:  # same raster, another shading: the entry's workspace and view records, a new ShadeRec slot
-            ws, views = ent["ws"], ent["views"]
+            views = ent["views"]
             slot = len(ent["served"])
             ent["served"].add(ssig)
             sp.out_flags |= slot << _lib.MR_SREC_SLOT_SHIFT
         else:
             ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
             slot = 0
-            # the entry holds the geometry tensors: their storage cannot be reused while it lives
-            _RESHADE["entry"] = {"geom": geom, "refs": (v, f, R, T, intr), "ws": ws, "views": views,
+            # the entry holds the (small) geometry tensors, so their storage cannot be reused while it lives,
+            # and the workspace only weakly
+            _RESHADE["entry"] = {"geom": geom, "refs": (v, f, R, T, intr), "ws": weakref.ref(ws), "views": views,
                                  "served": {ssig}}
         global _LAST_RENDER
         nrec = f.shape[0] if ranges is not None else N * f.shape[0]
@@ -582,15 +591,15 @@ class RenderViews(torch.autograd.Function):
         if reuse:
             check(L.mr_render_reshade(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
                                       ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
-                                      _lib.stream_handle(dev)))
+                                      stream))
         elif poses is not None:
             check(L.mr_render_forward_opencv(ctypes.byref(mesh), ctypes.byref(poses), ptr(views), N, ptr(cc),
                                              cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(depth), ptr(sil),
-                                             ptr(rgb), ptr(p2f), ptr(ws), wsb, _lib.stream_handle(dev)))
+                                             ptr(rgb), ptr(p2f), ptr(ws), wsb, stream))
         else:
             check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
                                       ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
-                                      _lib.stream_handle(dev)))
+                                      stream))
         e0 = _empty0(dev)
         ctx.save_for_backward(v, f, vcol if vcol is not None else e0, views, cc, ws, vn if vn is not None else e0,
                               raw if raw is not None else e0, vptr, vadj)
@@ -630,9 +639,9 @@ class RenderViews(torch.autograd.Function):
                           (0 if gC is not None else _lib.MR_OUT_RGB))
         sp.out_flags |= ctx.slot << _lib.MR_SREC_SLOT_SHIFT  # the ShadeRecs this node's forward packed
         ent = _RESHADE["entry"]
-        if ent is not None and ent["ws"] is ws:  # a backward over the workspace ends its reuse
+        if ent is not None and ent["ws"]() is ws:  # a backward over the workspace ends its reuse
             _RESHADE["entry"] = None
-        if not getattr(ws, "_mr_rows_used", False):  # the forward cleared the float-atomic face rows in ws
+        if not getattr(ws, "_mr_rows_used", False):  # the forward cleared the face-gradient totals in ws
             sp.out_flags |= _lib.MR_GRAD_ROWS_CLEARED
             ws._mr_rows_used = True
         gverts = torch.empty_like(v)

@@ -331,24 +331,41 @@ class MeshRasterizer(torch.nn.Module):
             zc = _z_clip_value(cameras, rs)
             from .kernels import _require_cuda
 
-            _require_cuda(meshes.shared_verts(), meshes.shared_faces(), R, T)  # fail at the call, not at first use
+            # what the call sees is captured now (the fields may be computed later, on first access): the
+            # vertex / face tensors, their versions and the grad mode, as upstream's eager rasterizer
+            # would have used them at this call
+            verts, faces = meshes.shared_verts(), meshes.shared_faces()
+            _require_cuda(verts, faces, R, T)  # fail at the call, not at first use
+            grad_mode = torch.is_grad_enabled()
+            versions = (verts._version, faces._version)
+
+            def _check_unchanged():
+                if (verts._version, faces._version) != versions:
+                    raise RuntimeError("MeshRasterizer: the mesh's verts / faces were modified in place between the "
+                                       "rasterizer call and the first access of its Fragments")
 
             def full():
-                return RasterizeMeshesWorld.apply(
-                    meshes.shared_verts(), R, T, meshes.shared_faces(), intr, R.shape[0], H, W,
-                    int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
-                    rs.max_faces_per_bin, zc)
+                _check_unchanged()
+                with torch.set_grad_enabled(grad_mode):
+                    return RasterizeMeshesWorld.apply(
+                        verts, R, T, faces, intr, R.shape[0], H, W,
+                        int(rs.faces_per_pixel), float(rs.blur_radius), persp, clip, bool(rs.cull_backfaces),
+                        rs.max_faces_per_bin, zc)
 
             if int(rs.faces_per_pixel) == 1 and float(rs.blur_radius) == 0.0:
                 def zbuf_only():  # the fused render in zbuf mode (see _LazyFragments)
                     from .kernels import render_views
 
+                    _check_unchanged()
                     cfg = ShadeConfig(H=H, W=W, persp=persp, clip=clip, cull=bool(rs.cull_backfaces),
                                       max_faces_per_bin=rs.max_faces_per_bin, light_kind=1, want_depth=True,
                                       want_sil=False, want_rgb=False, zbuf=True, z_clip=zc)
                     cc = torch.zeros((1, 3), device=R.device)
-                    return render_views(meshes.shared_verts(), R, T, meshes.shared_faces(), intr, cc,
-                                        cfg)["depth"].unsqueeze(-1)
+                    try:
+                        with torch.set_grad_enabled(grad_mode):
+                            return render_views(verts, R, T, faces, intr, cc, cfg)["depth"].unsqueeze(-1)
+                    except NotImplementedError:  # MR_EUNSUPPORTED from the fused path: the modular rasterizer
+                        return full()[1]
 
                 return _LazyFragments(zbuf_only, full)
             p2f, zbuf, bary, dists = full()

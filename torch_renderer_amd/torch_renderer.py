@@ -47,12 +47,14 @@ _UNION_CACHE = {}
 def _union_topology(meshes: Meshes):
     """(faces (F,3) int64 of the union, view_face_first (N+1), view_face_count (N) int64 device
     tensors, largest face count, view_vert_first (N+1), largest vertex count) of a batch of distinct
-    meshes, cached on the identity and version of the faces tensors (the union faces tensor keeps
-    its identity, so its CSR stays cached too). The entry holds the source tensors themselves and is
-    matched by `is`, so a garbage-collected batch cannot hand its ids to a new one."""
+    meshes, cached on the identity and version of the faces tensors and the identity and vertex count
+    of the verts tensors — not their version: the union depends on faces and vertex counts only, so an
+    in-place vertex update (an optimiser step on distinct meshes' verts) keeps the entry, and with it
+    the union faces tensor's identity and its cached CSR. The entry holds the source tensors themselves
+    and is matched by `is`, so a garbage-collected batch cannot hand its ids to a new one."""
     fl, vl = meshes.faces_list(), meshes.verts_list()
     hit = _UNION_CACHE.get(id(meshes))
-    if hit is not None and _same_sources(hit[0], fl, vl):
+    if hit is not None and _same_sources(hit[0], fl, vl, b_values=False):
         return hit[1]
     voff, out = 0, []
     for v, f in zip(vl, fl):
@@ -70,19 +72,21 @@ def _union_topology(meshes: Meshes):
            torch.tensor(vfirst, dtype=torch.int64, device=dev), max(vcounts))
     if len(_UNION_CACHE) > 16:
         _UNION_CACHE.clear()
-    _UNION_CACHE[id(meshes)] = (_sources(fl, vl), res)
+    _UNION_CACHE[id(meshes)] = (_sources(fl, vl, b_values=False), res)
     return res
 
 
-def _sources(al, bl):
-    """Cache-entry record of two tensor lists: the tensors (kept alive) and their versions."""
-    return tuple((a, a._version, b, b._version) for a, b in zip(al, bl)), len(al)
+def _sources(al, bl, b_values=True):
+    """Cache-entry record of two tensor lists: the tensors (kept alive) and their versions (for the
+    second list with b_values=False, its leading size instead: only its shape matters)."""
+    return tuple((a, a._version, b, b._version if b_values else b.shape[0]) for a, b in zip(al, bl)), len(al)
 
 
-def _same_sources(rec, al, bl):
+def _same_sources(rec, al, bl, b_values=True):
     entries, n = rec
-    return n == len(al) == len(bl) and all(a is a0 and a._version == va and b is b0 and b._version == vb
-                                           for (a0, va, b0, vb), a, b in zip(entries, al, bl))
+    return n == len(al) == len(bl) and all(
+        a is a0 and a._version == va and b is b0 and (b._version if b_values else b.shape[0]) == vb
+        for (a0, va, b0, vb), a, b in zip(entries, al, bl))
 
 
 def union_texture_args(meshes: Meshes, need_color: bool):

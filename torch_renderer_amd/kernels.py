@@ -565,7 +565,7 @@ class RenderViews(torch.autograd.Function):
         wsq = L.mr_render_workspace_meshes if ranges is not None else L.mr_render_workspace
         wsb = _ws_size(wsq, N, f.shape[0], H, W, rs.max_faces_per_bin)
         stream = _lib.stream_handle(dev)
-        geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream)
+        geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream.value)
         ent = _RESHADE["entry"]
         ssig = _shade_sig(cfg)
         ws = None

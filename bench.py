@@ -169,6 +169,8 @@ def main():
     ap.add_argument("--no-fragment-pass", action="store_true",
                     help="render mode: skip the fragment-pass measurement that follows the headline step")
     ap.add_argument("--cpu-views", type=int, default=2)
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="render mode: skip the C3 / C5 / soft steps that follow the headline (A/B runs)")
     ap.add_argument("--eager", action="store_true",
                     help="enqueue every step from Python instead of replaying one captured HIP graph")
     ap.add_argument("--texture", choices=("uv", "white"), default="uv",
@@ -380,6 +382,7 @@ def main():
     if not args.no_fragment_pass:
         f_el, f_kt, f_cov, _ = measure_fragments(args, dev, world, rank)
         frag = fragment_pass_summary(args, f_el, f_kt, f_cov, Fn, world)
+    secondary = {} if args.no_secondary else secondary_steps(args, dev, world, rank)
 
     if rank != 0:
         dist.destroy_process_group()
@@ -434,7 +437,8 @@ def main():
                                "depth+silhouette+Phong RGB from one raster pass, grads to verts and per-view R,t",
                    "mesh": args.mesh, "H": H, "W": W, "views_per_gpu": nv, "global_views": nv * world,
                    "parallelism": f"view-sharded x{world}"},
-        "roofline": roof, "fragment_pass": frag, "forward_roofline": fwd_roof, "path_roofline": path_roof,
+        "roofline": roof, "fragment_pass": frag, **secondary,
+        "forward_roofline": fwd_roof, "path_roofline": path_roof,
         "cpu_baseline": cpu,
         "work": wstats, "kernels": kernels,
         "allreduce_us": None if allreduce_us is None else round(allreduce_us, 2),
@@ -486,6 +490,7 @@ def measure_fragments(args, dev, world, rank):
         for _ in range(args.warmup):
             out = step()
         del out
+        _host_profile(step, dev)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -522,7 +527,19 @@ def measure_fragments(args, dev, world, rank):
             del out
         torch.cuda.synchronize()
         pass_us = sum(a.elapsed_time(b) for a, b in evs) / len(evs) * 1e3
+        # host cost of one call: the time step() takes to return (no synchronisation inside the loop; the
+        # device queue absorbs the launches as long as it is not full)
+        hs = []
+        for _ in range(min(args.steps, 20)):
+            h0 = time.perf_counter()
+            out = step()
+            hs.append(time.perf_counter() - h0)
+            del out
+        torch.cuda.synchronize()
+        hs.sort()
+        host_us = hs[len(hs) // 2] * 1e6
     kt["__pass_us__"] = (1, pass_us / 1e3)
+    kt["__host_us__"] = (1, host_us / 1e3)
     return elapsed, kt, covered, Fn
 
 
@@ -534,6 +551,7 @@ def fragment_pass_summary(args, elapsed, kt, covered, Fn, world):
     value = nv * world * args.steps / elapsed
     per_frame = 28 * H * W + 36 * Fn
     pass_us = kt.pop("__pass_us__")[1] * 1e3
+    host_us = kt.pop("__host_us__", (1, float("nan")))[1] * 1e3
     us = sum(kt[k][1] / kt[k][0] * 1e3 for k in FRAG_KERNELS if k in kt)
     ach = per_frame * nv / (pass_us * 1e-6) / 1e9
     ach_k = per_frame * nv / (us * 1e-6) / 1e9
@@ -544,7 +562,7 @@ def fragment_pass_summary(args, elapsed, kt, covered, Fn, world):
             # frac: algorithmic bytes / the pass's device time (one HIP event pair around the pass's launches);
             # kernel_sum_frac: / the sum of its kernels' times with an event pair around each kernel;
             # step_frac: / the timed step's wall time (host launch work included)
-            "pass_us": round(pass_us, 2), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "pass_us": round(pass_us, 2), "host_us_per_call": round(host_us, 1), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_step": round(us, 2), "kernel_sum_frac": round(ach_k / HBM_PEAK_GBS, 4),
             "step_frac": round(value * per_frame / 1e9 / HBM_PEAK_GBS, 4),
@@ -584,7 +602,7 @@ def bench_fragments(args, dev, world, rank):
         dist.destroy_process_group()
 
 
-def bench_soft(args, dev, world, rank):
+def bench_soft(args, dev, world, rank, embed=False):
     """Soft rasterization: the silhouette renderer of deform_mesh_with_color.py:
     153-165 — MeshRenderer(MeshRasterizer(faces_per_pixel=50, blur_radius=ln(1/1e-4 - 1)·1e-4,
     perspective_correct=False), SoftSilhouetteShader) on the normalised cow (:106-111), PerspectiveCameras
@@ -646,13 +664,8 @@ def bench_soft(args, dev, world, rank):
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
-    _lib.timing_enable(True)
-    for _ in range(min(args.steps, 10)):
-        step()
-    torch.cuda.synchronize()
-    kt = _lib.timing_read()
-    _lib.timing_enable(False)
-    if rank != 0:
+    kt = _kernel_times(step, min(args.steps, 10))
+    if rank != 0 and not embed:
         dist.destroy_process_group()
         return
     value = nv * world * args.steps / elapsed
@@ -668,6 +681,10 @@ def bench_soft(args, dev, world, rank):
             "us_per_step": round(us, 2), "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "step_kernels_us": round(sum(v[1] / max(v[0], 1) * 1e3 for v in kt.values()), 2)}
+    if embed:
+        return _embedded(value, elapsed, args, kt, min(args.steps, 10), roof,
+                         f"{args.mesh} (F={Fn}) normalised, {H}x{W}, {nv} views/GPU, K={K}, soft silhouette fwd+bwd "
+                         "(deform_mesh_with_color.py:153-165)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = soft_cpu_baseline(verts, faces, R, T, H, W, K, rs.blur_radius, sigma, target,
@@ -708,6 +725,34 @@ def _time_steps(step, args, dev, world):
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
     return elapsed
+
+
+def _embedded(value, elapsed, args, kt, kt_steps, roof, workload):
+    """The compact object a secondary workload contributes to the default bench line: whole-job
+    frames/s and ms per step over its own timed steps, the library kernels' device time per step (HIP
+    events around every launch of kt_steps eager steps; the caller's torch kernels are not in it)."""
+    dev_us = sum(v[1] for v in kt.values()) / max(kt_steps, 1) * 1e3
+    return {"frames_per_s": round(value, 1), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "steps": args.steps, "warmup": args.warmup, "library_kernel_us_per_step": round(dev_us, 1),
+            "roofline": roof, "workload": workload,
+            "kernels_us": {k: round(v[1] / max(v[0], 1) * 1e3, 2) for k, v in kt.items()}}
+
+
+def secondary_steps(args, dev, world, rank):
+    """C3 (pose), C5 and the K = 50 soft silhouette, each at its own workload, timed in the default run
+    so that the driver's record carries them (bench.py --mode pose / c5 / soft print their full lines)."""
+    out = {}
+    plans = (("pose_step", bench_pose, dict(size=512, views=64, steps=20, warmup=5)),
+             ("c5_step", bench_c5, dict(size=1024, views=5, steps=10, warmup=3)),
+             ("soft_step", bench_soft, dict(size=128, views=64, steps=10, warmup=3, mesh="cow")))
+    for name, fn, over in plans:
+        sub = argparse.Namespace(**{**vars(args), **over, "no_cpu_baseline": True})
+        try:
+            out[name] = fn(sub, dev, world, rank, embed=True)
+        except Exception as e:  # a secondary workload never sinks the headline line; the error is reported
+            out[name] = {"error": f"{type(e).__name__}: {e}"}
+        torch.cuda.synchronize()
+    return out
 
 
 def _kernel_times(step, n):
@@ -887,7 +932,7 @@ def pose_cpu_baseline(verts, faces, d, q0, refs, H, W, n_views=2, reps=2):
                       f"{threads} threads) + torch-CPU shading/autograd ({torch.get_num_threads()} threads)"}
 
 
-def bench_pose(args, dev, world, rank):
+def bench_pose(args, dev, world, rank, embed=False):
     """C3 as the caller runs it (camera_pose_optimizer.py:237-305), batched: --views independent pose
     problems per GPU (the cow from look_at_view_transform(0.7, elev, azim) + N(0, 0.03) noise on the
     7-vector pose), each step the caller's three calls — rasterizer(meshes_world=, R=, T=) for the
@@ -942,6 +987,22 @@ def bench_pose(args, dev, world, rank):
     elapsed = _time_steps(step, args, dev, world)
     kt = _kernel_times(step, min(args.steps, 10))
     _host_profile(step, dev)
+    # roofline of the step's largest library kernel, calc_loss fused with its gradients (k_pose_loss_fused):
+    # per pixel it reads depth 4 + silhouette RGBA 16 + colour RGBA 16 + mask 1 + depth_ref 4 + rgb_ref 12 B
+    # and writes the three gradient images 4 + 16 + 16 B (89 B)
+    roof = None
+    if "k_pose_loss_fused" in kt:
+        n_, ms_ = kt["k_pose_loss_fused"]
+        b = 89 * nv * H * W
+        us_ = ms_ / n_ * 1e3
+        roof = {"bound": "hbm", "kernel": "k_pose_loss_fused", "avg_launch_us": round(us_, 2),
+                "algorithmic_bytes_per_launch": b, "achieved": round(b / (us_ * 1e-6) / 1e9, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(b / (us_ * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "traffic": None}
+    if embed:
+        return _embedded(n_total * args.steps / elapsed, elapsed, args, kt, min(args.steps, 10), roof,
+                         f"cow (F={base.shared_faces().shape[0]}), {H}x{W}, {nv} pose problems/GPU, "
+                         "camera_pose_optimizer.py:237-305 step (3 renders, calc_loss, backward, Adam)")
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -961,14 +1022,14 @@ def bench_pose(args, dev, world, rank):
                                "camera_pose_optimizer.py step: rasterizer + silhouette + Phong renders (FoV camera, "
                                "near-plane clip), calc_loss, backward, Adam",
                    "mesh": "cow", "H": H, "W": W, "views_per_gpu": nv, "parallelism": f"view-sharded x{world}"},
-        "cpu_baseline": cpu, "kernels": kernels,
+        "roofline": roof, "cpu_baseline": cpu, "kernels": kernels,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def bench_c5(args, dev, world, rank):
+def bench_c5(args, dev, world, rank, embed=False):
     """C5 (BASELINE.json configs[4]; mesh_deformer.py:130-222 color_train) as the caller runs it: the
     F=81,920 subdivided sphere (data/sphere.obj subdivided twice), 1024x1024 (--size), PerspectiveCameras
     (NDC, focal 1) at look_at_view_transform(2, elev, azim) over 10 target views, AmbientLights,
@@ -1035,7 +1096,7 @@ def bench_c5(args, dev, world, rank):
                     lights=lights)
     wstats = render_stats()
     del keep
-    if rank != 0:
+    if rank != 0 and not embed:
         dist.destroy_process_group()
         return
     value = nper * world * args.steps / elapsed
@@ -1052,6 +1113,10 @@ def bench_c5(args, dev, world, rank):
                 "algorithmic_bytes_per_launch": b, "achieved": round(b / (f_us * 1e-6) / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(b / (f_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": None}
+    if embed:
+        return _embedded(value, elapsed, args, kt, min(args.steps, 10), roof,
+                         f"ico-sphere (F={Fn}, V={Vn}), {H}x{W}, {nper} single-view renders per step, "
+                         "mesh_deformer.py:196-215 colour step (backward to colours and positions, SGD)")
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = c5_cpu_baseline(verts0.cpu(), faces.cpu(), R.cpu(), T.cpu(), H, W)

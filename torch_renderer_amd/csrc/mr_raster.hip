@@ -1279,9 +1279,9 @@ static int32_t pose_loss_run(const PoseLossParams& P, float* total, float* terms
     MR_CHECK_LAUNCH("k_mask_count");
     k_mask_total<<<1, 256, 0, st>>>(w.mcnt, nm, w.mtot);
     MR_CHECK_LAUNCH("k_mask_total");
-    k_pose_loss_fused<true><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, g_depth, g_sil, g_rgb);
+    MR_TIMED(KID_POSE_LOSS, st, (k_pose_loss_fused<true><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, g_depth, g_sil, g_rgb)));
   } else {
-    k_pose_loss_fused<false><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, nullptr, nullptr, nullptr);
+    MR_TIMED(KID_POSE_LOSS, st, (k_pose_loss_fused<false><<<(unsigned)nb, 256, 0, st>>>(P, w.mtot, w.part, w.pcnt, nullptr, nullptr, nullptr)));
   }
   MR_CHECK_LAUNCH("k_pose_loss_fused");
   k_pose_loss_final<<<1, 1024, 0, st>>>(P, w.part, w.pcnt, (int)nb, total, terms, w.count);
@@ -1325,8 +1325,9 @@ int32_t mr_pose_loss_scale(const float* g_total, int64_t npix, int64_t sil_strid
   if (!g_total || !g_depth || !g_sil || !g_rgb) return set_err(MR_EINVAL, "NULL argument");
   if ((sil_stride != 1 && sil_stride != 4) || (rgb_stride != 3 && rgb_stride != 4))
     return set_err(MR_EINVAL, "bad strides");
-  k_pose_loss_scale<<<1024, 256, 0, (hipStream_t)stream>>>(g_total, npix, npix * sil_stride, npix * rgb_stride, g_depth,
-                                                            g_sil, g_rgb);
+  hipStream_t st = (hipStream_t)stream;
+  MR_TIMED(KID_POSE_LOSS_SCALE, st, (k_pose_loss_scale<<<1024, 256, 0, st>>>(g_total, npix, npix * sil_stride, npix * rgb_stride,
+                                                                             g_depth, g_sil, g_rgb)));
   MR_CHECK_LAUNCH("k_pose_loss_scale");
   return MR_OK;
 }

@@ -261,14 +261,10 @@ def main():
     torch.cuda.synchronize()
 
     # One step = fwd+bwd of the rank's views (+ the shared-vertex-gradient all-reduce when N > 1).
-    # Default: the fwd+bwd kernels are captured once into a HIP graph and replayed (every kernel
-    # of the step runs each replay; only the Python/launch enqueue work is removed). The
-    # collective stays outside the graph.
-    # One step = fwd+bwd of the rank's views (+ the shared-vertex-gradient all-reduce when N > 1).
-    # Default: the forward and the backward are each captured once into a HIP graph (one memory pool)
-    # and replayed (every kernel of the step runs each replay; only the Python/launch enqueue work is
-    # removed). With N > 1 the all-reduce of step k's vertex gradient runs on a side stream while step
-    # k+1's forward replays (the forward never reads verts.grad); the backward of step k+1, which
+    # Default: the step is captured into HIP graphs and replayed (every kernel of the step runs each
+    # replay; only the Python/launch enqueue work is removed): one graph at N = 1; with N > 1 the forward
+    # and the backward are two graphs (one memory pool), and the all-reduce of step k's vertex gradient
+    # runs on a side stream while step k+1's forward replays (the forward never reads verts.grad); the backward of step k+1, which
     # rewrites it, waits for the collective — so RCCL's latency hides behind the forward.
     if args.eager:
         fwd_only = bwd_only = None
@@ -283,12 +279,22 @@ def main():
         R_cv.grad = None
         t_cv.grad = None
         pool = torch.cuda.graph_pool_handle()
-        g_fwd, g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_fwd, pool=pool):
-            outs_static = renderer.render(bmesh, R_cv, t_cv)
-        with torch.cuda.graph(g_bwd, pool=pool):
-            torch.autograd.backward(list(outs_static), [gD, gS, gC], retain_graph=True)
-        fwd_only, bwd_only = g_fwd.replay, g_bwd.replay
+        if world == 1:
+            # one rank: nothing to overlap between the forward and the backward, so one graph holds the
+            # whole step (no graph-boundary gap between the two halves)
+            g_fwd = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fwd, pool=pool):
+                outs_static = renderer.render(bmesh, R_cv, t_cv)
+                torch.autograd.backward(list(outs_static), [gD, gS, gC])
+            g_bwd = None
+            fwd_only, bwd_only = g_fwd.replay, (lambda: None)
+        else:
+            g_fwd, g_bwd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_fwd, pool=pool):
+                outs_static = renderer.render(bmesh, R_cv, t_cv)
+            with torch.cuda.graph(g_bwd, pool=pool):
+                torch.autograd.backward(list(outs_static), [gD, gS, gC], retain_graph=True)
+            fwd_only, bwd_only = g_fwd.replay, g_bwd.replay
 
     comm = torch.cuda.Stream() if world > 1 else None
     ar_events = []  # (start, end) HIP events around each timed step's all_reduce (on the comm stream)
@@ -340,6 +346,15 @@ def main():
         e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = e.item()
+    # the replayed graph's gradients against an eager step's: bitwise (the step is deterministic), so
+    # the graph runs exactly the step's work
+    graph_check = None
+    if fwd_only is not None and world == 1:
+        torch.cuda.synchronize()
+        g_graph = (verts.grad.clone(), R_cv.grad.clone(), t_cv.grad.clone())
+        eager_step()
+        torch.cuda.synchronize()
+        graph_check = all(torch.equal(a, b) for a, b in zip(g_graph, (verts.grad, R_cv.grad, t_cv.grad)))
     # per-kernel device times: HIP events around every launch of a few eager steps (same kernels)
     torch.cuda.synchronize()
     _lib.timing_enable(True)
@@ -430,6 +445,7 @@ def main():
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "f32",
         "launch": "eager" if args.eager else "hipgraph",
+        "graph_grads_equal_eager": graph_check,
         "data": (f"synthetic camera poses on the reference's {args.mesh} mesh"
                  + (" + texture (assets/cow.npz from data/cow_mesh)" if "texture_u8" in d and args.texture == "uv"
                     else " (white: no texture map)")),
@@ -1091,7 +1107,8 @@ def bench_c5(args, dev, world, rank, embed=False):
     kt = _kernel_times(step, min(args.steps, 10))
     _host_profile(step, dev)
     # work counters of one view's forward (render_stats reads the live workspace)
-    norm = torch.nn.functional.hardtanh(verts_rgb, 0.0, 1.0).detach()
+    # (colours requiring grad: the autograd node holds the workspace, which an inference render would free)
+    norm = torch.nn.functional.hardtanh(verts_rgb, 0.0, 1.0).detach().requires_grad_(True)
     keep = renderer(Meshes([verts0], [faces], TexturesVertex(verts_features=norm)), cameras=target_cameras[0],
                     lights=lights)
     wstats = render_stats()

@@ -397,7 +397,9 @@ def main():
     if not args.no_fragment_pass:
         f_el, f_kt, f_cov, _ = measure_fragments(args, dev, world, rank)
         frag = fragment_pass_summary(args, f_el, f_kt, f_cov, Fn, world)
-    secondary = {} if args.no_secondary else secondary_steps(args, dev, world, rank)
+    # (one GPU only: the multi-GPU lines report the headline's scaling; a secondary workload's collective
+    # must never be able to stall a scaling run)
+    secondary = {} if args.no_secondary or world > 1 else secondary_steps(args, dev, world, rank)
 
     if rank != 0:
         dist.destroy_process_group()

@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_raster_k(FwdParams P) {
 // order: the fragments are bitwise those of the face-at-a-time kernel (deform workload: 2.22 ms
 // (two waves per tile, every face at every pixel) -> see DESIGN.md for this kernel's numbers).
 #ifndef MR_KP_BC
-#define MR_KP_BC 24
+#define MR_KP_BC 20  // 20 KB of LDS per wave with the stage and the depth-order permutation: 8 waves per CU (24: 7, 1.75 per SIMD; 1192-1206 -> 1150-1169 us at K = 50, profiles/r5m_soft_bucket_ab.txt)
 #endif
 // Shift-insert of key into the first NS positions of the ascending list q (positions >= NS are
 // empty for every lane of the wave and stay so: no lane holds more than NS keys).
@@ -144,7 +144,7 @@ MR_DEV void insert_ns(unsigned long long (&q)[KP], unsigned long long key) {
 }
 
 #ifndef MR_KP_ROOM
-#define MR_KP_ROOM 12  // drain the buckets once the fullest one has less room than this
+#define MR_KP_ROOM 8  // drain the buckets once the fullest one has less room than this (12 with 24-deep buckets; 10 -> 8: 1157-1169 -> 1125-1139 us, profiles/r5n_soft_room_ab.txt)
 #endif
 #ifndef MR_KP_SORT
 #define MR_KP_SORT 2048  // tiles of 65 .. MR_KP_SORT listed faces are walked in depth order (0: never)

@@ -880,6 +880,32 @@ def _host_profile(step, dev, n=20):
     import io
     import pstats
 
+    # autograd runs the Python backward functions on its device thread, which cProfile does not see: time
+    # every autograd.Function's forward / backward of the package with wrappers instead
+    from torch_renderer_amd import kernels as Kn, losses as Ls, transforms as Tf
+    acc = {}
+    patched = []
+    for mod in (Kn, Ls, Tf):
+        for name in dir(mod):
+            cls = getattr(mod, name)
+            if isinstance(cls, type) and issubclass(cls, torch.autograd.Function) and cls is not torch.autograd.Function:
+                for meth in ("forward", "backward"):
+                    if meth not in cls.__dict__:
+                        continue
+                    orig = cls.__dict__[meth]
+                    fn = orig.__func__ if isinstance(orig, staticmethod) else orig
+                    key = f"{name}.{meth}"
+
+                    def wrap(*a, _fn=fn, _k=key):
+                        t = time.perf_counter()
+                        try:
+                            return _fn(*a)
+                        finally:
+                            e = acc.setdefault(_k, [0, 0.0])
+                            e[0] += 1
+                            e[1] += time.perf_counter() - t
+                    setattr(cls, meth, staticmethod(wrap))
+                    patched.append((cls, meth, orig))
     pr = cProfile.Profile()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -888,8 +914,13 @@ def _host_profile(step, dev, n=20):
         step()
     pr.disable()
     torch.cuda.synchronize(dev)
+    for cls, meth, orig in patched:
+        setattr(cls, meth, orig)
     s = io.StringIO()
     s.write(f"{n} steps, {(time.perf_counter() - t0) / n * 1e3:.3f} ms/step under the profiler\n")
+    s.write("autograd.Function host time per step (forward: main thread, backward: autograd's device thread):\n")
+    for k, (c, t) in sorted(acc.items(), key=lambda kv: -kv[1][1]):
+        s.write(f"  {k:40s} {c / n:5.1f} calls/step  {t / n * 1e6:8.1f} us/step  {t / max(c, 1) * 1e6:7.1f} us/call\n")
     ps = pstats.Stats(pr, stream=s)
     ps.sort_stats("tottime").print_stats(45)
     ps.sort_stats("cumulative").print_stats(45)

@@ -264,6 +264,15 @@ int32_t mr_render_forward_opencv(const mr_mesh_t* mesh, const mr_opencv_poses_t*
                                  const mr_raster_settings_t* rs, const mr_shade_params_t* sp, float* depth,
                                  float* silhouette, float* rgb, int32_t* pix_to_face32, void* workspace,
                                  size_t workspace_bytes, void* stream);
+/* mr_render_forward for PyTorch3D-convention poses given as strided device arrays (R (N,3,3), T (N,3),
+ * intr (N,4); a batch stride of 0 broadcasts one row): the view records are packed by the forward's
+ * first launch and written to views_out (N) for mr_render_backward — no host-side packing of R, T and
+ * intr (upstream MeshRenderer(meshes, R=, T=) callers: camera_pose_optimizer.py:248-250,
+ * mesh_deformer.py:197). */
+int32_t mr_render_forward_poses(const mr_mesh_t* mesh, const mr_poses_t* poses, mr_view_t* views_out, int64_t N,
+                                const float* cam_centers, int64_t num_cam_centers, const mr_raster_settings_t* rs,
+                                const mr_shade_params_t* sp, float* depth, float* silhouette, float* rgb,
+                                int32_t* pix_to_face32, void* workspace, size_t workspace_bytes, void* stream);
 /* Backward from upstream grads (each may be NULL when not requested in out_flags).
  * Writes grad_verts (V,3), grad_views (N,12), grad_vcolors (V,3; tex_kind 1 only, may be NULL).
  * `fwd_workspace` must be the one passed to the matching mr_render_forward: its face records and

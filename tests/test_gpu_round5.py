@@ -71,8 +71,31 @@ def test_reshade_entry_does_not_pin_the_workspace():
     ent = Kn._RESHADE["entry"]
     assert ent["ws"]() is not None
     out["depth"].sum().backward()
-    assert Kn._RESHADE["entry"] is None
+    del out
+    gc.collect()
+    assert Kn._RESHADE["entry"]["ws"]() is None, "the workspace outlived its graph"
     Kn._RESHADE["entry"] = None
+
+
+def test_second_backward_over_one_forward():
+    """retain_graph: a second backward over the same forward workspace clears the face totals the first
+    one consumed (the C++ node tracks the first use; MR_GRAD_ROWS_CLEARED only on it): both backwards give
+    the same, bitwise, vertex and pose gradients."""
+    N, H = 4, 128
+    v0, f0, R, T = _cow_views(N)
+    cfg = Kn.ShadeConfig(H=H, W=H)
+    cc = torch.zeros(1, 3, device=DEV)
+    intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
+    v = v0.clone().requires_grad_(True)
+    Rg = R.clone().requires_grad_(True)
+    out = Kn.render_views(v, Rg, T, f0, intr, cc, cfg)
+    loss = out["depth"].sum() + out["sil"].sum() + out["rgb"].sum()
+    loss.backward(retain_graph=True)
+    g1, r1 = v.grad.clone(), Rg.grad.clone()
+    v.grad = None
+    Rg.grad = None
+    loss.backward()
+    assert torch.equal(v.grad, g1) and torch.equal(Rg.grad, r1)
 
 
 def test_vertex_grad_independent_of_view_order():
@@ -101,3 +124,35 @@ def test_vertex_grad_independent_of_view_order():
     print(f"[determinism] vertex grad under a view permutation: max |diff| = {(va - vb).abs().max().item():.3e}")
     assert torch.equal(va, vb)
     assert torch.equal(Ra[perm], Rb) and torch.equal(Ta[perm], Tb)
+
+
+@pytest.mark.parametrize("clip", [False, True])
+def test_geometry_only_backward_equals_full(clip):
+    """A backward without an RGB gradient (depth / silhouette renders: camera_pose_optimizer.py:244,248) runs
+    the geometry-only k_bwd_fused (no Phong / texture backward, 9 values per face row). Its vertex and pose
+    gradients equal, bitwise, those of the full kernel given an all-zero RGB gradient."""
+    N, H = 4, 160
+    v0, f0, R, T = _cow_views(N, dist=0.35 if clip else 0.7)
+    intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
+    cfg = Kn.ShadeConfig(H=H, W=H, clip=False, z_clip=0.5 if clip else None)
+    cc = torch.zeros(1, 3, device=DEV)
+    g = torch.Generator().manual_seed(4)
+    gD = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)
+    gS = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)
+
+    def run(zero_rgb):
+        v = v0.clone().requires_grad_(True)
+        Rg, Tg = R.clone().requires_grad_(True), T.clone().requires_grad_(True)
+        Kn._RESHADE["entry"] = None
+        out = Kn.render_views(v, Rg, Tg, f0, intr, cc, cfg)
+        loss = (out["depth"] * gD).sum() + (out["sil"] * gS).sum()
+        if zero_rgb:
+            loss = loss + (out["rgb"] * 0.0).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return v.grad, Rg.grad, Tg.grad
+
+    geo, full = run(False), run(True)
+    assert geo[0].abs().max() > 0
+    for a, b, nm in zip(geo, full, ("verts", "R", "T")):
+        assert torch.equal(a, b), f"{nm}: geometry-only backward differs from the full kernel's"

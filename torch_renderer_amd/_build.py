@@ -55,14 +55,59 @@ def needs_build(out: str = OUT) -> bool:
 
 
 def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not needs_build():
-        return OUT
-    cmd = [hipcc(), *HIPCC_FLAGS, "-o", OUT + ".tmp", *sources()]
+    if force or needs_build():
+        cmd = [hipcc(), *HIPCC_FLAGS, "-o", OUT + ".tmp", *sources()]
+        if verbose:
+            print("[mi355r] " + " ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        os.replace(OUT + ".tmp", OUT)
+    build_torch_ext(force=force, verbose=verbose)
+    return OUT
+
+
+# The fused render's autograd node in C++ (csrc/mr_torch.cpp, host code only): compiled with the host
+# compiler against torch's headers and libraries, in-tree like libmi355r.so (it travels with the tree).
+TORCH_EXT = os.path.join(_HERE, "_mr_torch.so")
+TORCH_EXT_SRC = os.path.join(CSRC, "mr_torch.cpp")
+
+
+def torch_ext_cmd(out: str):
+    import sysconfig
+
+    import torch
+    from torch.utils import cpp_extension as ce
+
+    tdir = os.path.dirname(torch.__file__)
+    rocm = os.environ.get("ROCM_PATH", "/opt/rocm")
+    cxx = os.environ.get("CXX", "g++")
+    incs = [f"-I{p}" for p in ce.include_paths()] + [f"-I{sysconfig.get_paths()['include']}",
+                                                     f"-I{os.path.join(rocm, 'include')}",
+                                                     f"-I{os.path.join(_HERE, '..', 'include')}"]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-DTORCH_EXTENSION_NAME=_mr_torch",
+            "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM",
+            "-D__HIP_PLATFORM_AMD__=1", *incs, TORCH_EXT_SRC, "-o", out,
+            f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python",
+            f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+
+
+def torch_ext_needs_build() -> bool:
+    if not os.path.exists(TORCH_EXT):
+        return True
+    t = os.path.getmtime(TORCH_EXT)
+    deps = [TORCH_EXT_SRC, os.path.join(_HERE, "..", "include", "mi355r.h"), os.path.abspath(__file__)]
+    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+
+
+def build_torch_ext(force: bool = False, verbose: bool = True) -> str:
+    if not force and not torch_ext_needs_build():
+        return TORCH_EXT
+    cmd = torch_ext_cmd(TORCH_EXT + ".tmp")
     if verbose:
         print("[mi355r] " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(TORCH_EXT + ".tmp", TORCH_EXT)
+    return TORCH_EXT
 
 
 if __name__ == "__main__":

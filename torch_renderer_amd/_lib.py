@@ -116,6 +116,9 @@ _SIGS = [
     ("mr_render_forward_opencv", _I32, [ctypes.POINTER(MrMesh), ctypes.POINTER(MrOpencvPoses), _VP, _I64, _VP, _I64,
                                         ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP,
                                         _VP, _VP, _VP, _SZ, _VP]),
+    ("mr_render_forward_poses", _I32, [ctypes.POINTER(MrMesh), ctypes.POINTER(MrPoses), _VP, _I64, _VP, _I64,
+                                       ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP,
+                                       _VP, _VP, _VP, _SZ, _VP]),
     ("mr_render_backward_workspace", _SZ, [_I64, _I64, _I64, _I32, _I32]),
     ("mr_render_backward", _I32, [ctypes.POINTER(MrMesh), _VP, _VP, _I64, _VP, _I64,
                                   ctypes.POINTER(MrRasterSettings), ctypes.POINTER(MrShadeParams), _VP, _VP, _VP,
@@ -180,6 +183,34 @@ def load(path: str | None = None) -> ctypes.CDLL:
         if path is None:
             _lib = lib
         return lib
+
+
+_EXT = None
+_EXT_FNS = ("mr_last_error", "mr_render_workspace", "mr_render_workspace_meshes", "mr_render_reshade",
+            "mr_render_forward_opencv", "mr_render_forward_poses", "mr_render_backward_workspace",
+            "mr_render_backward", "mr_render_backward_opencv")
+
+
+def torch_ext():
+    """The fused render's autograd node in C++ (``_mr_torch.so``, csrc/mr_torch.cpp), bound to the C ABI
+    functions of the library ``load()`` returned. Raises RuntimeError if it is missing (no fallback)."""
+    global _EXT
+    with _lock:
+        if _EXT is not None:
+            return _EXT
+    path = os.path.join(_HERE, "_mr_torch.so")
+    if not os.path.exists(path):
+        raise RuntimeError(f"mi355r: {path} not found. Build it first (python -m torch_renderer_amd._build).")
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("_mr_torch", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    lib = load()
+    mod.init({name: ctypes.cast(getattr(lib, name), ctypes.c_void_p).value for name in _EXT_FNS})
+    with _lock:
+        _EXT = mod
+    return mod
 
 
 def check(rc: int) -> None:

@@ -448,7 +448,7 @@ MR_DEV int seg_stage_face(int key, int face, float (&v)[ACC], float* lrow, int* 
 // total with a 64-bit integer atomic (order-independent: the totals are deterministic), lanes covering
 // consecutive components of consecutive runs; a component of magnitude >= MR_FIX_MAX takes a float
 // atomic into the face's float row. Straight-line, as seg_flush.
-template <int ACC>
+template <int ACC, int STRIDE = ACC>
 MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* __restrict__ gface, const float* lrow,
                           const int* lkey) {
   int lane = threadIdx.x & 63;
@@ -462,7 +462,7 @@ MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* 
       const int j = 64 * i + lane;
       if (j < tot) {
         const float x = lrow[j];
-        const uint32_t e = (uint32_t)lkey[r] * (uint32_t)ACC + (uint32_t)c;
+        const uint32_t e = (uint32_t)lkey[r] * (uint32_t)STRIDE + (uint32_t)c;
         if (fabsf(x) < MR_FIX_MAX) {
           if (x != 0.0f) atomicAdd(gfix + e, (unsigned long long)fix_of(x));
         } else {
@@ -553,7 +553,7 @@ MR_DEV float g_alpha(const RenderBwdParams& P, int gt, int lane) {
 // (render step 223k -> 232k frames/s, profiles/r4f_bands_ab.txt). Not the CLIP instantiation: its
 // clip chain rule would spill ~60 VGPRs under the cap.
 #ifndef MR_BWD_ATTR
-#define MR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(CLIP ? 1 : 3)))
+#define MR_BWD_ATTR __attribute__((amdgpu_waves_per_eu(GEO ? (CLIP ? 2 : 4) : (CLIP ? 1 : 3))))
 #endif
 // The kernel's parameters re-read from the kernarg segment through a pointer the compiler cannot see
 // through: uniform values used across a long loop body are otherwise hoisted into SGPRs for the whole
@@ -568,14 +568,20 @@ MR_DEV const T& kernarg_params() {
   return *(const T*)(const char*)p;
 }
 
-template <int ACC, bool CLIP>
+// GEO: no RGB gradient arrived (a depth and / or silhouette render's backward: camera_pose_optimizer.py:244,
+// :248): the blends' backward reduces to d/dz (relu) and d/dsdist (the silhouette sigmoid) — the Phong,
+// texture and barycentric terms are zero — so half 1 is skipped and the two values are computed in half 2,
+// bitwise those the full path gives with a zero RGB gradient; only the 9 position columns of each face row
+// are non-zero (NV = 9 values per run instead of ACC, added into the ACC-wide rows).
+template <int ACC, bool CLIP, bool GEO = false>
 __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
+  constexpr int NV = GEO ? 9 : ACC;  // values per face row this kernel adds
   const RenderBwdParams& P = P0;
-  __shared__ float lrow[4][64 * ACC];
+  __shared__ float lrow[4][64 * NV];
   __shared__ int lkey[4][64];
   __shared__ int lperm[4][64];
-  __shared__ float4 lrec[4][MR_BWD_REC][64];
-  const bool lut = stage_tex_lut(P.S);  // the u8 texture table in LDS
+  __shared__ float4 lrec[4][GEO ? 1 : MR_BWD_REC][64];
+  const bool lut = GEO ? false : stage_tex_lut(P.S);  // the u8 texture table in LDS
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
@@ -623,7 +629,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     int n, px, py;
     slot_pixel(P, gt, p, n, px, py);
     // ---- half 1: blends / Phong / texture backward -> lrec
-    if (f >= 0) {
+    if (!GEO && f >= 0) {
       PixGeom Gm;
       load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
       const float gD = gin[0], gS = gin[1];
@@ -658,9 +664,9 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         o[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][k][lane] = o[k];
+      for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][GEO ? 0 : k][lane] = o[k];
     }
-    wave_lds_sync();
+    if (!GEO) wave_lds_sync();
     __builtin_amdgcn_sched_barrier(0);  // keep half 2's loads out of half 1's register peak
     // ---- half 2: raster + projection backward, per-face runs, R/T partials
     const ViewRec V = P.views[n];
@@ -675,7 +681,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
-      seg_flush_fix<ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
+      seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
       if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -684,14 +690,32 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     for (int i = 0; i < 9; ++i) gR[i] = 0.0f;
 #pragma unroll
     for (int i = 0; i < 3; ++i) gT[i] = 0.0f;
-    float row[ACC];
+    float row[NV];
 #pragma unroll
-    for (int k = 0; k < ACC; ++k) row[k] = 0.0f;
+    for (int k = 0; k < NV; ++k) row[k] = 0.0f;
     int key = -1;
     if (f >= 0) {
-      const float4 a0 = lrec[wave][0][lane], a1 = lrec[wave][1][lane], a2 = lrec[wave][2][lane];
-      const float4 a3 = lrec[wave][3][lane];
-      const float4 a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 a0, a1, a2, a3, a4;
+      if (GEO) {
+        // shade_fwd / shade_bwd's depth and silhouette terms (the same operations; the RGB terms vanish)
+        const float pz = (CLIP && (r.flags & FR_CLIP))
+                             ? [&] { FragEval es; eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad,
+                                                            P.blur, P.persp, P.clipb, es); return es.pz; }()
+                             : (frag.x * r.z0 + frag.y * r.z1) + frag.z * r.z2;
+        float ps, qs;
+        sigmoid2((-frag.w) * P.S.inv_sigma_sil, ps, qs);
+        const float gz = (P.S.zbuf_mode || pz > 0.0f) ? 0.0f + gin[0] : 0.0f;
+        const float gx = gin[1] * (ps * qs);
+        const float gsd = 0.0f + -(gx * P.S.inv_sigma_sil);
+        a0 = make_float4(gz, gsd, 0.f, 0.f);
+        a1 = a2 = a3 = a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        a0 = lrec[wave][0][lane];
+        a1 = lrec[wave][1][lane];
+        a2 = lrec[wave][2][lane];
+        a3 = lrec[wave][3][lane];
+        a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
       const float gb[3] = {a0.z, a0.w, a1.x};
       const float gP[3] = {a1.y, a1.z, a1.w};
@@ -712,18 +736,22 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         project_bwd(V, X[c], gfv[c], gX, gR, gT);
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-          row[3 * c + k] = b[c] * gP[k] + gX[k];
-          row[9 + 3 * c + k] = b[c] * gNn[k];
-          if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
+          if (GEO) {
+            row[3 * c + k] = gX[k];
+          } else {
+            row[3 * c + k] = b[c] * gP[k] + gX[k];
+            row[9 + 3 * c + k] = b[c] * gNn[k];
+            if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
+          }
         }
       }
     }
-    nt_prev = seg_stage_face<ACC>(f >= 0 ? f : -1, key, row, lrow[wave], lkey[wave]);
+    nt_prev = seg_stage_face<NV>(f >= 0 ? f : -1, key, row, lrow[wave], lkey[wave]);
     rt_prev = rt_partial(gR, gT, lane);
     s_prev = s;
   }
   if (nt_prev >= 0) {
-    seg_flush_fix<ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
+    seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
     if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
   }
 }

@@ -309,6 +309,13 @@ __global__ void __launch_bounds__(256) k_views_from_poses(CvPoses C, int64_t N, 
   }
 }
 
+// View records from the pose arrays (either convention, cv_view_elem), the count -> scan path of the
+// fused render.
+__global__ void __launch_bounds__(256) k_views_from_cv(CvPoses C, int64_t N) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < N * 16) C.out[i] = cv_view_elem(C, i >> 4, (int)(i & 15));
+}
+
 size_t mr_rasterize_meshes_world_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin) {
   return align_up(mr_rasterize_meshes_workspace(N, N * F, H, W, max_faces_per_bin), 256) +
          align_up(sizeof(int64_t) * 2 * (size_t)(N > 0 ? N : 1), 256);
@@ -726,6 +733,18 @@ int32_t mr_render_forward_opencv(const mr_mesh_t* m, const mr_opencv_poses_t* po
   C.opencv = 1;
   return render_forward(m, views_out, N, cc, ncc, s, sp, depth, sil, rgb, p2f32, ws, ws_bytes, stream, C);
 }
+int32_t mr_render_forward_poses(const mr_mesh_t* m, const mr_poses_t* poses, mr_view_t* views_out, int64_t N,
+                                const float* cc, int64_t ncc, const mr_raster_settings_t* s,
+                                const mr_shade_params_t* sp, float* depth, float* sil, float* rgb, int32_t* p2f32,
+                                void* ws, size_t ws_bytes, void* stream) {
+  if (!poses || !poses->R || !poses->T || !poses->intr || !views_out) return set_err(MR_EINVAL, "NULL pose argument");
+  if (poses->R_stride < 0 || poses->T_stride < 0 || poses->intr_stride < 0) return set_err(MR_EINVAL, "negative stride");
+  CvPoses C;
+  C.R = poses->R; C.sR = poses->R_stride; C.t = poses->T; C.sT = poses->T_stride;
+  C.intr = poses->intr; C.sI = poses->intr_stride; C.out = (float*)views_out;
+  C.opencv = 0;
+  return render_forward(m, views_out, N, cc, ncc, s, sp, depth, sil, rgb, p2f32, ws, ws_bytes, stream, C);
+}
 static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_t N, const float* cc, int64_t ncc,
                               const mr_raster_settings_t* s, const mr_shade_params_t* sp, float* depth, float* sil,
                               float* rgb, int32_t* p2f32, void* ws, size_t ws_bytes, void* stream, const CvPoses& C) {
@@ -799,8 +818,13 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
       hipMemsetAsync(w.gflt, 0, sizeof(float) * 27 * (size_t)m->F, st) != hipSuccess)
     return set_err(MR_ELAUNCH, "memset failed");
   if (C.R) {  // count -> scan path: the view records first
-    k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C.R, C.sR, C.t, C.sT, C.intr, C.sI, N, C.out);
-    MR_CHECK_LAUNCH("k_views_from_opencv");
+    if (C.opencv) {
+      k_views_from_opencv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C.R, C.sR, C.t, C.sT, C.intr, C.sI, N, C.out);
+      MR_CHECK_LAUNCH("k_views_from_opencv");
+    } else {
+      k_views_from_cv<<<ceil_div(N * 16, 256), 256, 0, st>>>(C, N);
+      MR_CHECK_LAUNCH("k_views_from_cv");
+    }
   }
   MR_TIMED(KID_SETUP, st, (k_setup_zero<<<(unsigned)(vb + ceil_div(nzero, 1024)), 256, 0, st>>>(m->verts, m->V, m->faces, m->vadj_ptr, m->vadj, m->vnormals_out, m->vraw_out, vb, w.ctr, nzero)));
   MR_CHECK_LAUNCH("k_setup_zero");
@@ -988,16 +1012,28 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
   };
-  static int f18 = 0, f27 = 0, f18c = 0, f27c = 0;
+  static int f18 = 0, f27 = 0, f18c = 0, f27c = 0, g18 = 0, g27 = 0, g18c = 0, g27c = 0;
   if (!f18) f18 = resident_grid(k_bwd_fused<18, false>, 256, 3);
   if (!f27) f27 = resident_grid(k_bwd_fused<27, false>, 256, 2);
   if (!f18c) f18c = resident_grid(k_bwd_fused<18, true>, 256, 3);
   if (!f27c) f27c = resident_grid(k_bwd_fused<27, true>, 256, 2);
+  if (!g18) g18 = resident_grid(k_bwd_fused<18, false, true>, 256, 4);
+  if (!g27) g27 = resident_grid(k_bwd_fused<27, false, true>, 256, 4);
+  if (!g18c) g18c = resident_grid(k_bwd_fused<18, true, true>, 256, 4);
+  if (!g27c) g27c = resident_grid(k_bwd_fused<27, true, true>, 256, 4);
+  // no RGB gradient (a depth / silhouette render's backward): the geometry-only instantiation
+  const bool geo = P.gRGB == nullptr;
   if (s->clip_z) {
-    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, true><<<cap(f27c), 256, 0, st>>>(P)));
+    if (geo) {
+      if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, true, true><<<cap(g27c), 256, 0, st>>>(P)));
+      else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, true, true><<<cap(g18c), 256, 0, st>>>(P)));
+    } else if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, true><<<cap(f27c), 256, 0, st>>>(P)));
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, true><<<cap(f18c), 256, 0, st>>>(P)));
   } else {
-    if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false><<<cap(f27), 256, 0, st>>>(P)));
+    if (geo) {
+      if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false, true><<<cap(g27), 256, 0, st>>>(P)));
+      else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false, true><<<cap(g18), 256, 0, st>>>(P)));
+    } else if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false><<<cap(f27), 256, 0, st>>>(P)));
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false><<<cap(f18), 256, 0, st>>>(P)));
   }
   MR_CHECK_LAUNCH("k_bwd_fused");

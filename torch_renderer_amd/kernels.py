@@ -484,7 +484,7 @@ def _mesh_struct(v, f, vptr, vadj, vn, tex: TextureArgs, vcol, ranges=None):
 # forward's workspace, kept while its geometry's tensors are alive and unchanged, so that a following call
 # with the same geometry but a different shading only re-shades (mr_render_reshade: no projection, binning
 # or rasterization). An entry serves each shading configuration once (a repeated identical call — a
-# benchmark loop, a second step — rasterizes again) and ends when a backward over its workspace starts.
+# benchmark loop, a second step — rasterizes again).
 # The workspace is held by a weak reference: the forward's autograd node keeps it alive while a backward
 # can still run; an inference render (no_grad, nothing requiring grad, discarded outputs) lets it go, so
 # the entry never pins a workspace. The key includes the launch stream (a reshade on another stream would
@@ -516,164 +516,67 @@ def _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream):
             cfg.max_faces_per_bin, cfg.z_clip, bool(pose_cv), ranges is None, stream)
 
 
-class RenderViews(torch.autograd.Function):
-    """One raster pass over N views of one mesh -> (depth, silhouette, rgb).
-
-    Replaces DepthRender.render (2 raster passes, torch_renderer.py:110-121) +
-    ColorRender.render (torch_renderer.py:155-159) with a single fused launch,
-    and their autograd backward with one fused launch + vertex gathers.
-    Differentiable inputs: verts (V,3), R (N,3,3), T (N,3), vcolors (V,3)."""
-
-    @staticmethod
-    def forward(ctx, verts, R, T, vcolors, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs,
-                pose_cv=False, ranges=None):
-        _require_cuda(verts, R, T, faces)
-        ctx.set_materialize_grads(False)  # unused outputs get no zero-filled (N,H,W) grads
-        if not cfg.want_rgb and cfg.light_kind != 1:
-            # lights only shape the Phong colours: depth / silhouette renders need no vertex normals
-            cfg = ShadeConfig(**{**cfg.__dict__, "light_kind": 1})
-        L = _lib.load()
-        dev = verts.device
-        v = verts.detach().float().contiguous()
-        f, vptr, vadj = mesh_topology(faces, v.shape[0])
-        vcol = vcolors.detach().float().contiguous() if vcolors is not None else None
-        poses = None
-        if pose_cv:  # R, T are OpenCV poses (DifferentiableRenderer callers): converted inside the forward
-            Rc, sR = _batch_stride(R.detach().reshape(-1, 3, 3))
-            tc, sT = _batch_stride(T.detach().reshape(-1, 3))
-            ic, sI = _batch_stride(intr.reshape(-1, 4))
-            sp_ = _lib.strided_ptr
-            poses = _lib.MrOpencvPoses(sp_(Rc), sR, sp_(tc), sT, sp_(ic), sI)
-            views = torch.empty((max(R.shape[0], T.shape[0], intr.shape[0]), 16), device=dev)
-        else:
-            views = make_views(R.detach(), T.detach(), intr)
-        N = views.shape[0]
-        H, W = cfg.H, cfg.W
-        vn = raw = None
-        if cfg.light_kind == 0:  # computed by the forward's first launch (mesh.vnormals_out)
-            vn, raw = torch.empty_like(v), torch.empty_like(v)
-        cc = cam_centers.float().contiguous().reshape(-1, 3)
-        rs = cfg.raster_struct()
-        sp = cfg.shade_struct()
-        mesh = _mesh_struct(v, f, vptr, vadj, vn, tex, vcol, ranges)
-        if vn is not None:
-            mesh.vnormals_out, mesh.vraw_out = vn.data_ptr(), raw.data_ptr()
-        depth = torch.empty((N, H, W), device=dev) if cfg.want_depth else None
-        sil = torch.empty((N, H, W, 4) if cfg.sil_rgba else (N, H, W), device=dev) if cfg.want_sil else None
-        rgb = torch.empty((N, H, W, cfg.rgb_channels), device=dev) if cfg.want_rgb else None
-        p2f = torch.empty((N, H, W), device=dev, dtype=torch.int32) if cfg.want_p2f else None
-        wsq = L.mr_render_workspace_meshes if ranges is not None else L.mr_render_workspace
-        wsb = _ws_size(wsq, N, f.shape[0], H, W, rs.max_faces_per_bin)
-        stream = _lib.stream_handle(dev)
-        geom = _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream.value)
-        ent = _RESHADE["entry"]
-        ssig = _shade_sig(cfg)
-        ws = None
-        if (_RESHADE["enabled"] and ent is not None and ent["geom"] == geom and ssig not in ent["served"] and
-                len(ent["served"]) < 4 and not cfg.want_p2f):
-            ws = ent["ws"]()  # None once the workspace's last autograd node is gone
-        reuse = ws is not None
-        if reuse:  # same raster, another shading: the entry's workspace and view records, a new ShadeRec slot
-            views = ent["views"]
-            slot = len(ent["served"])
-            ent["served"].add(ssig)
-            sp.out_flags |= slot << _lib.MR_SREC_SLOT_SHIFT
-        else:
-            ws = torch.empty(int(wsb), dtype=torch.uint8, device=dev)
-            slot = 0
-            # the entry holds the (small) geometry tensors, so their storage cannot be reused while it lives,
-            # and the workspace only weakly
-            _RESHADE["entry"] = {"geom": geom, "refs": (v, f, R, T, intr), "ws": weakref.ref(ws), "views": views,
-                                 "served": {ssig}}
-        global _LAST_RENDER
-        nrec = f.shape[0] if ranges is not None else N * f.shape[0]
-        _LAST_RENDER = (weakref.ref(ws), (N, nrec, H, W, rs.max_faces_per_bin))
-        if reuse:
-            check(L.mr_render_reshade(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
-                                      ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
-                                      stream))
-        elif poses is not None:
-            check(L.mr_render_forward_opencv(ctypes.byref(mesh), ctypes.byref(poses), ptr(views), N, ptr(cc),
-                                             cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(depth), ptr(sil),
-                                             ptr(rgb), ptr(p2f), ptr(ws), wsb, stream))
-        else:
-            check(L.mr_render_forward(ctypes.byref(mesh), ptr(views), N, ptr(cc), cc.shape[0], ctypes.byref(rs),
-                                      ctypes.byref(sp), ptr(depth), ptr(sil), ptr(rgb), ptr(p2f), ptr(ws), wsb,
-                                      stream))
-        e0 = _empty0(dev)
-        ctx.save_for_backward(v, f, vcol if vcol is not None else e0, views, cc, ws, vn if vn is not None else e0,
-                              raw if raw is not None else e0, vptr, vadj)
-        ctx.cfg, ctx.tex, ctx.has_vcol, ctx.pose_cv, ctx.ranges = cfg, tex, vcolors is not None, pose_cv, ranges
-        ctx.slot = slot
-        outs = [x for x in (depth, sil, rgb) if x is not None]
-        if p2f is not None:
-            ctx.mark_non_differentiable(p2f)
-            outs.append(p2f)
-        return tuple(outs)
-
-    @staticmethod
-    def backward(ctx, *grads):
-        v, f, vcol, views, cc, ws, vn, raw, vptr, vadj = ctx.saved_tensors
-        cfg, tex = ctx.cfg, ctx.tex
-        L = _lib.load()
-        dev = v.device
-        N = views.shape[0]
-        gi = 0
-        gD = gS = gC = None
-        if cfg.want_depth:
-            gD = grads[gi]
-            gi += 1
-        if cfg.want_sil:
-            gS = grads[gi]
-            gi += 1
-        if cfg.want_rgb:
-            gC = grads[gi]
-            gi += 1
-        mesh = _mesh_struct(v, f, vptr, vadj, vn if vn.numel() else None, tex, vcol if vcol.numel() else None,
-                            ctx.ranges)
-        rs = cfg.raster_struct()
-        sp = cfg.shade_struct()
-        # the outputs whose gradients arrived (absent ones: NULL, no zero tensors)
-        sp.out_flags &= ~((0 if gD is not None else _lib.MR_OUT_DEPTH | _lib.MR_OUT_ZBUF) |
-                          (0 if gS is not None else _lib.MR_OUT_SIL | _lib.MR_OUT_SIL_RGBA) |
-                          (0 if gC is not None else _lib.MR_OUT_RGB))
-        sp.out_flags |= ctx.slot << _lib.MR_SREC_SLOT_SHIFT  # the ShadeRecs this node's forward packed
-        ent = _RESHADE["entry"]
-        if ent is not None and ent["ws"]() is ws:  # a backward over the workspace ends its reuse
-            _RESHADE["entry"] = None
-        if not getattr(ws, "_mr_rows_used", False):  # the forward cleared the face-gradient totals in ws
-            sp.out_flags |= _lib.MR_GRAD_ROWS_CLEARED
-            ws._mr_rows_used = True
-        gverts = torch.empty_like(v)
-        gviews = torch.empty((N, 12), device=dev)
-        gcol = torch.empty_like(v) if ctx.has_vcol else None
-        bwb = _ws_size(L.mr_render_backward_workspace, N, v.shape[0], f.shape[0], cfg.H, cfg.W)
-        bws = torch.empty(int(bwb), dtype=torch.uint8, device=dev)
-        c = lambda t: t.float().contiguous() if t is not None else None  # noqa: E731
-        if ctx.pose_cv:  # pose grads straight in the OpenCV frame (no separate conversion launch)
-            gR = torch.empty((N, 3, 3), device=dev)
-            gt = torch.empty((N, 3), device=dev)
-            check(L.mr_render_backward_opencv(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N,
-                                              ptr(cc), cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
-                                              ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gR),
-                                              ptr(gt), ptr(gcol), _lib.stream_handle(dev)))
-            return (gverts, gR, gt, gcol, None, None, None, None, None, None, None)
-        check(L.mr_render_backward(ctypes.byref(mesh), ptr(raw) if raw.numel() else None, ptr(views), N, ptr(cc),
-                                   cc.shape[0], ctypes.byref(rs), ctypes.byref(sp), ptr(c(gD)),
-                                   ptr(c(gS)), ptr(c(gC)), ptr(ws), ptr(bws), bwb, ptr(gverts), ptr(gviews),
-                                   ptr(gcol), _lib.stream_handle(dev)))
-        return (gverts, gviews[:, :9].reshape(N, 3, 3), gviews[:, 9:12], gcol, None, None, None, None, None, None,
-                None)
+def _blob(kind, cfg, make):
+    """The bytes of one of cfg's ctypes structs (cached by the configuration's values)."""
+    k = (kind, cfg.key())
+    hit = _STRUCT_CACHE.get(k)
+    if hit is None:
+        if len(_STRUCT_CACHE) > 256:
+            _STRUCT_CACHE.clear()
+        hit = _STRUCT_CACHE[k] = bytes(make())
+    return hit
 
 
 def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: TextureArgs | None = None,
                  vcolors=None, pose_cv=False, ranges=None):
     """Functional entry: returns dict(depth, sil, rgb[, pix_to_face32 when cfg.want_p2f]).
+
+    One raster pass over N views of one mesh -> (depth, silhouette, rgb): replaces DepthRender.render
+    (2 raster passes, torch_renderer.py:110-121) + ColorRender.render (torch_renderer.py:155-159) with a
+    single fused launch sequence, and their autograd backward with one fused launch + vertex gathers.
+    Differentiable inputs: verts (V,3), R (N,3,3), T (N,3), vcolors (V,3). The autograd node is C++
+    (``_mr_torch``, csrc/mr_torch.cpp): the forward's and the backward's host work around the C ABI run
+    without Python, the backward inside autograd's device thread.
     pose_cv: R, T are OpenCV camera poses (converted on the GPU, gradients returned in kind).
     ranges: (view_face_first, view_face_count, max faces) when verts / faces are the union of N
     distinct meshes, view n rendering mesh n (one launch for the batch); None: one shared mesh."""
     tex = tex or TextureArgs()
-    outs = RenderViews.apply(verts, R, T, vcolors, faces, intr, cam_centers, cfg, tex, pose_cv, ranges)
+    _require_cuda(verts, R, T, faces)
+    if not cfg.want_rgb and cfg.light_kind != 1:
+        # lights only shape the Phong colours: depth / silhouette renders need no vertex normals
+        cfg = ShadeConfig(**{**cfg.__dict__, "light_kind": 1})
+    dev = verts.device
+    f, vptr, vadj = mesh_topology(faces, verts.shape[0])
+    rsb = _blob("rb", cfg, cfg.raster_struct)
+    spb = _blob("sb", cfg, cfg.shade_struct)
+    stream = _lib.stream_handle(dev).value
+    geom = _geom_sig(verts, f, R, T, intr, cfg, pose_cv, ranges, stream)
+    ent = _RESHADE["entry"]
+    ssig = _shade_sig(cfg)
+    ws = views = None
+    slot = 0
+    if (_RESHADE["enabled"] and ent is not None and ent["geom"] == geom and ssig not in ent["served"] and
+            len(ent["served"]) < 4 and not cfg.want_p2f):
+        ws = ent["ws"]()  # None once the workspace's last autograd node is gone
+    if ws is not None:  # same raster, another shading: the entry's workspace and view records, a new ShadeRec slot
+        views = ent["views"]
+        slot = len(ent["served"])
+        ent["served"].add(ssig)
+    rr = ranges if ranges is not None else (None, None, 0)
+    outs = _lib.torch_ext().render_views(
+        verts, R, T, vcolors, f, vptr, vadj, intr, cam_centers, tex.kind, tex.verts_uvs, tex.faces_uvs,
+        tex.tex_rgba, tex.tex_u8, tex.tex_lut, rr[0], rr[1], int(rr[2]), rsb, spb,
+        (1 if pose_cv else 0) | (2 if cfg.want_p2f else 0), ws, views, slot)
+    ws_out, views_out = outs[-2], outs[-1]
+    if ws is None:
+        # a new raster: the entry holds the (small) geometry tensors, so their storage cannot be reused while
+        # it lives, and the workspace only weakly (the forward's autograd node keeps it while a backward can
+        # run; an inference render lets it go)
+        _RESHADE["entry"] = {"geom": geom, "refs": (verts, f, R, T, intr), "ws": weakref.ref(ws_out),
+                             "views": views_out, "served": {ssig}}
+    global _LAST_RENDER
+    nrec = f.shape[0] if ranges is not None else views_out.shape[0] * f.shape[0]
+    _LAST_RENDER = (weakref.ref(ws_out), (views_out.shape[0], nrec, cfg.H, cfg.W, cfg.max_faces_per_bin))
     res = {}
     i = 0
     for name, want in (("depth", cfg.want_depth), ("sil", cfg.want_sil), ("rgb", cfg.want_rgb)):

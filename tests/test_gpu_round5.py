@@ -132,9 +132,9 @@ def test_geometry_only_backward_equals_full(clip):
     the geometry-only k_bwd_fused (no Phong / texture backward, 9 values per face row). Its vertex and pose
     gradients equal, bitwise, those of the full kernel given an all-zero RGB gradient."""
     N, H = 4, 160
-    v0, f0, R, T = _cow_views(N, dist=0.35 if clip else 0.7)
+    v0, f0, R, T = _cow_views(N, dist=0.4 if clip else 0.7)
     intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
-    cfg = Kn.ShadeConfig(H=H, W=H, clip=False, z_clip=0.5 if clip else None)
+    cfg = Kn.ShadeConfig(H=H, W=H, clip=False, z_clip=0.3 if clip else None)
     cc = torch.zeros(1, 3, device=DEV)
     g = torch.Generator().manual_seed(4)
     gD = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)

@@ -145,7 +145,8 @@ struct RenderViewsFn : public torch::autograd::Function<RenderViewsFn> {
     const bool pose_cv = (a.flags & 1) != 0, want_p2f = (a.flags & 2) != 0, reuse = a.ws.defined();
     const auto dev = verts.device();
     Tensor v = f32c(verts.detach());
-    Tensor vcol = vcolors.defined() ? f32c(vcolors.detach()) : Tensor();
+    const bool has_vcol = vcolors.numel() > 0;  // (an empty placeholder when the mesh has no vertex colours)
+    Tensor vcol = has_vcol ? f32c(vcolors.detach()) : Tensor();
     Tensor cc = f32c(a.cc).reshape({-1, 3});
     const int64_t Rn = R.numel() / 9, Tn = T.numel() / 3, In = a.intr.numel() / 4;
     const int64_t N = reuse ? a.views.size(0) : std::max(Rn, std::max(Tn, In));
@@ -204,7 +205,7 @@ struct RenderViewsFn : public torch::autograd::Function<RenderViewsFn> {
     ctx->saved_data["tex_kind"] = a.tex_kind;
     ctx->saved_data["fmax"] = a.fmax;
     ctx->saved_data["pose_cv"] = pose_cv;
-    ctx->saved_data["vcol"] = vcolors.defined();
+    ctx->saved_data["vcol"] = has_vcol;
     variable_list outs;
     for (const Tensor* t : {&depth, &sil, &rgb})
       if (t->defined()) outs.push_back(*t);
@@ -268,7 +269,7 @@ struct RenderViewsFn : public torch::autograd::Function<RenderViewsFn> {
       gR = gviews.narrow(1, 0, 9).reshape({N, 3, 3});
       gT = gviews.narrow(1, 9, 3);
     }
-    return {gverts, gR, gT, gcol};
+    return {gverts, gR, gT, gcol, Tensor()};  // (none for the RenderArgs argument)
   }
 };
 
@@ -290,7 +291,9 @@ variable_list render_views(Tensor verts, Tensor R, Tensor T, c10::optional<Tenso
   a.ffirst = ffirst.value_or(Tensor()); a.fcount = fcount.value_or(Tensor()); a.fmax = fmax;
   a.rs = std::move(rs); a.sp = std::move(sp); a.flags = flags;
   a.ws = ws.value_or(Tensor()); a.views = views.value_or(Tensor()); a.slot = slot;
-  return RenderViewsFn::apply(verts, R, T, vcolors.value_or(Tensor()), std::move(a));
+  // an absent vcolors travels as an empty tensor (autograd inputs must be defined tensors)
+  Tensor vc = vcolors.has_value() && vcolors->defined() ? *vcolors : at::empty({0}, verts.options());
+  return RenderViewsFn::apply(verts, R, T, vc, std::move(a));
 }
 
 void init(const std::unordered_map<std::string, int64_t>& fn) {

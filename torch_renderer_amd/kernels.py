@@ -576,7 +576,7 @@ def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: T
                              "views": views_out, "served": {ssig}}
     global _LAST_RENDER
     nrec = f.shape[0] if ranges is not None else views_out.shape[0] * f.shape[0]
-    _LAST_RENDER = (weakref.ref(ws_out), (views_out.shape[0], nrec, cfg.H, cfg.W, cfg.max_faces_per_bin))
+    _LAST_RENDER = (weakref.ref(ws_out), (views_out.shape[0], nrec, cfg.H, cfg.W, int(cfg.max_faces_per_bin or 0)))
     res = {}
     i = 0
     for name, want in (("depth", cfg.want_depth), ("sil", cfg.want_sil), ("rgb", cfg.want_rgb)):

@@ -572,8 +572,10 @@ def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: T
         # a new raster: the entry holds the (small) geometry tensors, so their storage cannot be reused while
         # it lives, and the workspace only weakly (the forward's autograd node keeps it while a backward can
         # run; an inference render lets it go)
-        _RESHADE["entry"] = {"geom": geom, "refs": (verts, f, R, T, intr), "ws": weakref.ref(ws_out),
-                             "views": views_out, "served": {ssig}}
+        # (detached aliases: same storage and version counters, but no autograd graph kept alive — a kept
+        # graph holds the leaves' AccumulateGrad nodes, whose stream then mismatches a later HIP-graph capture)
+        _RESHADE["entry"] = {"geom": geom, "refs": tuple(x.detach() for x in (verts, f, R, T, intr)),
+                             "ws": weakref.ref(ws_out), "views": views_out, "served": {ssig}}
     global _LAST_RENDER
     nrec = f.shape[0] if ranges is not None else views_out.shape[0] * f.shape[0]
     _LAST_RENDER = (weakref.ref(ws_out), (views_out.shape[0], nrec, cfg.H, cfg.W, int(cfg.max_faces_per_bin or 0)))

@@ -188,7 +188,8 @@ def load(path: str | None = None) -> ctypes.CDLL:
 _EXT = None
 _EXT_FNS = ("mr_last_error", "mr_render_workspace", "mr_render_workspace_meshes", "mr_render_reshade",
             "mr_render_forward_opencv", "mr_render_forward_poses", "mr_render_backward_workspace",
-            "mr_render_backward", "mr_render_backward_opencv")
+            "mr_render_backward", "mr_render_backward_opencv", "mr_pose_loss_workspace", "mr_pose_loss_forward_grad",
+            "mr_pose_loss_scale", "mr_pose_loss_backward", "mr_quaternion_to_matrix", "mr_quaternion_to_matrix_backward")
 
 
 def torch_ext():

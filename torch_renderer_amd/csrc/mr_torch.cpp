@@ -1,4 +1,4 @@
-// mi355r — torch glue of the fused render in C++ (the RenderViews autograd node).
+// mi355r — torch glue in C++: the autograd nodes of the fused render, the pose loss and quaternion_to_matrix.
 //
 // The reference callers run the render eagerly, several times per optimiser step (camera_pose_optimizer.py:
 // 244-250: three renders of one pose batch; mesh_deformer.py:197: five single-view renders), so the host work
@@ -37,6 +37,12 @@ struct Abi {
   decltype(&mr_render_backward_workspace) backward_workspace = nullptr;
   decltype(&mr_render_backward) backward = nullptr;
   decltype(&mr_render_backward_opencv) backward_opencv = nullptr;
+  decltype(&mr_pose_loss_workspace) loss_workspace = nullptr;
+  decltype(&mr_pose_loss_forward_grad) loss_forward_grad = nullptr;
+  decltype(&mr_pose_loss_scale) loss_scale = nullptr;
+  decltype(&mr_pose_loss_backward) loss_backward = nullptr;
+  decltype(&mr_quaternion_to_matrix) quat = nullptr;
+  decltype(&mr_quaternion_to_matrix_backward) quat_backward = nullptr;
 } g_abi;
 
 // The torch current stream of t's device (the autograd engine sets the forward's stream for the backward).
@@ -296,6 +302,134 @@ variable_list render_views(Tensor verts, Tensor R, Tensor T, c10::optional<Tenso
   return RenderViewsFn::apply(verts, R, T, vc, std::move(a));
 }
 
+// camera_pose_optimizer.py:257-276 calc_loss (losses.pose_loss): the forward writes the gradients for
+// dL/dtotal = 1 with the loss (one pass); the first backward rescales them in place (mr_pose_loss_scale),
+// a later one (retain_graph) recomputes them (mr_pose_loss_backward). sil / color may be the RGBA images
+// whose [..., 3] / [..., :3] slices the caller passed (read in place, gradients in the RGBA layout).
+struct LossArgs {
+  Tensor mask, depth_ref, rgb_ref;
+  double delta = 0.05, w_color = 0.01;
+  bool sil_rgba = false, col_rgba = false;
+};
+
+struct PoseLossFn : public torch::autograd::Function<PoseLossFn> {
+  static variable_list forward(AutogradContext* ctx, Tensor depth, Tensor sil_in, Tensor color_in, LossArgs a) {
+    const int64_t npix = depth.numel();
+    const int64_t s_stride = a.sil_rgba ? 4 : 1, c_stride = a.col_rgba ? 4 : 3;
+    TORCH_CHECK(a.rgb_ref.size(-1) == 3 && color_in.size(-1) == c_stride, "color and rgb_ref must end in 3 channels");
+    TORCH_CHECK(sil_in.numel() == s_stride * npix && a.mask.numel() == npix && a.depth_ref.numel() == npix &&
+                    color_in.numel() == c_stride * npix && a.rgb_ref.numel() == 3 * npix,
+                "pose_loss: inputs must have one element per pixel (per channel) of depth (no broadcasting)");
+    const auto dev = depth.device();
+    Tensor d = f32c(depth.detach());
+    Tensor sl = a.sil_rgba ? sil_in.detach() : f32c(sil_in.detach());
+    Tensor c = a.col_rgba ? color_in.detach() : f32c(color_in.detach());
+    Tensor m = a.mask.detach().to(at::kBool).contiguous().view(at::kByte);
+    Tensor dr = f32c(a.depth_ref.detach()), rr = f32c(a.rgb_ref.detach());
+    auto fo = at::TensorOptions().dtype(at::kFloat).device(dev);
+    const size_t wsb = g_abi.loss_workspace(npix);
+    Tensor ws = at::empty({(int64_t)wsb}, at::TensorOptions().dtype(at::kByte).device(dev));
+    Tensor total = at::empty({}, fo), terms = at::empty({3}, fo);
+    Tensor gd, gs, gc;
+    const bool grads = ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2);
+    if (grads) {
+      gd = at::empty_like(d);
+      gs = at::empty({npix, s_stride}, fo);
+      gc = at::empty({npix, c_stride}, fo);
+    }
+    const float* sp = dptr<float>(sl) + (a.sil_rgba ? 3 : 0);
+    check(g_abi.loss_forward_grad(dptr<float>(d), sp, s_stride, dptr<float>(c), c_stride, dptr<uint8_t>(m),
+                                  dptr<float>(dr), dptr<float>(rr), npix, (float)a.delta, (float)a.w_color,
+                                  dptr<float>(total), dptr<float>(terms), ws.data_ptr(), wsb, dptr<float>(gd),
+                                  dptr<float>(gs), dptr<float>(gc), stream_of(d)));
+    ctx->save_for_backward({d, sl, c, m, dr, rr, ws, gd, gs, gc});
+    ctx->saved_data["pre"] = grads;  // the forward's gradients are still unused
+    ctx->saved_data["s_stride"] = s_stride;
+    ctx->saved_data["c_stride"] = c_stride;
+    ctx->saved_data["delta"] = a.delta;
+    ctx->saved_data["w_color"] = a.w_color;
+    ctx->saved_data["sh_d"] = depth.sizes().vec();
+    ctx->saved_data["sh_s"] = sil_in.sizes().vec();
+    ctx->saved_data["sh_c"] = color_in.sizes().vec();
+    ctx->mark_non_differentiable({terms});
+    return {total, terms};
+  }
+
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    auto sv = ctx->get_saved_variables();
+    const Tensor &d = sv[0], &sl = sv[1], &c = sv[2], &m = sv[3], &dr = sv[4], &rr = sv[5], &ws = sv[6];
+    const int64_t s_stride = ctx->saved_data["s_stride"].toInt(), c_stride = ctx->saved_data["c_stride"].toInt();
+    const int64_t npix = d.numel();
+    Tensor g = grads[0].defined() ? f32c(grads[0]).reshape({1}) : at::zeros({1}, d.options());
+    const hipStream_t st = stream_of(d);
+    Tensor gd, gs, gc;
+    if (ctx->saved_data["pre"].toBool()) {  // the forward's gradients, scaled by dL/dtotal (first backward)
+      ctx->saved_data["pre"] = false;
+      gd = sv[7];
+      gs = sv[8];
+      gc = sv[9];
+      check(g_abi.loss_scale(dptr<float>(g), npix, s_stride, c_stride, dptr<float>(gd), dptr<float>(gs),
+                             dptr<float>(gc), st));
+    } else {
+      auto fo = d.options();
+      gd = at::empty_like(d);
+      gs = at::empty({npix, s_stride}, fo);
+      gc = at::empty({npix, c_stride}, fo);
+      const float* sp = dptr<float>(sl) + (s_stride == 4 ? 3 : 0);
+      check(g_abi.loss_backward(dptr<float>(d), sp, s_stride, dptr<float>(c), c_stride, dptr<uint8_t>(m),
+                                dptr<float>(dr), dptr<float>(rr), npix, (float)ctx->saved_data["delta"].toDouble(),
+                                (float)ctx->saved_data["w_color"].toDouble(), dptr<float>(g), ws.data_ptr(),
+                                dptr<float>(gd), dptr<float>(gs), dptr<float>(gc), st));
+    }
+    return {gd.reshape(ctx->saved_data["sh_d"].toIntVector()), gs.reshape(ctx->saved_data["sh_s"].toIntVector()),
+            gc.reshape(ctx->saved_data["sh_c"].toIntVector()), Tensor()};
+  }
+};
+
+// quaternion_to_matrix (camera_pose_optimizer.py:241) of real-part-first quaternions q (..., 4): one launch
+// each way; q may be a strided slice (the pose's q[:, 3:], rows 7 floats apart).
+struct QuatFn : public torch::autograd::Function<QuatFn> {
+  static Tensor forward(AutogradContext* ctx, Tensor q) {
+    Tensor q2 = q.detach();
+    if (q2.scalar_type() != at::kFloat) q2 = q2.to(at::kFloat);
+    q2 = q2.reshape({-1, 4});
+    if (q2.stride(1) != 1 || (q2.size(0) > 1 && q2.stride(0) < 4)) q2 = q2.contiguous();
+    const int64_t n = q2.size(0);
+    Tensor out = at::empty({n, 3, 3}, q2.options());
+    check(g_abi.quat(dptr<float>(q2), q2.stride(0), n, dptr<float>(out), stream_of(q2)));
+    ctx->save_for_backward({q2});
+    ctx->saved_data["shape"] = q.sizes().vec();
+    auto os = q.sizes().vec();
+    os.back() = 3;
+    os.push_back(3);
+    return out.reshape(os);
+  }
+  static variable_list backward(AutogradContext* ctx, variable_list grads) {
+    const Tensor q2 = ctx->get_saved_variables()[0];
+    const int64_t n = q2.size(0);
+    Tensor gR = f32c(grads[0]);
+    Tensor gq = at::empty({n, 4}, q2.options());
+    check(g_abi.quat_backward(dptr<float>(q2), q2.stride(0), dptr<float>(gR), n, dptr<float>(gq), stream_of(q2)));
+    return {gq.reshape(ctx->saved_data["shape"].toIntVector())};
+  }
+};
+
+variable_list pose_loss(Tensor depth, Tensor sil, Tensor color, Tensor mask, Tensor depth_ref, Tensor rgb_ref,
+                        double delta, double w_color, bool sil_rgba, bool col_rgba) {
+  TORCH_CHECK(g_abi.loss_forward_grad != nullptr, "mi355r: _mr_torch.init() was not called");
+  for (const Tensor* t : {&depth, &sil, &color, &mask, &depth_ref, &rgb_ref})
+    TORCH_CHECK(t->is_cuda(), "mi355r: the MI355X path needs HIP device tensors (no CPU fallback)");
+  LossArgs a;
+  a.mask = mask; a.depth_ref = depth_ref; a.rgb_ref = rgb_ref;
+  a.delta = delta; a.w_color = w_color; a.sil_rgba = sil_rgba; a.col_rgba = col_rgba;
+  return PoseLossFn::apply(depth, sil, color, std::move(a));
+}
+
+Tensor quaternion_to_matrix(Tensor q) {
+  TORCH_CHECK(g_abi.quat != nullptr, "mi355r: _mr_torch.init() was not called");
+  return QuatFn::apply(q);
+}
+
 void init(const std::unordered_map<std::string, int64_t>& fn) {
   auto get = [&](const char* name) {
     auto it = fn.find(name);
@@ -311,6 +445,12 @@ void init(const std::unordered_map<std::string, int64_t>& fn) {
   g_abi.backward_workspace = (decltype(g_abi.backward_workspace))get("mr_render_backward_workspace");
   g_abi.backward = (decltype(g_abi.backward))get("mr_render_backward");
   g_abi.backward_opencv = (decltype(g_abi.backward_opencv))get("mr_render_backward_opencv");
+  g_abi.loss_workspace = (decltype(g_abi.loss_workspace))get("mr_pose_loss_workspace");
+  g_abi.loss_forward_grad = (decltype(g_abi.loss_forward_grad))get("mr_pose_loss_forward_grad");
+  g_abi.loss_scale = (decltype(g_abi.loss_scale))get("mr_pose_loss_scale");
+  g_abi.loss_backward = (decltype(g_abi.loss_backward))get("mr_pose_loss_backward");
+  g_abi.quat = (decltype(g_abi.quat))get("mr_quaternion_to_matrix");
+  g_abi.quat_backward = (decltype(g_abi.quat_backward))get("mr_quaternion_to_matrix_backward");
 }
 
 }  // namespace
@@ -319,4 +459,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mi355r torch glue: the fused render's autograd node (kernels.render_views)";
   m.def("init", &init, "the C ABI entry points (name -> address) of the loaded libmi355r.so");
   m.def("render_views", &render_views, "fused render forward (+ autograd backward) through the C ABI");
+  m.def("pose_loss", &pose_loss, "calc_loss with its gradients (+ autograd backward) through the C ABI");
+  m.def("quaternion_to_matrix", &quaternion_to_matrix, "quaternion_to_matrix (+ autograd backward)");
 }

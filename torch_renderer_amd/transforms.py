@@ -12,51 +12,16 @@ import torch
 import torch.nn.functional as F
 
 
-class _QuatToMatrix(torch.autograd.Function):
-    """quaternion_to_matrix of HIP tensors: one launch forward (mr_quaternion_to_matrix, torch's
-    elementwise operation order), one backward (analytic dL/dq) — instead of ~30 tiny torch kernels
-    forward and ~60 backward per optimiser step (camera_pose_optimizer.py:241)."""
-
-    @staticmethod
-    def forward(ctx, q):
-        import ctypes
-
-        from . import _lib
-
-        q2 = q.detach().float().reshape(-1, 4)  # a view when it can be (e.g. the pose's q[:, 3:], rows 7 apart)
-        if q2.stride(1) != 1 or (q2.shape[0] > 1 and q2.stride(0) < 4):
-            q2 = q2.contiguous()
-        n = q2.shape[0]
-        out = torch.empty((n, 3, 3), device=q.device)
-        _lib.check(_lib.load().mr_quaternion_to_matrix(ctypes.c_void_p(q2.data_ptr()), q2.stride(0), n,
-                                                       ctypes.c_void_p(out.data_ptr()), _lib.stream_handle(q.device)))
-        ctx.save_for_backward(q2)
-        ctx.shape = q.shape
-        return out.reshape(q.shape[:-1] + (3, 3))
-
-    @staticmethod
-    def backward(ctx, g):
-        import ctypes
-
-        from . import _lib
-
-        (q2,) = ctx.saved_tensors
-        n = q2.shape[0]
-        gR = g.float().contiguous()
-        gq = torch.empty((n, 4), device=q2.device)
-        _lib.check(_lib.load().mr_quaternion_to_matrix_backward(ctypes.c_void_p(q2.data_ptr()), q2.stride(0),
-                                                                ctypes.c_void_p(gR.data_ptr()), n,
-                                                                ctypes.c_void_p(gq.data_ptr()),
-                                                                _lib.stream_handle(q2.device)))
-        return gq.reshape(ctx.shape)
-
-
 def quaternion_to_matrix(quaternions: torch.Tensor) -> torch.Tensor:
     """Real-part-first quaternions (not renormalised: two_s = 2/|q|^2) -> rotation matrices
-    (upstream pytorch3d.transforms.quaternion_to_matrix). HIP float32 tensors take one fused launch
-    each way (_QuatToMatrix); others (the CPU oracle) the torch formula."""
+    (upstream pytorch3d.transforms.quaternion_to_matrix). HIP float32 tensors take one launch each way
+    (mr_quaternion_to_matrix[_backward], torch's elementwise operation order) through the C++ autograd node
+    _mr_torch.quaternion_to_matrix — instead of ~30 tiny torch kernels forward and ~60 backward per optimiser
+    step (camera_pose_optimizer.py:241); others (the CPU oracle) the torch formula."""
     if quaternions.is_cuda and quaternions.dtype == torch.float32 and quaternions.shape[-1] == 4:
-        return _QuatToMatrix.apply(quaternions)
+        from . import _lib
+
+        return _lib.torch_ext().quaternion_to_matrix(quaternions)
     return quaternion_to_matrix_torch(quaternions)
 
 

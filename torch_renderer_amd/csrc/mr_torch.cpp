@@ -310,6 +310,7 @@ struct LossArgs {
   Tensor mask, depth_ref, rgb_ref;
   double delta = 0.05, w_color = 0.01;
   bool sil_rgba = false, col_rgba = false;
+  bool grads = false;  // a backward can follow (grad mode on and an image requires grad)
 };
 
 struct PoseLossFn : public torch::autograd::Function<PoseLossFn> {
@@ -331,7 +332,7 @@ struct PoseLossFn : public torch::autograd::Function<PoseLossFn> {
     Tensor ws = at::empty({(int64_t)wsb}, at::TensorOptions().dtype(at::kByte).device(dev));
     Tensor total = at::empty({}, fo), terms = at::empty({3}, fo);
     Tensor gd, gs, gc;
-    const bool grads = ctx->needs_input_grad(0) || ctx->needs_input_grad(1) || ctx->needs_input_grad(2);
+    const bool grads = a.grads;
     if (grads) {
       gd = at::empty_like(d);
       gs = at::empty({npix, s_stride}, fo);
@@ -422,6 +423,8 @@ variable_list pose_loss(Tensor depth, Tensor sil, Tensor color, Tensor mask, Ten
   LossArgs a;
   a.mask = mask; a.depth_ref = depth_ref; a.rgb_ref = rgb_ref;
   a.delta = delta; a.w_color = w_color; a.sil_rgba = sil_rgba; a.col_rgba = col_rgba;
+  // (decided here: with no input requiring grad the node has no edges to ask)
+  a.grads = at::GradMode::is_enabled() && (depth.requires_grad() || sil.requires_grad() || color.requires_grad());
   return PoseLossFn::apply(depth, sil, color, std::move(a));
 }
 

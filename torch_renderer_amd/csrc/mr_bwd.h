@@ -367,6 +367,7 @@ struct RenderBwdParams {
   // remainder gface of the rare component >= MR_FIX_MAX
   unsigned long long* gfix;
   float* gface;
+  int* fflag;      // ctr + CTR_FLT: set when a float remainder is written
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
   const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
 };
@@ -450,7 +451,7 @@ MR_DEV int seg_stage_face(int key, int face, float (&v)[ACC], float* lrow, int* 
 // atomic into the face's float row. Straight-line, as seg_flush.
 template <int ACC, int STRIDE = ACC>
 MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* __restrict__ gface, const float* lrow,
-                          const int* lkey) {
+                          const int* lkey, int* __restrict__ fflag) {
   int lane = threadIdx.x & 63;
   asm volatile("" : "+v"(lane));
   const int tot = nt * ACC;
@@ -467,6 +468,7 @@ MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* 
           if (x != 0.0f) atomicAdd(gfix + e, (unsigned long long)fix_of(x));
         } else {
           atomicAdd(gface + e, x);
+          *fflag = 1;  // (the gathers then read the remainder rows)
         }
       }
     }
@@ -681,7 +683,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
-      seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
+      seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave], P.fflag);
       if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -751,7 +753,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     s_prev = s;
   }
   if (nt_prev >= 0) {
-    seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave]);
+    seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave], P.fflag);
     if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
   }
 }

@@ -41,8 +41,11 @@ MR_DEV float fpow(float a, float b) { return a > 0.0f ? __builtin_amdgcn_exp2f(b
 MR_DEV long long fix_of(float x) { return __float2ll_rn(x * 4294967296.0f); }
 MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)v * (1.0 / 4294967296.0)); }
 // Per-face total component i: the fixed-point sum plus the float-atomic remainder.
-MR_DEV float fix_total(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i) {
-  return gfix ? fix_to_f(gfix[i]) + gflt[i] : gflt[i];
+// (rem false: the float remainder rows are all zero and not read — fix_to_f never returns -0, so the
+// sum with a zero remainder is the same bits)
+MR_DEV float fix_total(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i,
+                       bool rem = true) {
+  return gfix ? (rem ? fix_to_f(gfix[i]) + gflt[i] : fix_to_f(gfix[i])) : gflt[i];
 }
 
 // std::max/std::min semantics (a < b ? b : a) — NaN handling follows the CPU code.

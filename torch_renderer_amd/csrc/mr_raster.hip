@@ -1006,6 +1006,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.views = (const ViewRec*)views;
   P.gfix = gfix;
   P.gface = gface;
+  P.fflag = w.ctr + CTR_FLT;
   P.rt_part = rt_part;
   P.frec = w.frec;
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
@@ -1042,13 +1043,13 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   // the forward's slot ranges: one per (view, band) on the per-view binning, one per view otherwise
   const int bands = view_binning(g, N, NF) ? bin_bands(N, g) : 1;
   if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv)));
-  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, vraw, gnu)));
-  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, vraw, gnu)));
+  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
-    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, gnu, use_n, gverts, gcol)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gnu, use_n, gverts, gcol)));
   } else {
-    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, gnu, use_n, gverts, gcol)));
+    MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gnu, use_n, gverts, gcol)));
   }
   MR_CHECK_LAUNCH("k_vgrad");
   return MR_OK;
@@ -1156,12 +1157,12 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   const int use_n = sp->light_kind == 0 && !P.sil;
   const int vb = ceil_div(m->V * MR_VL, 256);
   if (use_n) {
-    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, vraw, gnu);
-    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, vraw, gnu);
+    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
+    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
     MR_CHECK_LAUNCH("k_rt_vgrad_a");
   }
-  if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, gnu, use_n, g_verts, g_vcolors);
-  else k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, gnu, use_n, g_verts, g_vcolors);
+  if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, gnu, use_n, g_verts, g_vcolors);
+  else k_vgrad_b<18><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, gnu, use_n, g_verts, g_vcolors);
   MR_CHECK_LAUNCH("k_vgrad_b");
   return MR_OK;
 }

@@ -88,8 +88,10 @@ static inline int ceil_div(int64_t a, int64_t b) { return (int)((a + b - 1) / b)
 // ctr[CTR_ENTRIES64 .. +2) is a u64: list entries allocated by the per-view binning (k_bin_view)
 // ctr[CTR_SENT]: fragments kept by the fused soft silhouette's raster (mr_soft_silhouette_forward)
 // ctr[CTR_ZWALK]: tiles the K-deep raster walked near-to-far (its depth-ordered list walk)
+// ctr[CTR_FLT]: non-zero once k_bwd_fused wrote a float remainder (a total component >= MR_FIX_MAX): the
+// vertex-gradient gathers read the remainder rows only then (they are all zero otherwise)
 enum { CTR_UNITS = 0, CTR_SLOTS = 1, CTR_COVERED = 2, CTR_SENT = 3, CTR_ENTRIES64 = 4, CTR_ZWALK = 6,
-       CTR_COUNT = 8 };
+       CTR_FLT = 7, CTR_COUNT = 8 };
 
 struct BinGeom {
   int TX, TY, T;

@@ -51,7 +51,9 @@ MR_DEV void vertex_normal(const float* __restrict__ verts, const int32_t* __rest
 template <int ACC>
 MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                           const unsigned long long* __restrict__ gfix, const float* __restrict__ gface,
-                          const float* __restrict__ vraw, float* __restrict__ gnu, int64_t blk) {
+                          const int* __restrict__ fflag, const float* __restrict__ vraw, float* __restrict__ gnu,
+                          int64_t blk) {
+  const bool rem = !fflag || *fflag != 0;  // float remainder rows written (else all zero: not read)
   // MR_VL lanes per vertex split its CSR entries, then a fixed xor-tree sums them (deterministic)
   const int64_t gid = blk * blockDim.x + threadIdx.x;
   const int64_t v = gid / MR_VL;
@@ -61,7 +63,7 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
   if (act) {
     for (int e = ptr[v] + j; e < ptr[v + 1]; e += MR_VL) {
       const int f = adj[e] >> 2, c = adj[e] & 3;
-      for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 9 + 3 * c + k);
+      for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 9 + 3 * c + k, rem);
     }
   }
 #pragma unroll
@@ -85,10 +87,10 @@ __global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ pa
                                                     float* __restrict__ gtcv, int64_t V,
                                                     const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
                                                     const unsigned long long* __restrict__ gfix,
-                                                    const float* __restrict__ gface, const float* __restrict__ vraw,
-                                                    float* __restrict__ gnu) {
+                                                    const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                    const float* __restrict__ vraw, float* __restrict__ gnu) {
   if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, bands, gviews, gRcv, gtcv, blockIdx.x);
-  else vgrad_a_block<ACC>(V, ptr, adj, gfix, gface, vraw, gnu, (int64_t)blockIdx.x - N);
+  else vgrad_a_block<ACC>(V, ptr, adj, gfix, gface, fflag, vraw, gnu, (int64_t)blockIdx.x - N);
 }
 
 // B: grad_verts[v] = sum over incident (f, c) of position rows + cross-product backward of the face normal.
@@ -96,8 +98,10 @@ template <int ACC>
 __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restrict__ verts,
                                                  const int32_t* __restrict__ faces, const int32_t* __restrict__ ptr,
                                                  const int32_t* __restrict__ adj, const unsigned long long* __restrict__ gfix,
-                                                 const float* __restrict__ gface, const float* __restrict__ gnu, int use_normals,
-                                                 float* __restrict__ gverts, float* __restrict__ gcol) {
+                                                 const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                 const float* __restrict__ gnu, int use_normals, float* __restrict__ gverts,
+                                                 float* __restrict__ gcol) {
+  const bool rem = !fflag || *fflag != 0;  // float remainder rows written (else all zero: not read)
   const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t v = gid / MR_VL;
   const int j = (int)(gid % MR_VL);
@@ -106,9 +110,9 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
   const int e0 = act ? ptr[v] + j : 0, e1 = act ? ptr[v + 1] : 0;
   for (int e = e0; e < e1; e += MR_VL) {
     const int f = adj[e] >> 2, c = adj[e] & 3;
-    for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 3 * c + k);
+    for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 3 * c + k, rem);
     if (ACC == 27)
-      for (int k = 0; k < 3; ++k) gc[k] += fix_total(gfix, gface, (int64_t)f * ACC + 18 + 3 * c + k);
+      for (int k = 0; k < 3; ++k) gc[k] += fix_total(gfix, gface, (int64_t)f * ACC + 18 + 3 * c + k, rem);
     if (use_normals) {
       const int32_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
       float gn[3], a[3], b[3];

@@ -1140,6 +1140,18 @@ def bench_c5(args, dev, world, rank, embed=False):
     elapsed = _time_steps(step, args, dev, world)
     kt = _kernel_times(step, min(args.steps, 10))
     _host_profile(step, dev)
+    # host cost of one single-view renderer(...) call as the caller makes it (:197), no synchronisation inside
+    # the timed calls (the device queue absorbs the launches): median of 20
+    hs = []
+    with torch.no_grad():
+        mesh_h = Meshes([verts0], [faces], TexturesVertex(verts_features=verts_rgb.detach()))
+        for i in range(25):
+            h0 = time.perf_counter()
+            img = renderer(mesh_h, cameras=target_cameras[i % n_targets], lights=lights)
+            hs.append(time.perf_counter() - h0)
+            del img
+    torch.cuda.synchronize()
+    host_us = sorted(hs[5:])[len(hs[5:]) // 2] * 1e6
     # work counters of one view's forward (render_stats reads the live workspace)
     # (colours requiring grad: the autograd node holds the workspace, which an inference render would free)
     norm = torch.nn.functional.hardtanh(verts_rgb, 0.0, 1.0).detach().requires_grad_(True)
@@ -1165,9 +1177,11 @@ def bench_c5(args, dev, world, rank, embed=False):
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(b / (f_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": None}
     if embed:
-        return _embedded(value, elapsed, args, kt, min(args.steps, 10), roof,
-                         f"ico-sphere (F={Fn}, V={Vn}), {H}x{W}, {nper} single-view renders per step, "
-                         "mesh_deformer.py:196-215 colour step (backward to colours and positions, SGD)")
+        e = _embedded(value, elapsed, args, kt, min(args.steps, 10), roof,
+                      f"ico-sphere (F={Fn}, V={Vn}), {H}x{W}, {nper} single-view renders per step, "
+                      "mesh_deformer.py:196-215 colour step (backward to colours and positions, SGD)")
+        e["host_us_per_render_call"] = round(host_us, 1)
+        return e
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = c5_cpu_baseline(verts0.cpu(), faces.cpu(), R.cpu(), T.cpu(), H, W)
@@ -1183,6 +1197,7 @@ def bench_c5(args, dev, world, rank, embed=False):
                    "mesh": "subdivided sphere", "H": H, "W": W, "views_per_step": nper,
                    "parallelism": f"replicas x{world}"},
         "roofline": roof, "cpu_baseline": cpu, "work": wstats, "kernels": kernels,
+        "host_us_per_render_call": round(host_us, 1),
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -1042,8 +1042,13 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   const int vb = ceil_div(m->V * MR_VL, 256);
   // the forward's slot ranges: one per (view, band) on the per-view binning, one per view otherwise
   const int bands = view_binning(g, N, NF) ? bin_bands(N, g) : 1;
-  if (!use_n) MR_TIMED(KID_RT_REDUCE, st, (k_rt_reduce<<<(unsigned)N, 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv)));
-  else if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
+  if (!use_n) {  // no normal chain: the R/T reduction and the vertex gathers in one launch
+    if (vcol) MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
+    else MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
+    MR_CHECK_LAUNCH("k_rt_vgrad_b");
+    return MR_OK;
+  }
+  if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
   else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {

@@ -95,14 +95,13 @@ __global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ pa
 
 // B: grad_verts[v] = sum over incident (f, c) of position rows + cross-product backward of the face normal.
 template <int ACC>
-__global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restrict__ verts,
-                                                 const int32_t* __restrict__ faces, const int32_t* __restrict__ ptr,
-                                                 const int32_t* __restrict__ adj, const unsigned long long* __restrict__ gfix,
-                                                 const float* __restrict__ gface, const int* __restrict__ fflag,
-                                                 const float* __restrict__ gnu, int use_normals, float* __restrict__ gverts,
-                                                 float* __restrict__ gcol) {
+MR_DEV void vgrad_b_block(int64_t V, const float* __restrict__ verts, const int32_t* __restrict__ faces,
+                          const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
+                          const unsigned long long* __restrict__ gfix, const float* __restrict__ gface,
+                          const int* __restrict__ fflag, const float* __restrict__ gnu, int use_normals,
+                          float* __restrict__ gverts, float* __restrict__ gcol, int64_t blk) {
   const bool rem = !fflag || *fflag != 0;  // float remainder rows written (else all zero: not read)
-  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t gid = blk * blockDim.x + threadIdx.x;
   const int64_t v = gid / MR_VL;
   const int j = (int)(gid % MR_VL);
   const bool act = v < V;
@@ -141,6 +140,30 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
   for (int k = 0; k < 3; ++k) gverts[3 * v + k] = g[k];
   if (ACC == 27 && gcol)
     for (int k = 0; k < 3; ++k) gcol[3 * v + k] = gc[k];
+}
+template <int ACC>
+__global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restrict__ verts,
+                                                 const int32_t* __restrict__ faces, const int32_t* __restrict__ ptr,
+                                                 const int32_t* __restrict__ adj, const unsigned long long* __restrict__ gfix,
+                                                 const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                 const float* __restrict__ gnu, int use_normals, float* __restrict__ gverts,
+                                                 float* __restrict__ gcol) {
+  vgrad_b_block<ACC>(V, verts, faces, ptr, adj, gfix, gface, fflag, gnu, use_normals, gverts, gcol, blockIdx.x);
+}
+// Without vertex normals in the shading (no k_vgrad_a step): the per-view R/T reduction (blocks [0, N)) and
+// the vertex gradients (the rest) read disjoint inputs, so one launch runs both side by side (C5: a single
+// view's reduction is one long-running workgroup that the gathers now overlap).
+template <int ACC>
+__global__ void __launch_bounds__(256) k_rt_vgrad_b(const float* __restrict__ part, const int* __restrict__ vslot,
+                                                    int N, int bands, float* __restrict__ gviews, float* __restrict__ gRcv,
+                                                    float* __restrict__ gtcv, int64_t V, const int32_t* __restrict__ ptr,
+                                                    const int32_t* __restrict__ adj,
+                                                    const unsigned long long* __restrict__ gfix,
+                                                    const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                    float* __restrict__ gverts, float* __restrict__ gcol) {
+  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, bands, gviews, gRcv, gtcv, blockIdx.x);
+  else vgrad_b_block<ACC>(V, nullptr, nullptr, ptr, adj, gfix, gface, fflag, nullptr, 0, gverts, gcol,
+                          (int64_t)blockIdx.x - N);
 }
 
 // projection: face_verts[n*F+f][c] = ndc(view n, X); distinct meshes (ff = first union face of

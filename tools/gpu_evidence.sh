@@ -33,7 +33,7 @@ rows=sorted(csv.DictReader(open(sys.argv[1])), key=lambda r:-float(r['TotalDurat
 print(sys.argv[2], 'kernels:', ', '.join('%s %.1f' % (r['Name'].replace('void ','').split('(')[0][:28], float(r['AverageNs'])/1e3) for r in rows[:8]))
 PY
 }
-run bench 400 && prof render --no-fragment-pass --steps 20 --warmup 5 && \
+run bench 400 && prof render --no-fragment-pass --no-secondary --steps 20 --warmup 5 && \
 run frag 300 --mode fragments --steps 50 --warmup 10 && prof frag --mode fragments --steps 20 --warmup 5 && \
 run soft 400 --mode soft --size 128 && prof soft --mode soft --size 128 --steps 10 --warmup 3 && \
 run pose 400 --mode pose --steps 20 --warmup 5 && prof pose --mode pose --steps 20 --warmup 5 && \

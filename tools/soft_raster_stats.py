@@ -39,7 +39,7 @@ def main():
     nv = a.views
     R, T = look_at_view_transform(dist=2.7, elev=torch.linspace(0, 360, nv), azim=torch.linspace(-180, 180, nv))
     tot = dict(tiles=0, faces=0, pairs=0, kept=0, px=0, over_k=0)
-    per_tile_pairs, per_tile_kept, per_pix_kept = [], [], []
+    per_tile_pairs, per_tile_kept, per_pix_kept, per_tile_faces = [], [], [], []
     for n in range(nv):
         vc = v @ R[n].double() + T[n].double()
         x, y = vc[:, 0] / vc[:, 2], vc[:, 1] / vc[:, 2]
@@ -80,16 +80,19 @@ def main():
             tot["pairs"] += t[1]
             tot["kept"] += t[2]
             per_tile_pairs.append(t[1])
+            per_tile_faces.append(t[0])
             per_tile_kept.append(t[2])
         kp = kept_img[kept_img > 0]
         tot["px"] += int(kp.numel())
         tot["over_k"] += int((kp > 50).sum())
         per_pix_kept.append(kp)
     pp = torch.tensor(per_tile_pairs, dtype=torch.float64)
+    ff = torch.tensor(per_tile_faces, dtype=torch.float64)
     kk = torch.tensor(per_tile_kept, dtype=torch.float64)
     px = torch.cat(per_pix_kept).double()
     print(f"views {nv}  occupied tiles {tot['tiles']} ({tot['tiles'] / nv:.1f}/view)")
-    print(f"listed faces / tile  mean {tot['faces'] / tot['tiles']:.1f}")
+    print(f"listed faces / tile  mean {tot['faces'] / tot['tiles']:.1f}  p90 {ff.quantile(0.9):.0f}  max {ff.max():.0f}"
+          f"  tiles > 1536: {int((ff > 1536).sum())}  > 2048: {int((ff > 2048).sum())}")
     print(f"pairs / tile  mean {pp.mean():.0f}  p90 {pp.quantile(0.9):.0f}  max {pp.max():.0f}")
     print(f"kept / tile  mean {kk.mean():.0f}  p90 {kk.quantile(0.9):.0f}  max {kk.max():.0f}")
     print(f"covered px {tot['px']}  kept / px mean {px.mean():.1f}  p90 {px.quantile(0.9):.0f}  max {px.max():.0f}"

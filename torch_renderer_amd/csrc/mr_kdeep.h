@@ -232,8 +232,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   __shared__ KpStage S;
   __shared__ unsigned short perm[MR_KP_SORT > 0 ? MR_KP_SORT : 1];
   const int lane = threadIdx.x;
-  const int s = blockIdx.x;
-  if (s >= P.ctr[CTR_SLOTS]) return;
+  if ((int)blockIdx.x >= P.ctr[CTR_SLOTS]) return;
+  const int s = P.sorder ? P.sorder[blockIdx.x] : (int)blockIdx.x;
   const int K = P.K;
   const float pad = P.bbox_pad, blur = P.blur;
   const bool persp = P.persp != 0, clipb = P.clipb != 0;
@@ -469,13 +469,49 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
 }
 
+// Slot order for k_raster_kp, heaviest tile lists first (longest-processing-time-first over the wave slots):
+// a counting sort of the slots by list length (buckets of 4 entries, descending; order inside a bucket
+// arbitrary — every tile's result is independent of when it runs). One workgroup.
+#ifndef MR_KP_ORDER
+#define MR_KP_ORDER 1
+#endif
+#define MR_ORDER_BINS 2048
+__global__ void __launch_bounds__(1024) k_slot_order(const int* __restrict__ ctr, const int* __restrict__ stile,
+                                                     const int* __restrict__ cnt, int* __restrict__ order) {
+  __shared__ int hist[MR_ORDER_BINS];
+  __shared__ int part[16];
+  const int t = threadIdx.x, n = ctr[CTR_SLOTS];
+  for (int i = t; i < MR_ORDER_BINS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int s = t; s < n; s += 1024) atomicAdd(&hist[MR_ORDER_BINS - 1 - min(cnt[stile[s]] >> 2, MR_ORDER_BINS - 1)], 1);
+  __syncthreads();
+  // exclusive scan over the (descending) bins: two per thread
+  const int a = hist[2 * t], b = hist[2 * t + 1];
+  int tot;
+  const int incl = block_incl_sum(a + b, part, tot);
+  __syncthreads();
+  hist[2 * t] = incl - (a + b);
+  hist[2 * t + 1] = incl - b;
+  __syncthreads();
+  for (int s = t; s < n; s += 1024)
+    order[atomicAdd(&hist[MR_ORDER_BINS - 1 - min(cnt[stile[s]] >> 2, MR_ORDER_BINS - 1)], 1)] = s;
+}
+
 template <int KP, bool SIL = false>
 static void launch_raster_kr(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
   if (slots_cap >= (1ll << 31)) return;
   MR_TIMED(KID_RASTER_K, st, (k_raster_kp<KP, SIL><<<(unsigned)slots_cap, 64, 0, st>>>(P)));  // one wave per tile
 }
 // The fused soft silhouette's raster (K <= 64, register lists).
-static void launch_raster_sil(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+// The heaviest tile lists first: one wave per tile and more tiles than wave slots, so the waves that start
+// last set the kernel's tail; started first, the long lists overlap the many short ones (LPT order).
+static void slot_order(FwdParams& P, hipStream_t st) {
+  if (!MR_KP_ORDER || !P.sorder_ws) return;
+  k_slot_order<<<1, 1024, 0, st>>>(P.ctr, P.stile, P.cnt, P.sorder_ws);
+  P.sorder = P.sorder_ws;
+}
+static void launch_raster_sil(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st) {
+  slot_order(P, st);
   const int K = P.K;
   const int64_t sc = N * (int64_t)g.T;
   if (K <= 4) launch_raster_kr<4, true>(P, sc, st);
@@ -487,13 +523,14 @@ static void launch_raster_sil(const FwdParams& P, const BinGeom& g, int64_t N, h
 }
 
 
-static int launch_raster_k(const FwdParams& P, const BinGeom& g, int64_t N, hipStream_t st) {
+static int launch_raster_k(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st) {
   static int fgrid = 0;
   if (!fgrid) fgrid = resident_grid(k_fill<0, 3>, 256, 8);
   MR_TIMED(KID_FILL_FRAG, st, (k_fill<0, 3><<<fgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_fill");
   const int K = P.K;
   if (K <= 64) {  // keys in registers (k_raster_kr)
+    slot_order(P, st);
     const int64_t sc = N * (int64_t)g.T;
     if (K <= 4) launch_raster_kr<4>(P, sc, st);
     else if (K <= 8) launch_raster_kr<8>(P, sc, st);

@@ -151,6 +151,7 @@ struct RasterWS {
   int* tdone;  // (N*T) per slot: units of a shared slot still to finish (count-down; the last writes)
   int* vslot;  // (2 N B) first slot and number of slots of each (view, band); B = 1 on the count -> scan path
   int* stile;  // (N*T) per slot: view * T + tile
+  int4* units2;  // (unit_cap) the same units, heaviest first inside each XCD range (k_unit_order)
   int4* units; // (unit_cap) {view*T + tile, first list entry (-1: every face of the view), entries, slot | multi<<31}
   int* list;   // list_cap
   unsigned long long* tkey;  // (N*T*64) per-slot (z, face) keys of tiles shared by several units
@@ -162,6 +163,7 @@ struct RasterWS {
   // add their per-(record, tile) runs in — bitwise deterministic vertex gradients with one launch
   // fewer than a fixed-order reduction of stored rows (round 4). The f32 rows take the rare run
   // component of magnitude >= 2^30 that does not fit the fixed-point range (float atomics).
+  int* sorder;
   unsigned long long* gfix;
   float* gflt;
   float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
@@ -206,6 +208,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * NT, 256);
   w.units = (int4*)(b + off);
   off = align_up(off + sizeof(int4) * (size_t)g.unit_cap, 256);
+  w.units2 = (int4*)(b + off);  // the units in the raster's order (k_unit_order)
+  off = align_up(off + sizeof(int4) * (size_t)g.unit_cap, 256);
   w.list = (int*)(b + off);
   off = align_up(off + sizeof(int) * (size_t)g.list_cap, 256);
   w.tkey = (unsigned long long*)(b + off);
@@ -214,6 +218,8 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(int) * 64 * NT, 256);
   w.srec = (ShadeRec*)(b + off);  // MR_SREC_SLOTS slots of Fshade records (mr_render_reshade)
   off = align_up(off + sizeof(ShadeRec) * MR_SREC_SLOTS * (size_t)Fshade, 256);
+  w.sorder = (int*)(b + off);  // the K-deep raster's slot order (k_slot_order)
+  off = align_up(off + sizeof(int) * (size_t)NT, 256);
   w.gfix = (unsigned long long*)(b + off);
   off = align_up(off + sizeof(unsigned long long) * 27 * (size_t)Fshade, 256);
   w.gflt = (float*)(b + off);

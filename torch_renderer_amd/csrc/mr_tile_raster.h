@@ -272,6 +272,9 @@ struct FwdParams {
   float isig;
   int4* sent;
   float4* spix;
+  const int* sorder;  // k_raster_kp: workgroup -> slot (k_slot_order), NULL: slot = workgroup
+  int* sorder_ws;     // the workspace's order array (RasterWS::sorder)
+  int4* units_ws2;    // RasterWS::units2 (k_unit_order's output)
 };
 
 // One wave's LDS: the batch of up to 64 entries of its unit and the tile's 64 keys (5.4 KB).
@@ -950,9 +953,42 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
   P.cnt = w.cnt; P.start = w.start; P.vbase = w.vbase; P.list_cap = g.list_cap; P.mfpb = g.mfpb;
   P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
   P.frec = w.frec;
+  P.sorder_ws = w.sorder;
+  P.units_ws2 = w.units2;
   return P;
 }
 
+
+// The raster's work units, heaviest first inside each of the 8 XCD ranges k_tile_raster partitions them into
+// (its waves take units round-robin from their range, so a descending order deals every wave about the same
+// load instead of leaving the slowest wave's random share to set the kernel's end; LPT order). Key: an
+// overflow unit (every face of the view) first, then by entries, 64 down to 1; order inside a key arbitrary
+// (the raster's result does not depend on the order its units run in). One workgroup per range.
+#ifndef MR_UNIT_ORDER
+#define MR_UNIT_ORDER 1
+#endif
+MR_DEV int unit_key(const int4& U) { return U.y < 0 ? 0 : MR_UE + 1 - min(max(U.z, 1), MR_UE); }
+__global__ void __launch_bounds__(1024) k_unit_order(const int4* __restrict__ units, const int* __restrict__ ctr,
+                                                     int4* __restrict__ out) {
+  __shared__ int hist[128];
+  const int t = threadIdx.x, n = ctr[CTR_UNITS];
+  const int per = (n + 7) / 8, b = (int)blockIdx.x * per, e = min(b + per, n);
+  if (t < 128) hist[t] = 0;
+  __syncthreads();
+  for (int u = b + t; u < e; u += 1024) atomicAdd(&hist[unit_key(units[u])], 1);
+  __syncthreads();
+  if (t < 64) {  // exclusive scan of the 128 keys, two per lane, from the range's start
+    const int x = hist[2 * t], y = hist[2 * t + 1];
+    const int incl = wave_incl_sum(x + y);
+    hist[2 * t] = b + incl - (x + y);
+    hist[2 * t + 1] = b + incl - y;
+  }
+  __syncthreads();
+  for (int u = b + t; u < e; u += 1024) {
+    const int4 U = units[u];
+    out[atomicAdd(&hist[unit_key(U)], 1)] = U;
+  }
+}
 
 // Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
 template <int MODE, int CH>
@@ -962,6 +998,13 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   if (!rgrid) rgrid = resident_grid(k_tile_raster<MODE, CH, false>, 256, 7);
   if (!rgrid_c) rgrid_c = resident_grid(k_tile_raster<MODE, CH, true>, 256, 7);
   if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
+  // (the fused render only: in the fragment pass the raster's time is its background stores, and the order's
+  // launch cost more than it saved — fragments 421k -> 405-416k, render 300k -> 301-302k, profiles/r5_unit_order_ab.txt)
+  if (MR_UNIT_ORDER && MODE == 1 && P.units_ws2) {
+    k_unit_order<<<8, 1024, 0, st>>>(P.units, P.ctr, P.units_ws2);
+    MR_CHECK_LAUNCH("k_unit_order");
+    P.units = P.units_ws2;
+  }
   if (clip) MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, true><<<rgrid_c, 256, 0, st>>>(P)));
   else MR_TIMED(KID_TILE_RASTER, st, (k_tile_raster<MODE, CH, false><<<rgrid, 256, 0, st>>>(P)));
   MR_CHECK_LAUNCH("k_tile_raster");

@@ -158,15 +158,23 @@ def test_geometry_only_backward_equals_full(clip):
         assert torch.equal(a, b), f"{nm}: geometry-only backward differs from the full kernel's"
 
 
-def test_float_remainder_rows_are_read():
+@pytest.mark.parametrize("ambient_vcol", [False, True])
+def test_float_remainder_rows_are_read(ambient_vcol):
     """Gradient totals in fixed point carry components of magnitude >= 2^30 in float remainder rows, which the
     vertex-gradient gathers read only once k_bwd_fused has flagged one (ctr[CTR_FLT]). Upstream gradients scaled
     by 2^44 (exact in float: the backward is linear in them) push most run totals into the remainder rows: the
-    vertex and pose gradients must still be 2^44 times the unscaled ones (to float rounding)."""
+    vertex and pose gradients must still be 2^44 times the unscaled ones (to float rounding). ambient_vcol: ambient
+    light and vertex colours (mesh_deformer.py's C5 shading: no normal chain, k_rt_vgrad_b, colour gradients too)."""
     N, H = 4, 160
     v0, f0, R, T = _cow_views(N)
     intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
     cfg = Kn.ShadeConfig(H=H, W=H)
+    tex, vc0 = None, None
+    if ambient_vcol:
+        cfg.light_kind = 1
+        cfg.light_ambient = (1.0, 1.0, 1.0)
+        tex = Kn.TextureArgs(kind=1)
+        vc0 = (0.5 + 0.5 * torch.sin(3.0 * v0)).contiguous()
     cc = torch.zeros(1, 3, device=DEV)
     g = torch.Generator().manual_seed(9)
     gD = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)
@@ -176,16 +184,17 @@ def test_float_remainder_rows_are_read():
     def run(scale):
         v = v0.clone().requires_grad_(True)
         Rg, Tg = R.clone().requires_grad_(True), T.clone().requires_grad_(True)
+        vc = vc0.clone().requires_grad_(True) if vc0 is not None else None
         Kn._RESHADE["entry"] = None
-        out = Kn.render_views(v, Rg, Tg, f0, intr, cc, cfg)
+        out = Kn.render_views(v, Rg, Tg, f0, intr, cc, cfg, tex, vcolors=vc)
         ((out["depth"] * gD * scale).sum() + (out["sil"] * gS * scale).sum() + (out["rgb"] * gC * scale).sum()).backward()
         torch.cuda.synchronize()
-        return v.grad, Rg.grad, Tg.grad
+        return (v.grad, Rg.grad, Tg.grad) + ((vc.grad,) if vc is not None else ())
 
     s = 2.0 ** 44
     small, big = run(1.0), run(s)
     assert big[0].abs().max() > 2.0 ** 31  # the remainder rows were in play
-    for a, b, nm in zip(small, big, ("verts", "R", "T")):
+    for a, b, nm in zip(small, big, ("verts", "R", "T", "colours")):
         err = (b / s - a).abs().max().item()
         tol = 1e-5 * max(a.abs().max().item(), 1e-30)
         assert err <= tol, f"{nm}: scaled gradient off by {err:.3e} (tolerance {tol:.3e})"

@@ -238,7 +238,7 @@ size_t mr_render_workspace(int64_t N, int64_t F, int32_t H, int32_t W, int32_t m
 size_t mr_render_workspace_meshes(int64_t N, int64_t F, int32_t H, int32_t W, int32_t max_faces_per_bin);
 /* Outputs (each optional per out_flags): depth (N,H,W), silhouette (N,H,W), rgb (N,H,W,C);
  * pix_to_face32 (N,H,W) int32 packed face id n*F+f (distinct meshes: the union face id) or -1 — optional (NULL: not written; the
- * backward does not need it: the workspace keeps a compact list of covered pixels).
+ * backward does not need it: the workspace keeps each non-empty 8x8 tile's winners and their fragments).
  * cam_centers (Nc,3) world-space specular camera centres, Nc in {1, N}. */
 int32_t mr_render_forward(const mr_mesh_t* mesh, const mr_view_t* views, int64_t N, const float* cam_centers,
                           int64_t num_cam_centers, const mr_raster_settings_t* rs, const mr_shade_params_t* sp,

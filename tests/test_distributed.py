@@ -83,15 +83,17 @@ def _worker_empty_shards(rank, world, port, n_total, q):
         s, e = D.shard_range(n_total, rank, world)
         v = torch.zeros(6, 3, requires_grad=True)
         c = torch.zeros(4, requires_grad=True)   # no gradient on odd ranks
+        unused = torch.zeros(3, requires_grad=True)  # reached by no rank: stays None
         frozen = torch.ones(2)                   # requires no grad anywhere: not reduced
         if e > s:  # this rank's views contribute (view ids s..e-1)
             loss = (v * sum(range(s, e))).sum() + (v * 0).sum()
             if rank % 2 == 0:
                 loss = loss + (c * (e - s)).sum()
             loss.backward()
-        D.allreduce_grads([v, None, c, frozen])
+        D.allreduce_grads([v, None, c, unused, frozen])
         q.put((rank, {"v": None if v.grad is None else v.grad.numpy().copy(),
-                      "c": None if c.grad is None else c.grad.numpy().copy(), "frozen": frozen.grad is None}))
+                      "c": None if c.grad is None else c.grad.numpy().copy(), "frozen": frozen.grad is None,
+                      "unused": unused.grad is None}))
     finally:
         dist.destroy_process_group()
 
@@ -99,7 +101,7 @@ def _worker_empty_shards(rank, world, port, n_total, q):
 def test_gloo_world8_empty_shards_and_missing_grads():
     """Verdict r4 weak #7: with n_total = 5 views over 8 ranks three ranks hold empty shards, and a
     parameter has no .grad on some ranks. Every rank still joins the same all_reduce (zeros
-    materialised), and the sums are exact."""
+    materialised), and the sums are exact; a parameter no rank reached keeps .grad None."""
     world, n_total = 8, 5
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -117,6 +119,7 @@ def test_gloo_world8_empty_shards_and_missing_grads():
         assert torch.equal(torch.from_numpy(res[r]["v"]), torch.full((6, 3), exp_v)), r
         assert torch.equal(torch.from_numpy(res[r]["c"]), torch.full((4,), exp_c)), r
         assert res[r]["frozen"]
+        assert res[r]["unused"], r  # globally unused: .grad None on every rank, as with one rank / DDP
 
 
 def test_shard_range_edges():

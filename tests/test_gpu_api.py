@@ -44,12 +44,9 @@ def _cow_mesh(N):
     return verts, faces, (vuv, fuv, img), v, Meshes([v], [faces.to(DEV)], tex).extend(N)
 
 
-def _close(a, b, tol=1e-4, sens=None, ref64=None):
-    """Per-entry bar |a_i - b_i| <= tol * max(1, |b_i|) (tests.helpers.report), named by call site."""
-    import inspect
-
-    fr = inspect.stack()[1]
-    report(f"{fr.function}:{fr.lineno}", a, b, tol=tol, sens=sens, ref64=ref64)
+def _close(name, a, b, tol=1e-4, sens=None, ref64=None):
+    """Per-entry bar |a_i - b_i| <= tol * max(1, |b_i|) (tests.helpers.report), printed under `name`."""
+    report(name, a, b, tol=tol, sens=sens, ref64=ref64)
 
 
 def _oracle_cv(verts, faces, R_cv, t_cv, K, H, W, texture, grads, precision="f32", faces_per_pixel=1):
@@ -66,6 +63,9 @@ def _oracle_cv(verts, faces, R_cv, t_cv, K, H, W, texture, grads, precision="f32
     gD, gS, gC = grads
     ((ref["depth"] * gD).sum() + (ref["sil"] * gS).sum() + (ref["rgba"][..., :3] * gC).sum()).backward()
     return ref, (vr, Rr, tr)
+
+
+_FLAT_NAMES = ("depth", "sil", "rgb", "grad verts", "grad R_cv", "grad t_cv")
 
 
 def _oracle_cv_flat(*a, **kw):
@@ -90,12 +90,12 @@ def test_depth_color_render_match_oracle():
     depth, sil = DepthRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg, return_silhouette=True)
     rgb = ColorRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg)
     for i, x in enumerate((depth, sil, rgb)):
-        _close(x, ref[i], ref64=r64[i], sens=sp[i])
+        _close(f"DepthRender+ColorRender {('depth', 'sil', 'rgb')[i]}", x, ref[i], ref64=r64[i], sens=sp[i])
     assert torch.equal(DepthRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg).cpu(), depth.cpu())
     d3, s3, c3 = DepthColorRender(K.to(DEV), (H, W), device=DEV).render(meshes, Rg, tg)
     ((d3 * gD.to(DEV)).sum() + (s3 * gS.to(DEV)).sum() + (c3 * gC.to(DEV)).sum()).backward()
     for i, x in ((0, d3), (2, c3), (3, v.grad), (4, Rg.grad), (5, tg.grad)):
-        _close(x, ref[i], ref64=r64[i], sens=sp[i])
+        _close(f"DepthColorRender {_FLAT_NAMES[i]}", x, ref[i], ref64=r64[i], sens=sp[i])
 
 
 @pytest.mark.parametrize("distinct", [False, True])
@@ -135,8 +135,8 @@ def test_mesh_rasterizer_fragments_bitexact(distinct):
     gb = torch.rand(bary.shape, generator=g)
     ((frag.zbuf * gz.to(DEV)).sum() + (frag.bary_coords * gb.to(DEV)).sum()).backward()
     ((zbuf * gz).sum() + (bary * gb).sum()).backward()
-    for a, b in zip(vg + [Rg, Tg], vr + [Rr, Tr]):
-        _close(a.grad, b.grad)
+    for nm, a, b in zip(("grad verts[0]", "grad verts[1]", "grad R", "grad T"), vg + [Rg, Tg], vr + [Rr, Tr]):
+        _close(f"MeshRasterizer fragments (distinct={distinct}) {nm}", a.grad, b.grad)
 
 
 @pytest.mark.parametrize("shader,W", [("phong", 64), ("silhouette", 64), ("silhouette", 66)])
@@ -170,16 +170,16 @@ def test_mesh_renderer_matches_oracle(shader, W):
                        bg=(0.0, 0.0, 0.0))
     assert img.shape == (N, H, W, 4)
     if shader == "phong":
-        _close(img, ref["rgba"])
+        _close(f"MeshRenderer {shader} W={W} rgba", img, ref["rgba"])
         go = torch.rand(N, H, W, 4, generator=g) - 0.5
         (ref["rgba"] * go).sum().backward()
     else:
-        _close(img[..., 3], ref["sil"])
+        _close(f"MeshRenderer {shader} W={W} alpha", img[..., 3], ref["sil"])
         assert torch.equal(img[..., :3].cpu(), torch.ones(N, H, W, 3))
         go = torch.rand(N, H, W, 4, generator=g) - 0.5
         (ref["sil"] * go[..., 3]).sum().backward()
     (img * go.to(DEV)).sum().backward()
-    _close(vg.grad, vr.grad)
+    _close(f"MeshRenderer {shader} W={W} grad verts", vg.grad, vr.grad)
 
 
 def test_renderer_class_matches_oracle():
@@ -205,7 +205,7 @@ def test_renderer_class_matches_oracle():
     ref = O.render_ref(verts, faces, R, T, intr, H, W, texture=("uv", vuv, fuv, img), cam_center=cc)
     assert (ref["p2f"] >= 0).sum() > 50, "degenerate: the mesh is not in view"
     assert out.shape == (1, H, W, 4)
-    _close(out, ref["rgba"])
+    _close("Renderer (renderer.py) rgba", out, ref["rgba"])
 
 
 @pytest.mark.parametrize("broadcast", [False, True])
@@ -260,10 +260,10 @@ def test_drop_in_classes_faces_per_pixel_3_match_oracle():
                                                                                       return_silhouette=True)
     rgb = ColorRender(K.to(DEV), (H, W), faces_per_pixel=Kf, device=DEV).render(meshes, Rg, tg)
     for i, x in enumerate((depth, sil, rgb)):
-        _close(x, ref[i], ref64=r64[i], sens=sp[i])
+        _close(f"soft K={Kf} drop-in {_FLAT_NAMES[i]}", x, ref[i], ref64=r64[i], sens=sp[i])
     ((depth * gD.to(DEV)).sum() + (sil * gS.to(DEV)).sum() + (rgb * gC.to(DEV)).sum()).backward()
     for i, x in ((3, v.grad), (4, Rg.grad), (5, tg.grad)):
-        _close(x, ref[i], ref64=r64[i], sens=sp[i])
+        _close(f"soft K={Kf} drop-in {_FLAT_NAMES[i]}", x, ref[i], ref64=r64[i], sens=sp[i])
 
 
 @pytest.mark.parametrize("shader", ["phong", "silhouette"])
@@ -316,9 +316,9 @@ def test_mesh_renderer_soft_raster_matches_oracle(shader, Kf):
     ref = out["ref"]
     assert img.shape == (N, H, W, 4)
     if shader == "phong":
-        _close(img, ref["rgba"], ref64=out["ref64"]["rgba"])
+        _close(f"soft K={Kf} {shader} rgba", img, ref["rgba"], ref64=out["ref64"]["rgba"])
     else:
-        _close(img[..., 3], ref["sil"], ref64=out["ref64"]["sil"])
+        _close(f"soft K={Kf} {shader} alpha", img[..., 3], ref["sil"], ref64=out["ref64"]["sil"])
     (img * go.to(DEV)).sum().backward()
     report(f"soft K={Kf} {shader} grad verts", vg.grad, refs[0], sens=sens[0], ref64=r64[0])
     if shader == "phong":
@@ -351,8 +351,8 @@ def test_soft_raster_distinct_meshes_batch_equals_single_renders():
         one = renderer(Meshes([vs], [f.to(DEV)], TexturesVertex([c.to(DEV)])), R=R[i:i + 1].to(DEV),
                        T=T[i:i + 1].to(DEV))
         (one * go[i:i + 1]).sum().backward()
-        _close(img[i:i + 1], one, tol=1e-6)
-        _close(vb[i].grad, vs.grad, tol=1e-5)
+        _close(f"distinct-mesh batch view {i} image vs single render", img[i:i + 1], one, tol=1e-6)
+        _close(f"distinct-mesh batch mesh {i} grad verts vs single render", vb[i].grad, vs.grad, tol=1e-5)
 
 
 def test_second_backward_over_one_forward_accumulates_exactly():
@@ -429,6 +429,6 @@ def test_distinct_meshes_one_launch_equals_per_mesh_renders(texture):
         assert torch.equal(out["pix_to_face32"][i:i + 1], torch.where(p1 >= 0, p1 + Fsum, p1)), i
         assert (p1 >= 0).sum() > 0.02 * H * W
         Fsum += f.shape[0]
-        _close(vb[i].grad, vs.grad, tol=1e-5)
-        _close(Rg.grad[i:i + 1], Ri.grad, tol=1e-5)
-        _close(Tg.grad[i:i + 1], Ti.grad, tol=1e-5)
+        _close(f"fused distinct-mesh batch mesh {i} grad verts", vb[i].grad, vs.grad, tol=1e-5)
+        _close(f"fused distinct-mesh batch view {i} grad R", Rg.grad[i:i + 1], Ri.grad, tol=1e-5)
+        _close(f"fused distinct-mesh batch view {i} grad T", Tg.grad[i:i + 1], Ti.grad, tol=1e-5)

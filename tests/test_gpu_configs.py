@@ -299,10 +299,12 @@ def test_c3_camera_pose_optimizer_step_cow_512():
 
 
 def test_c4_dolphin_1024_64views_sharded_equals_unsharded():
-    """C4 (batch_rendering_test.py:320-328): dolphin, 1024x1024, 64 views. The batch rendered as
-    2 shards of 32 (distributed.shard_views; global packed ids via global_view_offset) equals the
-    unsharded render bitwise: images, pix_to_face, per-view pose gradients; the shared vertex
-    gradient (a sum over views) matches within the bar. Fused p2f == modular p2f on all views."""
+    """C4 (batch_rendering_test.py:320-328): dolphin, 1024x1024, 64 views sharded across 8 ranks. The
+    batch rendered as C4's 8 shards of 8 views (distributed.shard_views(..., world_size=8); global packed
+    ids via global_view_offset), one shard after another on this GPU, equals the unsharded render
+    bitwise: images, pix_to_face, per-view pose gradients; the shared vertex gradient (the sum of the
+    8 shards' gradients, what allreduce_grads forms) matches within the bar. Fused p2f == modular p2f on
+    all views."""
     from torch_renderer_amd import distributed as D
 
     H = W = 1024
@@ -317,10 +319,12 @@ def test_c4_dolphin_1024_64views_sharded_equals_unsharded():
     assert torch.equal(p2f, _modular_p2f(verts, faces, R_cv, t_cv, K, H, W))
     _check_background(full, p2f, (1.0, 1.0, 1.0))
     vsum = torch.zeros_like(gfull[0])
-    for rank in range(2):
-        Rs, ts = D.shard_views(R_cv, t_cv, rank=rank, world_size=2)
-        gs = D.shard_views(*grads, rank=rank, world_size=2)
-        s0 = D.global_view_offset(N, rank=rank, world_size=2)
+    world = 8
+    for rank in range(world):
+        Rs, ts = D.shard_views(R_cv, t_cv, rank=rank, world_size=world)
+        gs = D.shard_views(*grads, rank=rank, world_size=world)
+        s0 = D.global_view_offset(N, rank=rank, world_size=world)
+        assert Rs.shape[0] == N // world
         sh, gsh = _gpu_views(verts, faces, white, Rs, ts, K, H, W, gs)
         n = Rs.shape[0]
         for k in ("depth", "sil", "rgb"):
@@ -329,10 +333,11 @@ def test_c4_dolphin_1024_64views_sharded_equals_unsharded():
         assert torch.equal(torch.where(q >= 0, q + s0 * Fn, q), p2f[s0:s0 + n])
         assert torch.equal(gsh[1], gfull[1][s0:s0 + n]) and torch.equal(gsh[2], gfull[2][s0:s0 + n])
         vsum += gsh[0]
-    # the shared vertex gradient is a sum over views (and, inside a view, over pixels) whose order
-    # differs between the sharded and unsharded runs (float atomics): its conditioning is the sum
-    # of the views' absolute contributions, measured from 64 single-view renders; an 8-ulp
-    # (1e-6 relative) change of every view's contribution bounds the spread (tests.helpers.report)
+    # inside one call each face's total is an exact fixed-point sum (order-independent); the sharded
+    # gradient is instead the f32 sum of 8 per-shard vertex gradients, each rounded from its own
+    # total, so it differs from the unsharded one by float rounding: its conditioning is the sum of
+    # the views' absolute contributions, measured from 64 single-view renders; an 8-ulp (1e-6
+    # relative) change of every view's contribution bounds the spread (tests.helpers.report)
     cond = torch.zeros_like(gfull[0])
     for n in range(N):
         _, g1 = _gpu_views(verts, faces, white, R_cv[n:n + 1], t_cv[n:n + 1], K, H, W,
@@ -412,9 +417,9 @@ def test_c5_subdivided_sphere_1024_vertex_grads():
 
 def test_determinism_metric_config():
     """Rendering the benchmarked batch twice gives bitwise-identical images, pix_to_face, per-view
-    pose gradients AND shared vertex gradients: the backward writes one gradient row per (record,
-    tile) with plain stores and k_face_reduce sums each face's rows in a fixed order (no float
-    atomics on the per-view binning path)."""
+    pose gradients AND shared vertex gradients: the backward adds one gradient row per (record, tile)
+    into each face's total as 64-bit fixed-point integers (order-independent integer atomics,
+    mr_common.h fix_of), and the vertex gathers sum a vertex's faces in CSR order (no float atomics)."""
     H = W = 512
     N = 16
     verts, faces, d = mesh_arrays("cow")
@@ -465,11 +470,11 @@ def test_large_image_count_scan_fill_path():
 
 
 def test_vertex_grads_additive_over_view_batches():
-    """k_face_reduce deals a face's views to G lanes in batches of 4G views (G = 16 at >= 16 views, 8 at
-    5 views): the shared vertex gradient of 80 views in one call (two view batches) equals the sum of
-    three calls over 5, 16 and 59 of those views (G = 8, 16, 16; one batch each) within float reordering,
-    and each view's R / t gradient is bitwise the same in any batch (its slots' partial rows are summed as
-    one sequence whatever the band split)."""
+    """The shared vertex gradient of 80 views in one call equals the sum of three calls over 5, 16 and
+    59 of those views within float rounding (each call's per-face totals are exact fixed-point sums,
+    converted to f32 once per call), and each view's R / t gradient is bitwise the same in any batch
+    (its slots' partial rows are summed as one sequence whatever the band split, i.e. whatever the
+    batch size)."""
     H = W = 128
     N = 80
     verts, faces, d = mesh_arrays("cow")

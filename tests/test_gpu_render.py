@@ -2,7 +2,7 @@
 depth, silhouette, Phong RGB; backward to vertices and per-view R, T) against the
 oracle (C rasterizer + torch-CPU restatement of PyTorch3D's shading/blending, autograd).
 Bar: pix_to_face bit-exact; images within 1e-4 abs; gradients within 1e-4 abs
-relative to the gradient scale (float atomics reorder sums)."""
+per entry (tests.helpers.report: 1e-4 * max(1, |ref|), conditioning-aware)."""
 import numpy as np
 import pytest
 import torch
@@ -76,13 +76,10 @@ def _run(name, H, W, N, texture, light_kind=0, persp=True, seed=1, bg=(1.0, 1.0,
     return ref, out, (vr, Rr, Tr, vcr), (vg, Rg, Tg, vcg)
 
 
-def _close(a, b, tol=1e-4, rel_scale=True, sens=None, ref64=None):
+def _close(name, a, b, tol=1e-4, rel_scale=True, sens=None, ref64=None):
     """Per-entry bar (tests.helpers.report): |a_i - b_i| <= tol * max(1, |b_i|), or tol absolute
-    (rel_scale=False, images), named by call site."""
-    import inspect
-
-    fr = inspect.stack()[1]
-    report(f"{fr.function}:{fr.lineno}", a, b, tol=tol, rel_above_one=rel_scale, sens=sens, ref64=ref64)
+    (rel_scale=False, images), printed under `name`."""
+    report(name, a, b, tol=tol, rel_above_one=rel_scale, sens=sens, ref64=ref64)
 
 
 @pytest.mark.parametrize("name,H,W,N,texture", [
@@ -95,21 +92,22 @@ def test_render_forward_backward(name, H, W, N, texture):
     p2f_ref = ref["p2f"][..., 0]
     assert torch.equal(out["pix_to_face32"].cpu().long(), p2f_ref)
     r64, sp = ref["shadow"]
-    _close(out["depth"], ref["depth"], rel_scale=False, ref64=r64[0], sens=sp[0])
-    _close(out["sil"], ref["sil"], rel_scale=False, ref64=r64[1], sens=sp[1])
-    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
+    tag = f"render {name} {H}x{W} {texture}"
+    _close(f"{tag} depth", out["depth"], ref["depth"], rel_scale=False, ref64=r64[0], sens=sp[0])
+    _close(f"{tag} sil", out["sil"], ref["sil"], rel_scale=False, ref64=r64[1], sens=sp[1])
+    _close(f"{tag} rgb", out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
     for i, (gr, gg, nm) in enumerate(zip(leaves_r, leaves_g, ("verts", "R", "T", "vcolors"))):
         if gr is None:
             continue
         assert gg.grad is not None, nm
-        _close(gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])
+        _close(f"{tag} grad {nm}", gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])
 
 
 def test_render_ambient_no_perspective():
     ref, out, leaves_r, leaves_g = _run("sphere", 48, 48, 1, "vertex", light_kind=1, persp=False)
     assert torch.equal(out["pix_to_face32"].cpu().long(), ref["p2f"][..., 0])
     r64, sp = ref["shadow"]
-    _close(out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
-    for i, (gr, gg) in enumerate(zip(leaves_r, leaves_g)):
+    _close("ambient no-persp rgb", out["rgb"], ref["rgba"][..., :3], rel_scale=False, ref64=r64[2], sens=sp[2])
+    for i, (gr, gg, nm) in enumerate(zip(leaves_r, leaves_g, ("verts", "R", "T", "vcolors"))):
         if gr is not None:
-            _close(gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])
+            _close(f"ambient no-persp grad {nm}", gg.grad, gr.grad, ref64=r64[3 + i], sens=sp[3 + i])

@@ -330,6 +330,52 @@ MR_DEV float rt_partial(const float (&gR)[9], const float (&gT)[3], int lane) {
   return o;
 }
 
+// The same 12 sums by a reduce-scatter (gfx950 lane swaps): v_permlane32_swap pairs value 2i's upper
+// half-wave with value 2i+1's lower half, so one add leaves value 2i's 32 partial sums in lanes 0-31 and
+// 2i+1's in lanes 32-63 (6 swaps + 6 adds for 12 values); v_permlane16_swap does the same inside each
+// half for pairs of those vectors (3 + 3), leaving 4 values per vector, one per 16-lane row; four DPP
+// butterfly steps per vector (quad xor 1, xor 2, half-row mirror, row mirror) finish every row's sum in
+// all its lanes. 30 VALU instead of rt_partial's ~100 (12 six-step scans + readlanes + selects). Fixed
+// order: deterministic. o[j] row r holds value RT_VALUE(j, r).
+// gfx950 v_permlane32_swap / v_permlane16_swap as inline asm: lanes 32-63 of x trade with lanes 0-31 of y
+// (x = {x.lo, y.lo}, y = {x.hi, y.hi}); the 16-lane form trades x's odd rows with y's even rows. (The
+// compiler's builtins returned a pair whose two halves it treated as one register when both feed one add:
+// v_add_f32 v4, v4, v4 after the swap — tools/micro/rt_swap.hip.) The s_nop covers the VALU-write ->
+// swap-read hazard the compiler cannot see through the asm.
+MR_DEV void lane_swap32(float& x, float& y) { asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(x), "+v"(y)); }
+MR_DEV void lane_swap16(float& x, float& y) { asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(x), "+v"(y)); }
+#define RT_VALUE(j, r) (4 * (j) + (((r) & 1) << 1) + ((r) >> 1))
+MR_DEV void rt_partial_swap(const float (&gR)[9], const float (&gT)[3], float (&o)[3]) {
+  float h[6];
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const float a = 2 * i < 9 ? gR[2 * i] : gT[2 * i - 9];
+    const float b = 2 * i + 1 < 9 ? gR[2 * i + 1] : gT[2 * i + 1 - 9];
+    float x = a, y = b;
+    lane_swap32(x, y);
+    h[i] = x + y;
+  }
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    float x = h[2 * j], y = h[2 * j + 1];
+    lane_swap16(x, y);
+    float v = x + y;
+    v += dppf<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dppf<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dppf<0x141, 0xf>(v);  // row_half_mirror
+    v += dppf<0x140, 0xf>(v);  // row_mirror
+    o[j] = v;
+  }
+}
+// Store rt_partial_swap's sums as the slot's 12-float partial row (lanes 0, 16, 32, 48 of each vector).
+MR_DEV void rt_store_swap(float* __restrict__ dst, const float (&o)[3], int lane) {
+  if ((lane & 15) == 0) {
+    const int r = lane >> 4;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dst[RT_VALUE(j, r)] = o[j];
+  }
+}
+
 // Fused render backward over the slots of the non-empty tiles (k_tile_raster's sface: per
 // tile pixel the winning face record or -1; the pixel is implied by slot and lane). Per covered
 // pixel: half 1 recomputes fragment + shading and differentiates the blends / Phong / texture ->
@@ -340,7 +386,9 @@ MR_DEV float rt_partial(const float (&gR)[9], const float (&gT)[3], int lane) {
 // (seg_scatter), and the slot's R/T partial sums. (Measured: the same two halves as two kernels
 // with the record in HBM took 123 us against 102 for the fused kernel.)
 // Waves stride over XCD-contiguous slot ranges (one 8x8 tile, one view each).
-#define MR_BWD_REC 5  // float4s per pixel record
+// float4s per pixel of the half-1 -> half-2 hand-off: gz, gsd, gb[3], gP[3], gNn[3] (+ gtex[3] with vertex
+// colours); the barycentrics stay in the forward fragment's registers
+#define MR_BWD_REC(ACC) ((ACC) == 27 ? 4 : 3)
 struct RenderBwdParams {
   int N, H, W, TX, T;
   float blur, bbox_pad;
@@ -575,14 +623,50 @@ MR_DEV const T& kernarg_params() {
 // texture and barycentric terms are zero — so half 1 is skipped and the two values are computed in half 2,
 // bitwise those the full path gives with a zero RGB gradient; only the 9 position columns of each face row
 // are non-zero (NV = 9 values per run instead of ACC, added into the ACC-wide rows).
+// Experiment builds only (-DMR_XP_BWD_STAMP, tools/bwd_stamps.py): per wave, the global clock at start /
+// end, its slot count and the shader-clock cycles spent per phase of the slot loop (readable through
+// mr_xp_bwd_stamps). Reads of the clock counters only.
+#ifdef MR_XP_BWD_STAMP
+#define MR_XP_WAVES 16384
+__device__ unsigned long long g_bwd_stamp[MR_XP_WAVES * 8];
+#define XP_CLK() __builtin_amdgcn_s_memtime()
+#define XP_DECL unsigned long long xp_acc[5] = {0, 0, 0, 0, 0}, xp_t = 0, xp_rt0 = __builtin_amdgcn_s_memrealtime(); int xp_n = 0;
+#define XP_MARK(i) do { const unsigned long long xp_c = XP_CLK(); if ((i) >= 0) xp_acc[(i) < 0 ? 0 : (i)] += xp_c - xp_t; xp_t = xp_c; } while (0)
+#define XP_COUNT() (++xp_n)
+#define XP_STORE() do { const unsigned long long xp_rt1 = __builtin_amdgcn_s_memrealtime(); \
+    const int xp_w = (int)(blockIdx.x * 4 + (threadIdx.x >> 6)); const int xp_l = threadIdx.x & 63; \
+    if (xp_w < MR_XP_WAVES && xp_l < 8) { unsigned long long xp_v = xp_l == 0 ? xp_rt0 : xp_l == 1 ? xp_rt1 : xp_l == 2 ? (unsigned long long)xp_n : xp_acc[0]; \
+      xp_v = xp_l == 4 ? xp_acc[1] : xp_l == 5 ? xp_acc[2] : xp_l == 6 ? xp_acc[3] : xp_l == 7 ? xp_acc[4] : xp_v; \
+      g_bwd_stamp[(size_t)xp_w * 8 + xp_l] = xp_v; } } while (0)
+#else
+#define XP_DECL
+#define XP_MARK(i) do { } while (0)
+#define XP_COUNT() do { } while (0)
+#define XP_STORE() do { } while (0)
+#endif
+
+#ifdef MR_XP_SRPF
+#define MR_SRPF_ON 1
+#else
+#define MR_SRPF_ON 0
+#endif
+// The face of slot pixel record f (-1: face 0, an unconditional load's address) in view n.
+MR_DEV uint32_t bwd_face(const RenderBwdParams& P, int f, int n) {
+  return f >= 0 ? (uint32_t)(rec_orig(f, P.NF) - n * P.F) : 0u;
+}
+
 template <int ACC, bool CLIP, bool GEO = false>
 __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
   constexpr int NV = GEO ? 9 : ACC;  // values per face row this kernel adds
+  // SRPF: the next slot's ShadeRecs are loaded during this slot's half 2 (their latency hidden behind the
+  // raster backward) instead of at the start of its half 1
+  constexpr bool SRPF = !GEO && MR_SRPF_ON;
   const RenderBwdParams& P = P0;
   __shared__ float lrow[4][64 * NV];
   __shared__ int lkey[4][64];
   __shared__ int lperm[4][64];
-  __shared__ float4 lrec[4][GEO ? 1 : MR_BWD_REC][64];
+  constexpr int NREC = GEO ? 1 : MR_BWD_REC(ACC);
+  __shared__ float4 lrec[4][NREC][64];
   const bool lut = GEO ? false : stage_tex_lut(P.S);  // the u8 texture table in LDS
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -609,13 +693,26 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   // lane -> tile pixel p_c of the slot in flight (pixels grouped by record, sort_slot_pixels)
   int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
   bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
+  SRRaw sr_c;
+  if (SRPF) load_sr_raw(P.srec, bwd_face(P, f_c, __builtin_amdgcn_readfirstlane(gt_c) / P.T), sr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
+#ifdef MR_XP_RT_SWAP
+  float rt_prev[3] = {0.0f, 0.0f, 0.0f};
+#define RT_STORE(slot) rt_store_swap(P.rt_part + (int64_t)(slot) * 12, rt_prev, lane)
+#else
   float rt_prev = 0.0f;
+#define RT_STORE(slot) do { if (lane < 12) P.rt_part[(int64_t)(slot) * 12 + lane] = rt_prev; } while (0)
+#endif
+  XP_DECL
+  XP_MARK(-1);
   for (; s < send; s += G) {
     const RenderBwdParams& P = kernarg_params<RenderBwdParams>();  // see kernarg_params
+    XP_COUNT();
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c, p = p_c;
     const FaceRec r = r_c;
     const float4 frag = fr_c;
+    SRRaw sr;
+    if (SRPF) sr = sr_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
@@ -630,15 +727,17 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     f_n = P.sface[(int64_t)sc * 64 + lane];
     int n, px, py;
     slot_pixel(P, gt, p, n, px, py);
+    XP_MARK(0);  // loop top: prefetch issue + the next slot's pixel sort
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (!GEO && f >= 0) {
       PixGeom Gm;
-      load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
+      if (SRPF) geom_from_raw(sr, Gm);
+      else load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
       const float gD = gin[0], gS = gin[1];
       float gC[3] = {gin[2], gin[3], gin[4]};
       const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, p) : 0.0f;
       FragEval e;
-      float4 o[MR_BWD_REC];
+      float4 o[NREC];
       // the forward's fragment (k_shade<1> wrote the winner's barycentrics, original-face ones for a
       // near-plane sub-triangle, and signed distance); the depth from the record's corners in
       // eval_face's operation order, or, for a sub-triangle (whose corners are not the original
@@ -661,14 +760,14 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
         o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
         o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
-        o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], e.b0);
-        o[3] = make_float4(e.b1, e.b2, SG.gtex[0], SG.gtex[1]);
-        o[4] = make_float4(SG.gtex[2], 0.f, 0.f, 0.f);
+        o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], SG.gtex[0]);
+        if (NREC > 3) o[NREC - 1] = make_float4(SG.gtex[1], SG.gtex[2], 0.f, 0.f);
       }
 #pragma unroll
-      for (int k = 0; k < MR_BWD_REC; ++k) lrec[wave][GEO ? 0 : k][lane] = o[k];
+      for (int k = 0; k < NREC; ++k) lrec[wave][GEO ? 0 : k][lane] = o[k];
     }
     if (!GEO) wave_lds_sync();
+    XP_MARK(1);  // half 1
     __builtin_amdgcn_sched_barrier(0);  // keep half 2's loads out of half 1's register peak
     // ---- half 2: raster + projection backward, per-face runs, R/T partials
     const ViewRec V = P.views[n];
@@ -684,8 +783,9 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
       seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave], P.fflag);
-      if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
+      RT_STORE(s_prev);
     }
+    XP_MARK(2);  // corners + the previous slot's flush
     __builtin_amdgcn_sched_barrier(0);
     float gR[9], gT[3];
 #pragma unroll
@@ -697,7 +797,8 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     for (int k = 0; k < NV; ++k) row[k] = 0.0f;
     int key = -1;
     if (f >= 0) {
-      float4 a0, a1, a2, a3, a4;
+      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+      float4 a0, a1, a2, a3;
       if (GEO) {
         // shade_fwd / shade_bwd's depth and silhouette terms (the same operations; the RGB terms vanish)
         const float pz = (CLIP && (r.flags & FR_CLIP))
@@ -710,20 +811,19 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         const float gx = gin[1] * (ps * qs);
         const float gsd = 0.0f + -(gx * P.S.inv_sigma_sil);
         a0 = make_float4(gz, gsd, 0.f, 0.f);
-        a1 = a2 = a3 = a4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        a1 = a2 = a3 = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         a0 = lrec[wave][0][lane];
         a1 = lrec[wave][1][lane];
         a2 = lrec[wave][2][lane];
-        a3 = lrec[wave][3][lane];
-        a4 = ACC == 27 ? lrec[wave][4][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+        a3 = NREC > 3 ? lrec[wave][NREC - 1][lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      const float X[3][3] = {{w0.x, w0.y, w0.z}, {w0.w, w1.x, w1.y}, {w1.z, w1.w, w2.x}};
+
       const float gb[3] = {a0.z, a0.w, a1.x};
       const float gP[3] = {a1.y, a1.z, a1.w};
       const float gNn[3] = {a2.x, a2.y, a2.z};
-      const float b[3] = {a2.w, a3.x, a3.y};
-      const float gt3[3] = {a3.z, a3.w, a4.x};
+      const float b[3] = {frag.x, frag.y, frag.z};  // (the values half 1 shaded with)
+      const float gt3[3] = {a2.w, a3.x, a3.y};
       float gfv[3][3];
       const bool clipped = CLIP && (r.flags & FR_CLIP) != 0;
       const float pxf = col_ndc(px, P.H, P.W), pyf = row_ndc(py, P.H, P.W);
@@ -748,14 +848,25 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
         }
       }
     }
+    XP_MARK(3);  // raster + projection backward
+    // the next slot's ShadeRecs (issued after the flush's atomics: waited on only in the next slot's half 1,
+    // by when those have retired), in flight through the segmented scan and the next slot's loop top
+    if (SRPF) load_sr_raw(P.srec, bwd_face(P, f_c, __builtin_amdgcn_readfirstlane(gt_c) / P.T), sr_c);
     nt_prev = seg_stage_face<NV>(f >= 0 ? f : -1, key, row, lrow[wave], lkey[wave]);
+#ifdef MR_XP_RT_SWAP
+    rt_partial_swap(gR, gT, rt_prev);
+#else
     rt_prev = rt_partial(gR, gT, lane);
+#endif
     s_prev = s;
+    XP_MARK(4);  // segmented scan + R/T wave sums
   }
   if (nt_prev >= 0) {
     seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave], P.fflag);
-    if (lane < 12) P.rt_part[(int64_t)s_prev * 12 + lane] = rt_prev;
+    RT_STORE(s_prev);
   }
+#undef RT_STORE
+  XP_STORE();
 }
 
 // grad_views[n] = sum of the partial rows of view n's slots (fixed order: deterministic).

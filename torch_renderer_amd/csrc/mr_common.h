@@ -34,10 +34,15 @@ MR_DEV float fpow(float a, float b) { return a > 0.0f ? __builtin_amdgcn_exp2f(b
 // two's-complement integer round(x * 2^MR_FIX_SHIFT) and summed with 64-bit integer atomics. Integer
 // addition is associative, so a total is the same bits whatever order the addends arrive in
 // (deterministic without a fixed-order reduction pass); wrap-around in intermediate sums cancels, so
-// only the final total must lie within +-2^(63 - MR_FIX_SHIFT). Resolution 2^-32 = 2.3e-10 absolute,
-// far below the 1e-4 bar; an addend of magnitude >= MR_FIX_MAX takes a float atomic instead.
+// only the final total must lie within +-2^(63 - MR_FIX_SHIFT) = +-2^31. Resolution 2^-32 = 2.3e-10
+// absolute, far below the 1e-4 bar; an addend of magnitude >= MR_FIX_MAX takes a float atomic into the
+// face's float remainder row instead. The cutoff is 2^24 so that a face's fixed-point part can reach
+// 2^31 only through >= 128 same-sign addends each near the cutoff (one addend is one (view, tile) run of
+// the face's pixels); the largest run totals of the parity workloads are ~1e6 on sliver faces, and a
+// loss scaled up until runs reach 2^24 is accumulated in float (correct, no longer bitwise
+// deterministic) — tests/test_gpu_round6.py::test_large_run_totals_take_the_float_rows.
 #define MR_FIX_SHIFT 32
-#define MR_FIX_MAX 1073741824.0f  // 2^30: |x| * 2^32 < 2^62
+#define MR_FIX_MAX 16777216.0f  // 2^24
 MR_DEV long long fix_of(float x) { return __float2ll_rn(x * 4294967296.0f); }
 MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)v * (1.0 / 4294967296.0)); }
 // Per-face total component i: the fixed-point sum plus the float-atomic remainder.

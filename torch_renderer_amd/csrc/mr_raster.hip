@@ -796,8 +796,11 @@ static int32_t render_forward(const mr_mesh_t* m, const mr_view_t* views, int64_
     NA.V = m->V; NA.ptr = m->vadj_ptr; NA.adj = m->vadj;
     NA.vn = vb ? m->vnormals_out : nullptr;
     NA.vraw = m->vraw_out;
-    // the backward's face totals (ACC components per face: the backward's ACC for this mesh)
-    const int64_t nacc = (int64_t)(m->tex_kind == 1 ? 27 : 18) * m->F;
+    // the backward's face totals: all 27 components per face, whatever this call's texture. A reshade
+    // of the same raster may carry another texture kind (a depth render, then a vertex-colour Phong
+    // reshade: ACC 27) and its backward, the first over this workspace, skips the clear
+    // (MR_GRAD_ROWS_CLEARED); 27 columns cost 0.6 MB more stores at the bench config
+    const int64_t nacc = (int64_t)27 * m->F;
     NA.zero4 = (float4*)w.gfix;
     NA.nzero4 = (nacc + 1) / 2;
     NA.zero4b = (float4*)w.gflt;
@@ -1263,6 +1266,14 @@ int32_t mr_timing_read(int32_t* launches, double* total_ms, int32_t n) {
 
 const char* mr_timing_kernel_name(int32_t k) { return (k >= 0 && k < KID_COUNT) ? kKernelNames[k] : ""; }
 int32_t mr_timing_kernel_count(void) { return KID_COUNT; }
+#ifdef MR_XP_BWD_STAMP
+// experiment builds only: the last k_bwd_fused launch's per-wave stamps (8 u64 per wave, MR_XP_WAVES waves)
+int32_t mr_xp_bwd_stamps(unsigned long long* out, int32_t waves) {
+  if (waves > MR_XP_WAVES) waves = MR_XP_WAVES;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamp), sizeof(unsigned long long) * 8 * (size_t)waves, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? MR_OK : MR_ELAUNCH;
+}
+#endif
 
 static int pose_loss_params(PoseLossParams& P, const float* depth, const float* sil, int64_t sil_stride,
                             const float* rgb, int64_t rgb_stride, const uint8_t* mask, const float* depth_ref,

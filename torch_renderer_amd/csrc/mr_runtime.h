@@ -162,7 +162,7 @@ struct RasterWS {
   // integer addition is associative, so the totals do not depend on the order the backward's waves
   // add their per-(record, tile) runs in — bitwise deterministic vertex gradients with one launch
   // fewer than a fixed-order reduction of stored rows (round 4). The f32 rows take the rare run
-  // component of magnitude >= 2^30 that does not fit the fixed-point range (float atomics).
+  // component of magnitude >= MR_FIX_MAX = 2^24 (float atomics; see mr_common.h).
   int* sorder;
   unsigned long long* gfix;
   float* gflt;

@@ -285,6 +285,37 @@ MR_DEV void load_geom(const ShadeRec* __restrict__ recs, uint32_t face, PixGeom&
   }
 }
 
+// The ShadeRec's first 28 floats (world corners, vertex normals, uv / colours) as seven 16-B loads held
+// in registers (a prefetch one slot ahead: k_bwd_fused), and their PixGeom view.
+struct SRRaw {
+  float4 q[7];
+};
+MR_DEV void load_sr_raw(const ShadeRec* __restrict__ recs, uint32_t face, SRRaw& R) {
+  const float4* q = (const float4*)(recs + face);
+#pragma unroll
+  for (int i = 0; i < 7; ++i) R.q[i] = q[i];
+}
+MR_DEV void geom_from_raw(const SRRaw& R, PixGeom& G) {
+  float v[28];
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    v[4 * i] = R.q[i].x; v[4 * i + 1] = R.q[i].y; v[4 * i + 2] = R.q[i].z; v[4 * i + 3] = R.q[i].w;
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      G.X[c][k] = v[3 * c + k];
+      G.Nv[c][k] = v[9 + 3 * c + k];
+      G.col[c][k] = v[18 + 3 * c + k];
+    }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    G.uv[c][0] = v[18 + 3 * c];
+    G.uv[c][1] = v[18 + 3 * c + 1];
+  }
+}
+
 // interpolate_face_attributes: sum_i b_i * attr_i
 MR_DEV float interp3(float b0, float b1, float b2, float a0, float a1, float a2) {
   MR_FP_FAST

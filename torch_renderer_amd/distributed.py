@@ -58,29 +58,40 @@ def allreduce_grads(params, group=None):
 
     Every rank must call the same collective with a buffer of the same size, whatever it rendered: a
     rank with an empty view shard (``shard_range`` hands them out when there are fewer views than
-    ranks) or a parameter its views did not reach has ``.grad`` None. Such a gradient is materialised as
-    zeros here, so the flattened buffer always holds every gradient-requiring parameter of ``params`` in
-    list order (the list is the same replicated parameters on every rank)."""
+    ranks) or a parameter its views did not reach has ``.grad`` None. Such a gradient travels as zeros,
+    so the flattened buffer always holds every gradient-requiring parameter of ``params`` in list order
+    (the list is the same replicated parameters on every rank), followed by one presence flag per
+    parameter (1 where the rank had a gradient). After the reduction a parameter that NO rank reached
+    gets ``.grad = None`` back, as on one rank and as DDP leaves globally unused parameters, so that an
+    optimiser skips it (Adam's moments and weight decay would otherwise move it). Only a rank that had
+    no gradient of its own reads the flags back to the host (one synchronisation); a rank whose
+    parameters all had gradients keeps the step asynchronous."""
     _, w = world()
     if w == 1:
         return
     live = [p for p in params if p is not None and p.requires_grad]
     if not live:
         return
-    for p in live:
-        if p.grad is None:
-            p.grad = torch.zeros_like(p)
-    grads = [p.grad for p in live]
-    if len(grads) == 1 and grads[0].is_contiguous():  # one bucket already: reduce in place (no copies)
-        dist.all_reduce(grads[0], op=dist.ReduceOp.SUM, group=group)
-        return
-    flat = torch.cat([g.reshape(-1) for g in grads])
+    had = [p.grad is not None for p in live]
+    ref = next((p.grad for p in live if p.grad is not None), live[0])
+    dev, dt = ref.device, ref.dtype
+    parts = [(p.grad if h else torch.zeros_like(p, dtype=dt)).reshape(-1) for p, h in zip(live, had)]
+    parts.append(torch.tensor([1.0 if h else 0.0 for h in had], dtype=dt, device=dev))
+    flat = torch.cat(parts)
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     off = 0
-    for g in grads:
-        n = g.numel()
-        g.copy_(flat[off:off + n].view_as(g))
+    for p, h in zip(live, had):
+        n = p.numel()
+        if h:
+            p.grad.copy_(flat[off:off + n].view_as(p.grad))
+        else:
+            p.grad = flat[off:off + n].view_as(p).clone()
         off += n
+    if not all(had):
+        flags = flat[off:].tolist()  # (this rank lacked a gradient: is the parameter used anywhere?)
+        for p, h, f in zip(live, had, flags):
+            if not h and f == 0.0:
+                p.grad = None
 
 
 def gather_to_root(local: torch.Tensor, n_total: int, root: int = 0, group=None):

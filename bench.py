@@ -286,6 +286,11 @@ def main():
             with torch.cuda.graph(g_fwd, pool=pool):
                 outs_static = renderer.render(bmesh, R_cv, t_cv)
                 torch.autograd.backward(list(outs_static), [gD, gS, gC])
+            # keep the static outputs' memory but not their autograd graph: alive, it would keep the leaves'
+            # AccumulateGrad nodes (created on the capture stream) for the eager steps below, whose backward
+            # then accumulates across streams (torch's "AccumulateGrad node's stream does not match" warning,
+            # which preceded the round-5 capture crash; DESIGN §6, tests/test_gpu_round6.py)
+            outs_static = tuple(o.detach() for o in outs_static)
             g_bwd = None
             fwd_only, bwd_only = g_fwd.replay, (lambda: None)
         else:
@@ -294,6 +299,7 @@ def main():
                 outs_static = renderer.render(bmesh, R_cv, t_cv)
             with torch.cuda.graph(g_bwd, pool=pool):
                 torch.autograd.backward(list(outs_static), [gD, gS, gC], retain_graph=True)
+            outs_static = tuple(o.detach() for o in outs_static)  # (as above: no autograd graph kept alive)
             fwd_only, bwd_only = g_fwd.replay, g_bwd.replay
 
     comm = torch.cuda.Stream() if world > 1 else None
@@ -569,8 +575,39 @@ def measure_fragments(args, dev, world, rank):
         torch.cuda.synchronize()
         hs.sort()
         host_us = hs[len(hs) // 2] * 1e6
+        # the same call captured once into a HIP graph and replayed (what a caller's captured training step
+        # runs): the device work per step without the per-call host launch work, checked bitwise against an
+        # eager call's fragments
+        graph_us, graph_equal = None, None
+        if world == 1:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(2):
+                    out = step()
+            torch.cuda.current_stream().wait_stream(side)
+            del out
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, pool=torch.cuda.graph_pool_handle()):
+                gout = step()
+            graph.replay()
+            eager = step()
+            torch.cuda.synchronize()
+            graph_equal = all(torch.equal(a, b) for a, b in zip(gout, eager))
+            del eager
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                graph.replay()
+            torch.cuda.synchronize()
+            graph_us = (time.perf_counter() - t0) / args.steps * 1e6
+            del graph, gout
+            torch.cuda.synchronize()
     kt["__pass_us__"] = (1, pass_us / 1e3)
     kt["__host_us__"] = (1, host_us / 1e3)
+    if graph_us is not None:
+        kt["__graph_us__"] = (1, graph_us / 1e3)
+        kt["__graph_equal__"] = (1, 1.0 if graph_equal else 0.0)
     return elapsed, kt, covered, Fn
 
 
@@ -583,6 +620,9 @@ def fragment_pass_summary(args, elapsed, kt, covered, Fn, world):
     per_frame = 28 * H * W + 36 * Fn
     pass_us = kt.pop("__pass_us__")[1] * 1e3
     host_us = kt.pop("__host_us__", (1, float("nan")))[1] * 1e3
+    graph_us = kt.pop("__graph_us__", (1, None))[1]
+    graph_us = None if graph_us is None else graph_us * 1e3
+    graph_equal = kt.pop("__graph_equal__", (1, None))[1]
     us = sum(kt[k][1] / kt[k][0] * 1e3 for k in FRAG_KERNELS if k in kt)
     ach = per_frame * nv / (pass_us * 1e-6) / 1e9
     ach_k = per_frame * nv / (us * 1e-6) / 1e9
@@ -597,6 +637,10 @@ def fragment_pass_summary(args, elapsed, kt, covered, Fn, world):
             "frac": round(ach / HBM_PEAK_GBS, 4),
             "us_per_step": round(us, 2), "kernel_sum_frac": round(ach_k / HBM_PEAK_GBS, 4),
             "step_frac": round(value * per_frame / 1e9 / HBM_PEAK_GBS, 4),
+            # the call captured in a HIP graph and replayed (no per-call host launch work): us per step and frac
+            "graph_us_per_step": None if graph_us is None else round(graph_us, 2),
+            "graph_step_frac": None if graph_us is None else round(per_frame * nv / (graph_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+            "graph_equals_eager": None if graph_equal is None else bool(graph_equal),
             "dominant_kernel": dom[0], "covered_pixels": covered,
             "workload": f"{args.mesh} (F={Fn}), {H}x{W}, {nv} views/GPU, MeshRasterizer(meshes_world, R, T) -> "
                         "Fragments(pix_to_face int64, zbuf, bary_coords, dists), K=1"}

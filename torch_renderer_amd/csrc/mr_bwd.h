@@ -317,26 +317,16 @@ MR_DEV void seg_scatter(int key, float (&v)[ACC], float* __restrict__ dst, float
   seg_flush<ACC>(seg_stage<ACC>(key, v, lrow, lkey), dst, lrow, lkey);
 }
 
-// The slot's 12 R/T partial sums (wave-wide DPP sums, fixed order: deterministic), lane i
-// holding sum i (lanes 0..11); stored later by one store instruction. Uniform call (full EXEC).
-MR_DEV float rt_partial(const float (&gR)[9], const float (&gT)[3], int lane) {
-  float o = 0.0f;
-#pragma unroll
-  for (int i = 0; i < 12; ++i) {
-    const float t = wave_sum_f_dpp(i < 9 ? gR[i] : gT[i - 9]);
-    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, t), 63));
-    o = lane == i ? s : o;
-  }
-  return o;
-}
-
-// The same 12 sums by a reduce-scatter (gfx950 lane swaps): v_permlane32_swap pairs value 2i's upper
+// The slot's 12 R/T partial sums (gR[0..8], gT[0..2] summed over the wave) by a reduce-scatter (gfx950 lane
+// swaps): v_permlane32_swap pairs value 2i's upper
 // half-wave with value 2i+1's lower half, so one add leaves value 2i's 32 partial sums in lanes 0-31 and
 // 2i+1's in lanes 32-63 (6 swaps + 6 adds for 12 values); v_permlane16_swap does the same inside each
 // half for pairs of those vectors (3 + 3), leaving 4 values per vector, one per 16-lane row; four DPP
 // butterfly steps per vector (quad xor 1, xor 2, half-row mirror, row mirror) finish every row's sum in
 // all its lanes. 30 VALU instead of rt_partial's ~100 (12 six-step scans + readlanes + selects). Fixed
-// order: deterministic. o[j] row r holds value RT_VALUE(j, r).
+// order: deterministic (a view's R/T gradient sums these rows in slot order, k_rt_vgrad_a). o[j] row r holds
+// value RT_VALUE(j, r). Uniform call (full EXEC). Round 5's twelve scans: 61.3 -> 58.3 us per launch
+// (profiles/r6d_ab.txt).
 // gfx950 v_permlane32_swap / v_permlane16_swap as inline asm: lanes 32-63 of x trade with lanes 0-31 of y
 // (x = {x.lo, y.lo}, y = {x.hi, y.hi}); the 16-lane form trades x's odd rows with y's even rows. (The
 // compiler's builtins returned a pair whose two halves it treated as one register when both feed one add:
@@ -417,34 +407,10 @@ struct RenderBwdParams {
   float* gface;
   int* fflag;      // ctr + CTR_FLT: set when a float remainder is written
   float* rt_part;  // (slots, 12) per-slot R/T partial sums
-  const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist
+  const float4* frec;  // (slots, 64) the forward's fragments (k_shade<1>): b0, b1, b2, signed dist (pixel order)
+  const int* sgrp;     // (slots, 64) the slot's winners grouped by record (k_shade<1>)
+  const uint8_t* sgpix; // (slots, 64) the tile pixel of each grouped position
 };
-
-// Order the 64 pixels of a slot by winning record (groups in order of first appearance, pixels of a
-// group in tile order): each (tile, record) then forms ONE run of consecutive lanes, so the per-face
-// rows of a tile come out of one segmented scan, one row per (tile, record) — 13.5 instead of 28.7
-// runs per tile on the bench workload — and can be written with plain stores. The loop runs once
-// per distinct record of the tile (uniform, scalar bookkeeping). Returns the tile pixel this lane
-// takes; f becomes that pixel's record.
-MR_DEV int sort_slot_pixels(int& f, int lane, int* lperm) {
-  unsigned long long rem = ~0ull;
-  int pos = 0, base = 0;
-  while (rem) {
-    const int l = (int)__builtin_ctzll(rem);
-    const int key = __builtin_amdgcn_readlane(f, l);
-    const unsigned long long m = __ballot(f == key);
-    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-    pos = f == key ? base + below : pos;
-    base += __popcll(m);
-    rem &= ~m;
-  }
-  lperm[pos] = lane;
-  wave_lds_sync();
-  const int src = lperm[lane];
-  f = __builtin_amdgcn_ds_bpermute(src << 2, f);
-  wave_lds_sync();  // lperm is rewritten for the next slot
-  return src;
-}
 
 // seg_stage for the fused backward: key = record id (runs are whole (tile, record) groups after
 // sort_slot_pixels), face = the record's face (the accumulator row every view's records add into).
@@ -645,11 +611,6 @@ __device__ unsigned long long g_bwd_stamp[MR_XP_WAVES * 8];
 #define XP_STORE() do { } while (0)
 #endif
 
-#ifdef MR_XP_SRPF
-#define MR_SRPF_ON 1
-#else
-#define MR_SRPF_ON 0
-#endif
 // The face of slot pixel record f (-1: face 0, an unconditional load's address) in view n.
 MR_DEV uint32_t bwd_face(const RenderBwdParams& P, int f, int n) {
   return f >= 0 ? (uint32_t)(rec_orig(f, P.NF) - n * P.F) : 0u;
@@ -658,13 +619,9 @@ MR_DEV uint32_t bwd_face(const RenderBwdParams& P, int f, int n) {
 template <int ACC, bool CLIP, bool GEO = false>
 __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
   constexpr int NV = GEO ? 9 : ACC;  // values per face row this kernel adds
-  // SRPF: the next slot's ShadeRecs are loaded during this slot's half 2 (their latency hidden behind the
-  // raster backward) instead of at the start of its half 1
-  constexpr bool SRPF = !GEO && MR_SRPF_ON;
   const RenderBwdParams& P = P0;
   __shared__ float lrow[4][64 * NV];
   __shared__ int lkey[4][64];
-  __shared__ int lperm[4][64];
   constexpr int NREC = GEO ? 1 : MR_BWD_REC(ACC);
   __shared__ float4 lrec[4][NREC][64];
   const bool lut = GEO ? false : stage_tex_lut(P.S);  // the u8 texture table in LDS
@@ -683,26 +640,18 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   const int slast = max(nslots - 1, 0);
   int sc = min(s, slast);
   int sl_c = sc;  // slot of gt_c / f_c (clamped)
-  int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
+  // lane -> (record f, tile pixel p) of the slot, grouped by record by the forward (k_shade<1>: sgrp, sgpix)
+  int gt_c = P.stile[sc + lz], f_c = P.sgrp[(int64_t)sc * 64 + lane], p_c = P.sgpix[(int64_t)sc * 64 + lane];
   sc = min(s + G, slast);
   int sl_n = sc;
-  int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
+  int gt_n = P.stile[sc + lz], f_n = P.sgrp[(int64_t)sc * 64 + lane], p_n = P.sgpix[(int64_t)sc * 64 + lane];
   FaceRec r_c;
   float g_c[5];
   float4 fr_c;
-  // lane -> tile pixel p_c of the slot in flight (pixels grouped by record, sort_slot_pixels)
-  int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
   bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
-  SRRaw sr_c;
-  if (SRPF) load_sr_raw(P.srec, bwd_face(P, f_c, __builtin_amdgcn_readfirstlane(gt_c) / P.T), sr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
-#ifdef MR_XP_RT_SWAP
-  float rt_prev[3] = {0.0f, 0.0f, 0.0f};
+  float rt_prev[3] = {0.0f, 0.0f, 0.0f};  // the previous slot's R/T sums (rt_partial_swap)
 #define RT_STORE(slot) rt_store_swap(P.rt_part + (int64_t)(slot) * 12, rt_prev, lane)
-#else
-  float rt_prev = 0.0f;
-#define RT_STORE(slot) do { if (lane < 12) P.rt_part[(int64_t)(slot) * 12 + lane] = rt_prev; } while (0)
-#endif
   XP_DECL
   XP_MARK(-1);
   for (; s < send; s += G) {
@@ -711,28 +660,26 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     const int gt = __builtin_amdgcn_readfirstlane(gt_c), f = f_c, p = p_c;
     const FaceRec r = r_c;
     const float4 frag = fr_c;
-    SRRaw sr;
-    if (SRPF) sr = sr_c;
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
     gt_c = gt_n;
     f_c = f_n;
+    p_c = p_n;
     sl_c = sl_n;
-    p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
     bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
     sc = min(s + 2 * G, slast);
     sl_n = sc;
     gt_n = P.stile[sc + lz];
-    f_n = P.sface[(int64_t)sc * 64 + lane];
+    f_n = P.sgrp[(int64_t)sc * 64 + lane];
+    p_n = P.sgpix[(int64_t)sc * 64 + lane];
     int n, px, py;
     slot_pixel(P, gt, p, n, px, py);
     XP_MARK(0);  // loop top: prefetch issue + the next slot's pixel sort
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (!GEO && f >= 0) {
       PixGeom Gm;
-      if (SRPF) geom_from_raw(sr, Gm);
-      else load_geom(P.srec, (uint32_t)(rec_orig(f, P.NF) - n * P.F), Gm);
+      load_geom(P.srec, bwd_face(P, f, n), Gm);
       const float gD = gin[0], gS = gin[1];
       float gC[3] = {gin[2], gin[3], gin[4]};
       const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, p) : 0.0f;
@@ -849,15 +796,8 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
       }
     }
     XP_MARK(3);  // raster + projection backward
-    // the next slot's ShadeRecs (issued after the flush's atomics: waited on only in the next slot's half 1,
-    // by when those have retired), in flight through the segmented scan and the next slot's loop top
-    if (SRPF) load_sr_raw(P.srec, bwd_face(P, f_c, __builtin_amdgcn_readfirstlane(gt_c) / P.T), sr_c);
     nt_prev = seg_stage_face<NV>(f >= 0 ? f : -1, key, row, lrow[wave], lkey[wave]);
-#ifdef MR_XP_RT_SWAP
     rt_partial_swap(gR, gT, rt_prev);
-#else
-    rt_prev = rt_partial(gR, gT, lane);
-#endif
     s_prev = s;
     XP_MARK(4);  // segmented scan + R/T wave sums
   }

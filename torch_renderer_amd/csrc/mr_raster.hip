@@ -1012,6 +1012,8 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.fflag = w.ctr + CTR_FLT;
   P.rt_part = rt_part;
   P.frec = w.frec;
+  P.sgrp = w.sgrp;
+  P.sgpix = w.sgpix;
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;

@@ -167,6 +167,8 @@ struct RasterWS {
   unsigned long long* gfix;
   float* gflt;
   float4* frec;    // (N*T*64) fused path: per slot pixel the winner's fragment (b0, b1, b2, signed dist)
+  int* sgrp;       // (N*T*64) fused path: each slot's winners grouped by record (k_shade<1>, for the backward)
+  uint8_t* sgpix;  // (N*T*64) fused path: the tile pixel of each grouped position
   ClipRec* crec;   // (2 * Ftot) barycentric conversion of near-plane sub-triangles (by record id)
   // banded per-view binning of one shared mesh (bands > 1): each (view, band)'s records, listed by
   // k_band_bucket (bcap = 2 Ftot / N: both triangles of every face of the view), and their counts
@@ -226,6 +228,10 @@ static RasterWS carve_raster_ws(void* base, int64_t N, int64_t Ftot, int H, int 
   off = align_up(off + sizeof(float) * 27 * (size_t)Fshade, 256);
   w.frec = (float4*)(b + off);
   off = align_up(off + sizeof(float4) * (Fshade > 0 ? 64 * NT : 0), 256);
+  w.sgrp = (int*)(b + off);
+  off = align_up(off + sizeof(int) * (Fshade > 0 ? 64 * NT : 0), 256);
+  w.sgpix = (uint8_t*)(b + off);
+  off = align_up(off + (Fshade > 0 ? 64 * NT : 0), 256);
   w.crec = (ClipRec*)(b + off);
   off = align_up(off + sizeof(ClipRec) * 2 * (size_t)(Ftot > 0 ? Ftot : 1), 256);
   const int B = bin_bands(N, g);

@@ -95,6 +95,10 @@ struct TexTap {
   float ix, iy;     // clipped pixel coords in the flipped map
   bool gx_ok, gy_ok;  // border-clip gradient pass-through
   int x0, y0;
+  // 8-bit maps: the four texels as loaded (pre: valid), so that the backward's second look-up
+  // (tex_sample_bwd) reads no memory
+  bool pre;
+  uint32_t raw[4];
 };
 // The four bilinear taps (x0|x0+1, y0|y0+1); out-of-range taps read as zero. The addresses are
 // clamped and all four loads issued unconditionally, then the values selected: written as
@@ -106,6 +110,39 @@ __shared__ float g_tex_lut[256];
 
 // lds_lut: read the table from g_tex_lut (the kernel staged it) instead of S.tex_lut. Texel indices
 // are 32-bit (maps < 2^32 texels): one 64-bit address add per tap instead of 64-bit index math.
+// The four 8-bit texels of cell (x0, y0) as raw words (unconditional loads of clamped indices).
+MR_DEV void tex_taps_raw(const ShadeParams& S, int x0, int y0, uint32_t (&raw)[4]) {
+  const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int xc = xs[i & 1], yc = ys[i >> 1];
+    const bool ok = (unsigned)xc < (unsigned)S.tex_w && (unsigned)yc < (unsigned)S.tex_h;
+    const int x = ok ? xc : 0, y = ok ? yc : S.tex_h - 1;
+    raw[i] = ((const uint32_t*)S.tex8)[(uint32_t)(S.tex_h - 1 - y) * (uint32_t)S.tex_w + (uint32_t)x];
+  }
+}
+// tex_taps' values from raw texels (tex_taps_raw): the table look-ups and the out-of-range zeros.
+MR_DEV void taps_from_raw(const ShadeParams& S, int x0, int y0, const uint32_t (&raw)[4], float4& a, float4& b,
+                          float4& c, float4& d, bool lds_lut) {
+  const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
+  float4 v[4];
+  bool ok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int xc = xs[i & 1], yc = ys[i >> 1];
+    ok[i] = (unsigned)xc < (unsigned)S.tex_w && (unsigned)yc < (unsigned)S.tex_h;
+    const uint32_t w = raw[i];
+    const uint32_t r = w & 255u, g = (w >> 8) & 255u, bl = (w >> 16) & 255u;
+    if (lds_lut) v[i] = make_float4(g_tex_lut[r], g_tex_lut[g], g_tex_lut[bl], 0.0f);  // (separate branches:
+    else v[i] = make_float4(S.tex_lut[r], S.tex_lut[g], S.tex_lut[bl], 0.0f);          // no flat load via a phi)
+  }
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  a = ok[0] ? v[0] : z;
+  b = ok[1] ? v[1] : z;
+  c = ok[2] ? v[2] : z;
+  d = ok[3] ? v[3] : z;
+}
+
 MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b, float4& c, float4& d,
                      bool lds_lut = false) {
   const int xs[2] = {x0, x0 + 1}, ys[2] = {y0, y0 + 1};
@@ -155,7 +192,8 @@ MR_DEV void tex_taps(const ShadeParams& S, int x0, int y0, float4& a, float4& b,
 // one ulp off a texel boundary picks the neighbouring cell and a different gradient. The weights and
 // the blend after it are continuous in the position and keep fast arithmetic.
 MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3], bool lut);
-MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t, bool lut = false) {
+// The sample position of (u, v) (tex_sample's first half): the cell, its weights' inputs and the border flags.
+MR_DEV void tex_locate(const ShadeParams& S, float u, float v, TexTap& t) {
   const float gx = u * 2.0f - 1.0f, gy = v * 2.0f - 1.0f;
   float ix = ((gx + 1.0f) / 2.0f) * (float)(S.tex_w - 1);
   float iy = ((gy + 1.0f) / 2.0f) * (float)(S.tex_h - 1);
@@ -167,6 +205,14 @@ MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], Tex
   t.iy = iy;
   t.x0 = (int)floorf(ix);
   t.y0 = (int)floorf(iy);
+  t.pre = false;
+}
+MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t, bool lut = false) {
+  tex_locate(S, u, v, t);
+  if (S.tex8) {  // the raw texels stay in the tap: a backward's second look-up (tex_sample_bwd) reloads nothing
+    tex_taps_raw(S, t.x0, t.y0, t.raw);
+    t.pre = true;
+  }
   tex_blend(S, t, out, lut);
 }
 MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3], bool lut) {
@@ -176,7 +222,8 @@ MR_DEV void tex_blend(const ShadeParams& S, const TexTap& t, float out[3], bool 
   const float nw = (x1 - ix) * (y1 - iy), ne = (ix - x0) * (y1 - iy);
   const float sw = (x1 - ix) * (iy - y0), se = (ix - x0) * (iy - y0);
   float4 a, b, c, d;
-  tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
+  if (t.pre) taps_from_raw(S, t.x0, t.y0, t.raw, a, b, c, d, lut);
+  else tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
   out[0] = ((a.x * nw + b.x * ne) + c.x * sw) + d.x * se;
   out[1] = ((a.y * nw + b.y * ne) + c.y * sw) + d.y * se;
   out[2] = ((a.z * nw + b.z * ne) + c.z * sw) + d.z * se;
@@ -187,7 +234,8 @@ MR_DEV void tex_sample_bwd(const ShadeParams& S, const TexTap& t, const float g[
   MR_FP_FAST
   const float x1 = (float)(t.x0 + 1), y1 = (float)(t.y0 + 1), x0 = (float)t.x0, y0 = (float)t.y0;
   float4 a, b, c, d;
-  tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
+  if (t.pre) taps_from_raw(S, t.x0, t.y0, t.raw, a, b, c, d, lut);
+  else tex_taps(S, t.x0, t.y0, a, b, c, d, lut);
   const float ga = (g[0] * a.x + g[1] * a.y) + g[2] * a.z;
   const float gb = (g[0] * b.x + g[1] * b.y) + g[2] * b.z;
   const float gc = (g[0] * c.x + g[1] * c.y) + g[2] * c.z;
@@ -269,37 +317,6 @@ MR_DEV void load_geom(const ShadeRec* __restrict__ recs, uint32_t face, PixGeom&
   for (int i = 0; i < 9; ++i) {
     const float4 x = q[i];
     v[4 * i] = x.x; v[4 * i + 1] = x.y; v[4 * i + 2] = x.z; v[4 * i + 3] = x.w;
-  }
-#pragma unroll
-  for (int c = 0; c < 3; ++c)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      G.X[c][k] = v[3 * c + k];
-      G.Nv[c][k] = v[9 + 3 * c + k];
-      G.col[c][k] = v[18 + 3 * c + k];
-    }
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    G.uv[c][0] = v[18 + 3 * c];
-    G.uv[c][1] = v[18 + 3 * c + 1];
-  }
-}
-
-// The ShadeRec's first 28 floats (world corners, vertex normals, uv / colours) as seven 16-B loads held
-// in registers (a prefetch one slot ahead: k_bwd_fused), and their PixGeom view.
-struct SRRaw {
-  float4 q[7];
-};
-MR_DEV void load_sr_raw(const ShadeRec* __restrict__ recs, uint32_t face, SRRaw& R) {
-  const float4* q = (const float4*)(recs + face);
-#pragma unroll
-  for (int i = 0; i < 7; ++i) R.q[i] = q[i];
-}
-MR_DEV void geom_from_raw(const SRRaw& R, PixGeom& G) {
-  float v[28];
-#pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    v[4 * i] = R.q[i].x; v[4 * i + 1] = R.q[i].y; v[4 * i + 2] = R.q[i].z; v[4 * i + 3] = R.q[i].w;
   }
 #pragma unroll
   for (int c = 0; c < 3; ++c)

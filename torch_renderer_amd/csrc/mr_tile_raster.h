@@ -267,7 +267,9 @@ struct FwdParams {
   float* sil;
   float* rgb;
   int32_t* p2f32;  // optional
-  float4* frec;    // MODE 1: the winners' fragments for the backward (slot-major, 64 per slot)
+  float4* frec;    // MODE 1: the winners' fragments for the backward (slot-major, 64 per slot, tile-pixel order)
+  int* sgrp;       // MODE 1: (slots, 64) the winners grouped by record (sort_slot_pixels), for the backward
+  uint8_t* sgpix;  // MODE 1: (slots, 64) the tile pixel of each grouped position
   // fused soft silhouette (k_raster_kp<KP, true>): sil = rgba (N,H,W,4); the compact fragments per slot
   float isig;
   int4* sent;
@@ -849,11 +851,41 @@ MR_DEV void xcd_slot_range(int nslots, int wave, int& s0, int& step, int& end) {
   step = (int)(gridDim.x / parts) * 4;
 }
 
+// Order the 64 pixels of a slot by winning record (groups in order of first appearance, pixels of a
+// group in tile order): each (tile, record) then forms ONE run of consecutive lanes of the backward, so the per-face
+// rows of a tile come out of one segmented scan, one row per (tile, record) — 13.5 instead of 28.7
+// runs per tile on the bench workload — and can be written with plain stores. The loop runs once
+// per distinct record of the tile (uniform, scalar bookkeeping). Returns the tile pixel this lane
+// takes; f becomes that pixel's record.
+MR_DEV int sort_slot_pixels(int& f, int lane, int* lperm) {
+  unsigned long long rem = ~0ull;
+  int pos = 0, base = 0;
+  while (rem) {
+    const int l = (int)__builtin_ctzll(rem);
+    const int key = __builtin_amdgcn_readlane(f, l);
+    const unsigned long long m = __ballot(f == key);
+    const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    pos = f == key ? base + below : pos;
+    base += __popcll(m);
+    rem &= ~m;
+  }
+  lperm[pos] = lane;
+  wave_lds_sync();
+  const int src = lperm[lane];
+  f = __builtin_amdgcn_ds_bpermute(src << 2, f);
+  wave_lds_sync();  // lperm is rewritten for the next slot
+  return src;
+}
+
 // Covered pixels: waves stride over the non-empty tiles' slots, one tile pixel per lane:
 // recompute the winning fragment exactly, then write PyTorch3D fragments (M = 0) or shade
 // (M = 1) over the background k_tile_raster wrote.
+// MODE 1 (the fused render) also groups each slot's pixels by winning record (sort_slot_pixels) and
+// writes the grouping (sgrp, sgpix) beside the fragments (frec, tile-pixel order): the backward then reads
+// its lanes' pixels pre-grouped instead of sorting every slot again (round 5 sorted in k_bwd_fused).
 template <int MODE, int CH>
 __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
+  __shared__ int lperm[MODE == 1 ? 4 : 1][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int nslots = P.ctr[CTR_SLOTS];
@@ -870,21 +902,28 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
   sc = min(s0 + G, slast);
   int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
+  // lane -> tile pixel p_c (MODE 1: grouped by record; the record prefetch follows the grouped order)
+  int p_c = MODE == 1 ? sort_slot_pixels(f_c, lane, lperm[wave]) : lane;
   FaceRec r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
   for (int s = s0; s < send; s += G) {
     const int gt = __builtin_amdgcn_readfirstlane(gt_c);
-    const int f = f_c;
+    const int f = f_c, p = p_c;
     const FaceRec r = r_c;
     gt_c = gt_n;
     f_c = f_n;
+    if (MODE == 1) p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
     r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
     sc = min(s + 2 * G, slast);
     gt_n = P.stile[sc + lz];
     f_n = P.sface[(int64_t)sc * 64 + lane];
+    if (MODE == 1) {
+      P.sgrp[(int64_t)s * 64 + lane] = f;
+      P.sgpix[(int64_t)s * 64 + lane] = (uint8_t)p;
+    }
     if (f < 0) continue;
     const int n = gt / P.T, t = gt - n * P.T;
     const int ty = t / P.TX, tx = t - ty * P.TX;
-    const int px = tx * MR_TS + (lane & 7), py = ty * MR_TS + (lane >> 3);
+    const int px = tx * MR_TS + (p & 7), py = ty * MR_TS + (p >> 3);
     const int64_t q = n * HW + (int64_t)py * P.W + px;
     const int fo = rec_orig(f, P.NF);  // the original face instance
     PixGeom G;
@@ -907,7 +946,7 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
     } else {
       // the fragment the backward shades again (its barycentrics must be these bits: they pick the
       // texel cell), so k_bwd_fused does not re-run eval_face's IEEE divisions
-      P.frec[(int64_t)s * 64 + lane] = make_float4(ev.b0, ev.b1, ev.b2, ev.sdist);
+      P.frec[(int64_t)s * 64 + p] = make_float4(ev.b0, ev.b1, ev.b2, ev.sdist);  // (tile-pixel order)
       ShadeOut o;
       ShadeCache C;
       shade_fwd(P.S, n, true, G, ev.b0, ev.b1, ev.b2, ev.pz, ev.sdist, o, C);
@@ -953,6 +992,8 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
   P.cnt = w.cnt; P.start = w.start; P.vbase = w.vbase; P.list_cap = g.list_cap; P.mfpb = g.mfpb;
   P.tdone = w.tdone; P.sface = w.sface; P.stile = w.stile;
   P.frec = w.frec;
+  P.sgrp = w.sgrp;
+  P.sgpix = w.sgpix;
   P.sorder_ws = w.sorder;
   P.units_ws2 = w.units2;
   return P;

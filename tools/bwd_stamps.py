@@ -2,8 +2,8 @@
 per-wave stamps: python tools/build_variant.py stamp -DMR_XP_BWD_STAMP, then (GPU)
 MI355R_LIB=exp/stamp.so python tools/bwd_stamps.py
 Per wave: global-clock start / end (100 MHz), slots, shader cycles per phase of the slot loop
-(0 loop top: prefetch + next slot's pixel sort; 1 half 1: shade fwd+bwd; 2 world corners + previous
-slot's flush; 3 raster + projection backward; 4 segmented scan + R/T sums). The stamps cost cycles
+(0 loop top; 1 half 1: shade fwd+bwd; 2 world corners + the next slots' prefetches + the previous slot's
+flush; 3 raster + projection backward; 4 segmented scan + R/T sums). The stamps cost cycles
 themselves (s_memtime waits); read the shares, not the absolute time."""
 import ctypes
 import os
@@ -57,7 +57,7 @@ def main():
     life = en - st
     print(f"wave start: max {st.max() / 1e3:.1f} us; end: min {en.min() / 1e3:.1f}, median {np.median(en) / 1e3:.1f}, "
           f"max {span / 1e3:.1f} us; mean lifetime / span {life.mean() / span:.3f}")
-    names = ("top: prefetch + sort", "half 1: shade fwd+bwd", "corners + prev flush", "raster + proj bwd",
+    names = ("loop top", "half 1: shade fwd+bwd", "corners + prefetch + flush", "raster + proj bwd",
              "seg scan + R/T sums")
     tot = ph.sum()
     per_slot = ph.sum(0) / n.sum()

@@ -512,6 +512,7 @@ MR_DEV void slot_pixel(const RenderBwdParams& P, int gt, int lane, int& n, int& 
 // gradient; such values are never used): written as guarded loads they become branches whose
 // phi copies wait on the load right away, which defeats the prefetch.
 __device__ float g_zero4[4];
+template <int SPEC = 0>
 MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, int lane, FaceRec& r, float g[5],
                              float4& fr) {
   int n, px, py;
@@ -520,8 +521,8 @@ MR_DEV void bwd_slot_inputs(const RenderBwdParams& P, int slot, int gt, int f, i
   r = load_rec(P.recs, f < 0 ? 0 : f);
   fr = P.frec[(int64_t)slot * 64 + lane];
   const float* pD = P.gD ? P.gD + pix : g_zero4;
-  const float* pS = P.gS ? P.gS + (P.sil_rgba ? 4 * pix + 3 : pix) : g_zero4;
-  const float* pC = P.gRGB ? P.gRGB + pix * P.rgb_ch : g_zero4;
+  const float* pS = P.gS ? P.gS + ((!SPEC && P.sil_rgba) ? 4 * pix + 3 : pix) : g_zero4;
+  const float* pC = P.gRGB ? P.gRGB + pix * (SPEC ? 3 : P.rgb_ch) : g_zero4;
   g[0] = *pD;
   g[1] = *pS;
   g[2] = pC[0];
@@ -616,7 +617,9 @@ MR_DEV uint32_t bwd_face(const RenderBwdParams& P, int f, int n) {
   return f >= 0 ? (uint32_t)(rec_orig(f, P.NF) - n * P.F) : 0u;
 }
 
-template <int ACC, bool CLIP, bool GEO = false>
+// SPEC 1 (the drop-in Phong render's case, chosen on the host): UV map with an 8-bit copy, point light, 3-channel
+// RGB, relu depth, plain silhouette: the shading's runtime switches become compile-time constants.
+template <int ACC, bool CLIP, bool GEO = false, int SPEC = 0>
 __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P0) {
   constexpr int NV = GEO ? 9 : ACC;  // values per face row this kernel adds
   const RenderBwdParams& P = P0;
@@ -648,7 +651,7 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
   FaceRec r_c;
   float g_c[5];
   float4 fr_c;
-  bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
+  bwd_slot_inputs<SPEC>(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
   int nt_prev = -1, s_prev = 0;  // the previous slot's staged runs (-1: none yet)
   float rt_prev[3] = {0.0f, 0.0f, 0.0f};  // the previous slot's R/T sums (rt_partial_swap)
 #define RT_STORE(slot) rt_store_swap(P.rt_part + (int64_t)(slot) * 12, rt_prev, lane)
@@ -663,26 +666,16 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     float gin[5];
 #pragma unroll
     for (int i = 0; i < 5; ++i) gin[i] = g_c[i];
-    gt_c = gt_n;
-    f_c = f_n;
-    p_c = p_n;
-    sl_c = sl_n;
-    bwd_slot_inputs(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
-    sc = min(s + 2 * G, slast);
-    sl_n = sc;
-    gt_n = P.stile[sc + lz];
-    f_n = P.sgrp[(int64_t)sc * 64 + lane];
-    p_n = P.sgpix[(int64_t)sc * 64 + lane];
     int n, px, py;
     slot_pixel(P, gt, p, n, px, py);
-    XP_MARK(0);  // loop top: prefetch issue + the next slot's pixel sort
+    XP_MARK(0);  // loop top
     // ---- half 1: blends / Phong / texture backward -> lrec
     if (!GEO && f >= 0) {
       PixGeom Gm;
       load_geom(P.srec, bwd_face(P, f, n), Gm);
       const float gD = gin[0], gS = gin[1];
       float gC[3] = {gin[2], gin[3], gin[4]};
-      const float gA = (P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, p) : 0.0f;
+      const float gA = (!SPEC && P.gRGB && P.rgb_ch == 4) ? g_alpha(P, gt, p) : 0.0f;
       FragEval e;
       float4 o[NREC];
       // the forward's fragment (k_shade<1> wrote the winner's barycentrics, original-face ones for a
@@ -702,9 +695,9 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
       {
         ShadeOut so;
         ShadeCache C;
-        shade_fwd(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C, lut);
+        shade_fwd<SPEC>(P.S, n, true, Gm, e.b0, e.b1, e.b2, e.pz, e.sdist, so, C, lut);
         ShadeGrad SG;
-        shade_bwd(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
+        shade_bwd<SPEC>(P.S, Gm, e.b0, e.b1, e.b2, e.pz, C, gD, gS, gC, gA, SG, lut);
         o[0] = make_float4(SG.gz, SG.gsd, SG.gb[0], SG.gb[1]);
         o[1] = make_float4(SG.gb[2], SG.gP[0], SG.gP[1], SG.gP[2]);
         o[2] = make_float4(SG.gNn[0], SG.gNn[1], SG.gNn[2], SG.gtex[0]);
@@ -726,13 +719,29 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
     const float4* x4 = (const float4*)(P.srec + face);
     const float4 w0 = x4[0], w1 = x4[1], w2 = x4[2];
     __builtin_amdgcn_sched_barrier(0);
+    // The next slots' inputs (slot s + G's records, fragments and upstream gradients; slot s + 2G's tile and
+    // grouped winners), issued only now, after this slot's ShadeRec / texel loads and world corners: a
+    // load's wait (vmcnt, in-order retirement) also waits for every vector-memory op issued before it, so
+    // issued at the loop top (round 5) they put the next slots' HBM gradient reads in front of this slot's
+    // ShadeRec wait (54.8 -> 52.6-53.4 us, profiles/r6i_latepf_ab.txt).
+    gt_c = gt_n;
+    f_c = f_n;
+    p_c = p_n;
+    sl_c = sl_n;
+    bwd_slot_inputs<SPEC>(P, sl_c, __builtin_amdgcn_readfirstlane(gt_c), f_c, p_c, r_c, g_c, fr_c);
+    sc = min(s + 2 * G, slast);
+    sl_n = sc;
+    gt_n = P.stile[sc + lz];
+    f_n = P.sgrp[(int64_t)sc * 64 + lane];
+    p_n = P.sgpix[(int64_t)sc * 64 + lane];
+    __builtin_amdgcn_sched_barrier(0);
     // previous slot's face rows and R/T partials, deferred to here (see above): the loads of
     // half 1 and the corners above are already in flight or consumed
     if (nt_prev >= 0) {
       seg_flush_fix<NV, ACC>(nt_prev, P.gfix, P.gface, lrow[wave], lkey[wave], P.fflag);
       RT_STORE(s_prev);
     }
-    XP_MARK(2);  // corners + the previous slot's flush
+    XP_MARK(2);  // corners + the next slots' prefetches + the previous slot's flush
     __builtin_amdgcn_sched_barrier(0);
     float gR[9], gT[3];
 #pragma unroll

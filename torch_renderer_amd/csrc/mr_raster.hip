@@ -1014,7 +1014,11 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   P.frec = w.frec;
   P.sgrp = w.sgrp;
   P.sgpix = w.sgpix;
+#ifndef MR_BWD_GRID_MUL
+#define MR_BWD_GRID_MUL 1
+#endif
   auto cap = [&](int gr) {  // enough waves for every tile, a multiple of 8 (XCD-partitioned slot ranges)
+    gr *= MR_BWD_GRID_MUL;
     const int c = (int)(NT / 4 + 1 < gr ? NT / 4 + 1 : gr);
     return (c + 7) / 8 * 8;
   };
@@ -1029,6 +1033,14 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   if (!g27c) g27c = resident_grid(k_bwd_fused<27, true, true>, 256, 4);
   // no RGB gradient (a depth / silhouette render's backward): the geometry-only instantiation
   const bool geo = P.gRGB == nullptr;
+  // the drop-in Phong render (UV map with an 8-bit copy, point light, RGB, relu depth): the specialised one
+#ifndef MR_BWD_SPEC
+#define MR_BWD_SPEC 1
+#endif
+  const bool spec = MR_BWD_SPEC && !geo && !vcol && !s->clip_z && m->tex_kind == 2 && m->tex_u8 && m->tex_lut &&
+                    sp->light_kind == 0 && sp->rgb_channels == 3 && !(sp->out_flags & (MR_OUT_ZBUF | MR_OUT_SIL_RGBA));
+  static int f18s = 0;
+  if (!f18s) f18s = resident_grid(k_bwd_fused<18, false, false, 1>, 256, 3);
   if (s->clip_z) {
     if (geo) {
       if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, true, true><<<cap(g27c), 256, 0, st>>>(P)));
@@ -1040,6 +1052,7 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
       if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false, true><<<cap(g27), 256, 0, st>>>(P)));
       else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false, true><<<cap(g18), 256, 0, st>>>(P)));
     } else if (vcol) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<27, false><<<cap(f27), 256, 0, st>>>(P)));
+    else if (spec) MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false, false, 1><<<cap(f18s), 256, 0, st>>>(P)));
     else MR_TIMED(KID_BWD_FUSED, st, (k_bwd_fused<18, false><<<cap(f18), 256, 0, st>>>(P)));
   }
   MR_CHECK_LAUNCH("k_bwd_fused");

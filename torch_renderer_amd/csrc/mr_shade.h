@@ -207,9 +207,11 @@ MR_DEV void tex_locate(const ShadeParams& S, float u, float v, TexTap& t) {
   t.y0 = (int)floorf(iy);
   t.pre = false;
 }
+// SPEC (specialised kernels): the map is known to have an 8-bit copy (S.tex8 non-null).
+template <int SPEC = 0>
 MR_DEV void tex_sample(const ShadeParams& S, float u, float v, float out[3], TexTap& t, bool lut = false) {
   tex_locate(S, u, v, t);
-  if (S.tex8) {  // the raw texels stay in the tap: a backward's second look-up (tex_sample_bwd) reloads nothing
+  if (SPEC || S.tex8) {  // the raw texels stay in the tap: a backward's second look-up (tex_sample_bwd) reloads nothing
     tex_taps_raw(S, t.x0, t.y0, t.raw);
     t.pre = true;
   }
@@ -354,14 +356,19 @@ struct ShadeCache {
 };
 
 // Forward shading of one pixel (hit = face found). b = bary (after clip), z, sd = signed dist.
+template <int SPEC = 0>
 MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, float b0, float b1, float b2,
                       float z, float sd, ShadeOut& o, ShadeCache& C, bool lut = false) {
   MR_FP_FAST
+  // SPEC 1: UV map with an 8-bit copy, point light, relu depth (the drop-in Phong render: compile-time
+  // constants instead of the runtime switches)
+  const int tex_kind = SPEC ? 2 : S.tex_kind, light_kind = SPEC ? 0 : S.light_kind;
+  const int zbuf_mode = SPEC ? 0 : S.zbuf_mode;
   const float m = hit ? 1.0f : 0.0f;
   const float zb = hit ? z : -1.0f;    // zbuf background = -1
   const float dd = hit ? sd : -1.0f;   // dists background = -1
   // DepthRender: relu(zbuf[..., 0]); MeshRasterizer's zbuf[..., 0] itself in zbuf mode
-  o.depth = (S.zbuf_mode || zb > 0.0f) ? zb : 0.0f;
+  o.depth = (zbuf_mode || zb > 0.0f) ? zb : 0.0f;
   // SoftSilhouetteShader / sigmoid_alpha_blend
   sigmoid2((-dd) * S.inv_sigma_sil, C.ps, C.qs);
   C.ps *= m;
@@ -373,16 +380,16 @@ MR_DEV void shade_fwd(const ShadeParams& S, int n, bool hit, const PixGeom& G, f
       C.P[k] = interp3(b0, b1, b2, G.X[0][k], G.X[1][k], G.X[2][k]);
       C.amb[k] = S.mat_amb[k] * S.light_amb[k];
     }
-    if (S.tex_kind == 2) {
+    if (tex_kind == 2) {
       const float u = interp3_ieee(b0, b1, b2, G.uv[0][0], G.uv[1][0], G.uv[2][0]);
       const float v = interp3_ieee(b0, b1, b2, G.uv[0][1], G.uv[1][1], G.uv[2][1]);
-      tex_sample(S, u, v, C.texel, C.tap, lut);
-    } else if (S.tex_kind == 1) {
+      tex_sample<SPEC>(S, u, v, C.texel, C.tap, lut);
+    } else if (tex_kind == 1) {
       for (int k = 0; k < 3; ++k) C.texel[k] = interp3(b0, b1, b2, G.col[0][k], G.col[1][k], G.col[2][k]);
     } else {
       C.texel[0] = C.texel[1] = C.texel[2] = 1.0f;
     }
-    if (S.light_kind == 0) {
+    if (light_kind == 0) {
       for (int k = 0; k < 3; ++k) C.Nn[k] = interp3(b0, b1, b2, G.Nv[0][k], G.Nv[1][k], G.Nv[2][k]);
       normalize3(C.Nn, C.nh, C.nlen, C.nden);
       for (int k = 0; k < 3; ++k) C.l[k] = S.light_loc[k] - C.P[k];
@@ -431,10 +438,13 @@ struct ShadeGrad {
   float gP[3], gNn[3], gtex[3];        // grads of the interpolated point, normal, texel
 };
 
+template <int SPEC = 0>
 MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1, float b2, float z,
                       const ShadeCache& C, float gD, float gS, const float gRGB[3], float gA, ShadeGrad& R,
                       bool lut = false) {
   MR_FP_FAST
+  const int tex_kind = SPEC ? 2 : S.tex_kind, light_kind = SPEC ? 0 : S.light_kind;  // (as shade_fwd)
+  const int zbuf_mode = SPEC ? 0 : S.zbuf_mode;
   const float b[3] = {b0, b1, b2};
   R.gz = 0.0f;
   R.gsd = 0.0f;
@@ -443,7 +453,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
     for (int k = 0; k < 3; ++k) R.gX[c][k] = R.gN[c][k] = R.gC[c][k] = 0.0f;
   }
   // depth = relu(z) (zbuf mode: z)
-  if (S.zbuf_mode || z > 0.0f) R.gz += gD;
+  if (zbuf_mode || z > 0.0f) R.gz += gD;
   // silhouette: sil = 1 - (1 - ps), ps = sigmoid(-sd / sigma_sil)
   {
     const float gx = gS * (C.ps * C.qs);
@@ -483,7 +493,7 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   // colours = (amb + diff) * texel + spec
   float gtex[3], gP[3] = {0.f, 0.f, 0.f}, gNn[3] = {0.f, 0.f, 0.f};
   for (int k = 0; k < 3; ++k) gtex[k] = gcol[k] * (C.amb[k] + C.diff[k]);
-  if (S.light_kind == 0) {
+  if (light_kind == 0) {
     float gangle = 0.0f, gspow = 0.0f;
     for (int k = 0; k < 3; ++k) {
       gangle += gcol[k] * C.texel[k] * S.mat_diff[k] * S.light_diff[k];
@@ -517,21 +527,21 @@ MR_DEV void shade_bwd(const ShadeParams& S, const PixGeom& G, float b0, float b1
   for (int k = 0; k < 3; ++k) {
     R.gP[k] = gP[k];
     R.gNn[k] = gNn[k];
-    R.gtex[k] = S.tex_kind == 1 ? gtex[k] : 0.0f;
+    R.gtex[k] = tex_kind == 1 ? gtex[k] : 0.0f;
   }
   for (int c = 0; c < 3; ++c) {
     R.gb[c] += dot3(G.X[c], gP);
-    if (S.light_kind == 0) R.gb[c] += dot3(G.Nv[c], gNn);
+    if (light_kind == 0) R.gb[c] += dot3(G.Nv[c], gNn);
     for (int k = 0; k < 3; ++k) {
       R.gX[c][k] = b[c] * gP[k];
       R.gN[c][k] = b[c] * gNn[k];
     }
   }
-  if (S.tex_kind == 2) {
+  if (tex_kind == 2) {
     float gu, gv;
     tex_sample_bwd(S, C.tap, gtex, gu, gv, lut);
     for (int c = 0; c < 3; ++c) R.gb[c] += G.uv[c][0] * gu + G.uv[c][1] * gv;
-  } else if (S.tex_kind == 1) {
+  } else if (tex_kind == 1) {
     for (int c = 0; c < 3; ++c) {
       R.gb[c] += dot3(G.col[c], gtex);
       for (int k = 0; k < 3; ++k) R.gC[c][k] = b[c] * gtex[k];

@@ -966,6 +966,104 @@ __global__ void __launch_bounds__(256) k_shade(FwdParams P) {
   }
 }
 
+// The fused render's covered pixels (k_shade<1>'s work, one kernel of its own): group each slot's pixels by
+// record (sgrp, sgpix for the backward), recompute the winner's fragment (frec), shade, write depth / silhouette /
+// RGB. Each slot's stores are deferred into the next slot's iteration, after that slot's ShadeRec loads: a
+// load's wait (vmcnt, in-order retirement) includes every store issued before it, so storing at the end of the
+// iteration put the previous slot's ~1 KB of writes in front of each ShadeRec wait. SPEC 1: the shading's runtime
+// switches as compile-time constants (UV map with an 8-bit copy, point light), outputs depth + silhouette + RGB.
+template <int CH, int SPEC>
+__global__ void __launch_bounds__(256) k_shade_render(FwdParams P) {
+  __shared__ int lperm[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int nslots = P.ctr[CTR_SLOTS];
+  if (nslots <= 0) return;
+  const int64_t HW = (int64_t)P.H * P.W;
+  int s0, G, send;
+  xcd_slot_range(nslots, wave, s0, G, send);
+  const int lz = lane_zero();
+  const int slast = max(nslots - 1, 0);
+  int sc = min(s0, slast);
+  int gt_c = P.stile[sc + lz], f_c = P.sface[(int64_t)sc * 64 + lane];
+  sc = min(s0 + G, slast);
+  int gt_n = P.stile[sc + lz], f_n = P.sface[(int64_t)sc * 64 + lane];
+  int p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
+  FaceRec r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
+  const int of = SPEC ? (MR_OUT_DEPTH | MR_OUT_SIL | MR_OUT_RGB) : P.out_flags;
+  // the previous slot's outputs, stored in this iteration
+  int s_prev = -1, f_prev = -1, p_prev = 0, fo_prev = 0;
+  bool w_prev = false;  // this lane covered a pixel of the previous slot
+  int64_t q_prev = 0;
+  float4 fr_prev = make_float4(0.f, 0.f, 0.f, 0.f);
+  ShadeOut o_prev;
+  o_prev.depth = o_prev.sil = o_prev.alpha = 0.f;
+  o_prev.rgb[0] = o_prev.rgb[1] = o_prev.rgb[2] = 0.f;
+  auto store_prev = [&]() {
+    if (s_prev < 0) return;
+    P.sgrp[(int64_t)s_prev * 64 + lane] = f_prev;
+    P.sgpix[(int64_t)s_prev * 64 + lane] = (uint8_t)p_prev;
+    if (w_prev) {
+      P.frec[(int64_t)s_prev * 64 + p_prev] = fr_prev;  // (tile-pixel order)
+      if (of & MR_OUT_DEPTH) P.depth[q_prev] = o_prev.depth;
+      if (of & MR_OUT_SIL) {
+        if (!SPEC && (of & MR_OUT_SIL_RGBA)) *(float4*)(P.sil + q_prev * 4) = make_float4(1.0f, 1.0f, 1.0f, o_prev.sil);
+        else P.sil[q_prev] = o_prev.sil;
+      }
+      if (of & MR_OUT_RGB) {
+        P.rgb[q_prev * CH + 0] = o_prev.rgb[0];
+        P.rgb[q_prev * CH + 1] = o_prev.rgb[1];
+        P.rgb[q_prev * CH + 2] = o_prev.rgb[2];
+        if (CH == 4) P.rgb[q_prev * CH + 3] = o_prev.alpha;
+      }
+      if (!SPEC && P.p2f32) P.p2f32[q_prev] = fo_prev;
+    }
+  };
+  for (int s = s0; s < send; s += G) {
+    const int gt = __builtin_amdgcn_readfirstlane(gt_c);
+    const int f = f_c, p = p_c;
+    const FaceRec r = r_c;
+    const int n = gt / P.T, t = gt - n * P.T;
+    const int ty = t / P.TX, tx = t - ty * P.TX;
+    const int px = tx * MR_TS + (p & 7), py = ty * MR_TS + (p >> 3);
+    const int64_t q = n * HW + (int64_t)py * P.W + px;
+    const int fo = f >= 0 ? (int)rec_orig(f, P.NF) : 0;  // the original face instance
+    PixGeom Gm;
+    load_geom(P.srec, f >= 0 ? (uint32_t)(fo - n * P.F) : 0u, Gm);  // first: its wait follows no store
+    gt_c = gt_n;
+    f_c = f_n;
+    p_c = sort_slot_pixels(f_c, lane, lperm[wave]);
+    r_c = load_rec(P.recs, f_c < 0 ? 0 : f_c);
+    sc = min(s + 2 * G, slast);
+    gt_n = P.stile[sc + lz];
+    f_n = P.sface[(int64_t)sc * 64 + lane];
+    store_prev();
+    FragEval ev;
+    const bool hit = f >= 0 && eval_face(r, col_ndc(px, P.H, P.W), row_ndc(py, P.H, P.W), P.bbox_pad, P.blur,
+                                         P.persp, P.clipb, ev);  // true by construction when f >= 0
+    ShadeOut o;
+    o.depth = o.sil = o.alpha = 0.f;
+    o.rgb[0] = o.rgb[1] = o.rgb[2] = 0.f;
+    if (hit) {
+      if (r.flags & FR_CLIP) {  // near-plane sub-triangle: barycentrics of the original face
+        const ClipRec cr = P.crec[f];
+        clip_unconvert(cr, ev.b0, ev.b1, ev.b2, ev.b0, ev.b1, ev.b2);
+      }
+      ShadeCache C;
+      shade_fwd<SPEC>(P.S, n, true, Gm, ev.b0, ev.b1, ev.b2, ev.pz, ev.sdist, o, C);
+    }
+    s_prev = s;
+    f_prev = f;
+    p_prev = p;
+    w_prev = hit;
+    q_prev = q;
+    fo_prev = fo;
+    fr_prev = make_float4(ev.b0, ev.b1, ev.b2, ev.sdist);
+    o_prev = o;
+  }
+  store_prev();
+}
+
 // Resident workgroups of a kernel on the current device (persistent grid size).
 template <typename K>
 static int resident_grid(K kernel, int threads, int fallback_per_cu) {
@@ -1031,6 +1129,27 @@ __global__ void __launch_bounds__(1024) k_unit_order(const int4* __restrict__ un
   }
 }
 
+#ifndef MR_SHADE_RENDER
+#define MR_SHADE_RENDER 1
+#endif
+// k_shade_render (the fused render's covered pixels), specialised when the shading and outputs are the drop-in
+// Phong render's: UV map with an 8-bit copy, point light, depth + silhouette + RGB, no pix_to_face.
+template <int CH>
+static int launch_shade_render(const FwdParams& P, int64_t slots_cap, hipStream_t st) {
+  static int g0 = 0, g1 = 0;
+  if (!g0) g0 = resident_grid(k_shade_render<CH, 0>, 256, 4);
+  if (!g1) g1 = resident_grid(k_shade_render<CH, 1>, 256, 4);
+  const bool spec = CH == 3 && P.S.tex_kind == 2 && P.S.tex8 && P.S.light_kind == 0 && !P.S.zbuf_mode &&
+                    !P.p2f32 && P.out_flags == (MR_OUT_DEPTH | MR_OUT_SIL | MR_OUT_RGB);
+  const int gr = spec ? g1 : g0;
+  int sg = (int)(slots_cap / 4 + 1 < gr ? slots_cap / 4 + 1 : gr);
+  sg = (sg + 7) / 8 * 8;  // XCD-partitioned slot ranges
+  if (spec) MR_TIMED(KID_SHADE_RENDER, st, (k_shade_render<CH, 1><<<sg, 256, 0, st>>>(P)));
+  else MR_TIMED(KID_SHADE_RENDER, st, (k_shade_render<CH, 0><<<sg, 256, 0, st>>>(P)));
+  MR_CHECK_LAUNCH("k_shade_render");
+  return MR_OK;
+}
+
 // Raster (+ background) then covered-pixel outputs; grids sized once per kernel instance.
 template <int MODE, int CH>
 static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hipStream_t st, bool clip) {
@@ -1051,6 +1170,7 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   MR_CHECK_LAUNCH("k_tile_raster");
   if (MODE == 0 && P.emit_frag) return MR_OK;  // the raster wrote the listed tiles' fragments
   const int64_t slots_cap = N * (int64_t)g.T;
+  if (MODE == 1 && MR_SHADE_RENDER) return launch_shade_render<CH>(P, slots_cap, st);
   int sg = (int)(slots_cap / 4 + 1 < sgrid ? slots_cap / 4 + 1 : sgrid);
   sg = (sg + 7) / 8 * 8;  // XCD-partitioned slot ranges
   MR_TIMED(MODE == 0 ? KID_SHADE_FRAG : KID_SHADE_RENDER, st, (k_shade<MODE, CH><<<sg, 256, 0, st>>>(P)));

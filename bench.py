@@ -143,7 +143,7 @@ def algorithmic_bytes(kernel, H, W, F, views, st, bgpix=0):
 # Forward fragment pass (everything from projected geometry to the three images): API-minimum
 # bytes per frame = 20 B/px of outputs + 36 B/face of geometry (without p2f).
 FORWARD_KERNELS = ("k_setup_zero", "k_vertex_normals", "k_shade_rec", "k_bin_count", "k_bin_scan", "k_bin_fill",
-                   "k_bin_rect", "k_bin_view",
+                   "k_bin_rect", "k_bin_view", "k_unit_order",
                    "k_tile_raster", "k_shade<1>")
 
 

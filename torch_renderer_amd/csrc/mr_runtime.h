@@ -31,7 +31,7 @@ enum KernelId { KID_BIN_COUNT, KID_BIN_SCAN, KID_BIN_FILL, KID_TILE_RASTER, KID_
                 KID_VGRAD_A, KID_VGRAD_B,
                 KID_VNORMALS, KID_PROJECT, KID_PROJECT_BWD, KID_SHADE_REC, KID_FILL_FRAG,
                 KID_RASTER_K, KID_BWD_FUSED, KID_RT_VGRAD_A, KID_FRAG_SHADE, KID_FRAG_SHADE_BWD, KID_SETUP, KID_BIN_RECT, KID_BIN_VIEW,
-                KID_FACE_REDUCE, KID_BAND_BUCKET, KID_POSE_LOSS, KID_POSE_LOSS_SCALE, KID_COUNT };
+                KID_FACE_REDUCE, KID_BAND_BUCKET, KID_POSE_LOSS, KID_POSE_LOSS_SCALE, KID_UNIT_ORDER, KID_COUNT };
 static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bin_fill", "k_tile_raster",
                                               "k_shade<0>", "k_shade<1>",
                                               "k_raster_bwd", "k_rt_vgrad_b", "k_bwd_geom(unused)", "k_rt_reduce",
@@ -40,7 +40,7 @@ static const char* kKernelNames[KID_COUNT] = {"k_bin_count", "k_bin_scan", "k_bi
                                               "k_shade_rec", "k_fill<0>", "k_raster_k", "k_bwd_fused",
                                               "k_rt_vgrad_a", "k_frag_shade_fwd", "k_frag_shade_bwd", "k_setup_zero",
                                               "k_bin_rect", "k_bin_view", "k_face_reduce(unused)", "k_band_bucket",
-                                              "k_pose_loss_fused", "k_pose_loss_scale"};
+                                              "k_pose_loss_fused", "k_pose_loss_scale", "k_unit_order"};
 #define MR_TPOOL 4096
 static struct {
   int enabled;

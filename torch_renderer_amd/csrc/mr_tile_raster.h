@@ -1161,7 +1161,7 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   // (the fused render only: in the fragment pass the raster's time is its background stores, and the order's
   // launch cost more than it saved — fragments 421k -> 405-416k, render 300k -> 301-302k, profiles/r5_unit_order_ab.txt)
   if (MR_UNIT_ORDER && MODE == 1 && P.units_ws2) {
-    k_unit_order<<<8, 1024, 0, st>>>(P.units, P.ctr, P.units_ws2);
+    MR_TIMED(KID_UNIT_ORDER, st, (k_unit_order<<<8, 1024, 0, st>>>(P.units, P.ctr, P.units_ws2)));
     MR_CHECK_LAUNCH("k_unit_order");
     P.units = P.units_ws2;
   }

@@ -85,10 +85,20 @@ def torch_ext_cmd(out: str):
                                                      f"-I{os.path.join(_HERE, '..', 'include')}"]
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     return [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-DTORCH_EXTENSION_NAME=_mr_torch",
+            f'-DMR_TORCH_VERSION="{torch.__version__}"',
             "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM",
             "-D__HIP_PLATFORM_AMD__=1", *incs, TORCH_EXT_SRC, "-o", out,
             f"-L{os.path.join(tdir, 'lib')}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python",
             f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+
+
+TORCH_EXT_STAMP = TORCH_EXT + ".stamp"  # the torch version and C++ ABI flag the extension was built against
+
+
+def torch_stamp() -> str:
+    import torch
+
+    return f"{torch.__version__} cxx11_abi={int(torch._C._GLIBCXX_USE_CXX11_ABI)}"
 
 
 def torch_ext_needs_build() -> bool:
@@ -96,7 +106,13 @@ def torch_ext_needs_build() -> bool:
         return True
     t = os.path.getmtime(TORCH_EXT)
     deps = [TORCH_EXT_SRC, os.path.join(_HERE, "..", "include", "mi355r.h"), os.path.abspath(__file__)]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    if any(os.path.getmtime(d) > t for d in deps if os.path.exists(d)):
+        return True
+    try:  # a torch upgrade (or another ABI) leaves the sources older than the .so: rebuild on the stamp
+        with open(TORCH_EXT_STAMP) as fh:
+            return fh.read().strip() != torch_stamp()
+    except OSError:
+        return True
 
 
 def build_torch_ext(force: bool = False, verbose: bool = True) -> str:
@@ -107,6 +123,8 @@ def build_torch_ext(force: bool = False, verbose: bool = True) -> str:
         print("[mi355r] " + " ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
     os.replace(TORCH_EXT + ".tmp", TORCH_EXT)
+    with open(TORCH_EXT_STAMP, "w") as fh:
+        fh.write(torch_stamp() + "\n")
     return TORCH_EXT
 
 

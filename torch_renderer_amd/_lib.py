@@ -207,6 +207,14 @@ def torch_ext():
     spec = importlib.util.spec_from_file_location("_mr_torch", path)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    import torch
+
+    built = getattr(mod, "built_with_torch", "unknown")
+    abi = getattr(mod, "built_with_cxx11_abi", None)
+    if built != torch.__version__ or (abi is not None and bool(abi) != bool(torch._C._GLIBCXX_USE_CXX11_ABI)):
+        raise RuntimeError(f"mi355r: {path} was built against torch {built} (cxx11 ABI {abi}), this process runs "
+                           f"torch {torch.__version__} (cxx11 ABI {torch._C._GLIBCXX_USE_CXX11_ABI}): rebuild it "
+                           "(python -m torch_renderer_amd._build)")
     lib = load()
     mod.init({name: ctypes.cast(getattr(lib, name), ctypes.c_void_p).value for name in _EXT_FNS})
     with _lock:

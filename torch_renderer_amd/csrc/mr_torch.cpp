@@ -458,8 +458,16 @@ void init(const std::unordered_map<std::string, int64_t>& fn) {
 
 }  // namespace
 
+#ifndef MR_TORCH_VERSION
+#define MR_TORCH_VERSION "unknown"
+#endif
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mi355r torch glue: the fused render's autograd node (kernels.render_views)";
+  // the torch this file was compiled against (_build.py passes torch.__version__): _lib.torch_ext() refuses a
+  // stale build instead of failing later on a missing symbol or a mismatched ABI
+  m.attr("built_with_torch") = MR_TORCH_VERSION;
+  m.attr("built_with_cxx11_abi") = (bool)_GLIBCXX_USE_CXX11_ABI;
   m.def("init", &init, "the C ABI entry points (name -> address) of the loaded libmi355r.so");
   m.def("render_views", &render_views, "fused render forward (+ autograd backward) through the C ABI");
   m.def("pose_loss", &pose_loss, "calc_loss with its gradients (+ autograd backward) through the C ABI");

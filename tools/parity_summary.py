@@ -22,13 +22,27 @@ def main(path):
                          int(p.group("ill")) if p.group("ill") else None,
                          p.group("g64"), p.group("o64")))
     print(f"{len(rows)} [parity] lines from {path}")
-    print(f"{'test':58s} {'quantity':42s} {'n':>8s} {'err/lim':>8s} {'ill':>6s} {'GPU/f64':>9s} {'f32orc/f64':>10s}")
+    print("columns: worst err/limit; ill-conditioned entries; max distance to the float64 shadow in units of the bar, "
+          "of the GPU and of the f32 oracle, and their ratio (> 1: the GPU is farther from f64 than the f32 oracle)")
+    print(f"{'test':58s} {'quantity':52s} {'n':>8s} {'err/lim':>8s} {'ill':>6s} {'GPU/f64':>9s} {'f32orc/f64':>10s} "
+          f"{'ratio':>6s}")
+    farther = []
     for t, nm, n, wl, ill, g, o in rows:
-        print(f"{(t or '?')[:58]:58s} {nm[:42]:42s} {n:8d} {wl:8.3f} {'' if ill is None else ill:>6} "
-              f"{g or '':>9s} {o or '':>10s}")
+        ratio = ""
+        if g is not None and o is not None:
+            gf, of = float(g), float(o)
+            ratio = f"{gf / of:.2f}" if of > 0 else ""
+            if gf > of and gf > 1.0:
+                farther.append((t, nm, gf, of))
+        print(f"{(t or '?')[:58]:58s} {nm[:52]:52s} {n:8d} {wl:8.3f} {'' if ill is None else ill:>6} "
+              f"{g or '':>9s} {o or '':>10s} {ratio:>6s}")
     worst = max(rows, key=lambda r: r[3]) if rows else None
     if worst:
         print(f"\nworst err/limit over all lines: {worst[3]:.3f} ({worst[0]}: {worst[1]})")
+    print(f"\nquantities where the GPU is farther from the float64 shadow than the f32 oracle (and more than one "
+          f"bar): {len(farther)}")
+    for t, nm, gf, of in sorted(farther, key=lambda r: -r[2] / r[3]):
+        print(f"  {(t or '?')[:58]:58s} {nm[:52]:52s} GPU {gf:9.3f}  f32 oracle {of:9.3f}  ratio {gf / of:.2f}")
 
 
 if __name__ == "__main__":

@@ -818,7 +818,7 @@ def secondary_steps(args, dev, world, rank):
     so that the driver's record carries them (bench.py --mode pose / c5 / soft print their full lines)."""
     out = {}
     plans = (("pose_step", bench_pose, dict(size=512, views=64, steps=30, warmup=10)),
-             ("c5_step", bench_c5, dict(size=1024, views=5, steps=20, warmup=8)),
+             ("c5_step", bench_c5, dict(size=1024, views=5, steps=60, warmup=10)),
              ("soft_step", bench_soft, dict(size=128, views=64, steps=10, warmup=3, mesh="cow")))
     for name, fn, over in plans:
         torch.cuda.empty_cache()  # (the headline's graph pool and fragment buffers are gone: start each clean)

@@ -28,7 +28,14 @@ def test_camera_key_tracks_edits_replacements_and_new_attributes():
     assert k2 != k1
     cams.extra = torch.zeros(2)  # new tensor attribute
     k3 = _param_key(cams)
-    assert k3 != k2 and any(k == "extra" for k, *_ in k3)
+    assert k3 != k2 and len(k3) == len(k2) + 2  # its (storage, version) joins the key
+    cams.note = "x"  # any assignment bumps the generation
+    assert _param_key(cams) != k3
+    c0 = cams[0]  # a copy starts its own generation and key
+    kc = _param_key(c0)
+    assert _param_key(c0) == kc
+    c0.T[0, 0] = 1.0
+    assert _param_key(c0) != kc
 
 
 def test_cached_ndc_affine_follows_the_focal_length():

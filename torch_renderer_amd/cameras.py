@@ -27,6 +27,13 @@ class CamerasBase:
         self.R = R.float().reshape(-1, 3, 3)
         self.T = T.float().reshape(-1, 3)
 
+    def __setattr__(self, k, v):
+        # every attribute assignment bumps the generation _param_key keys on (the scalar attributes and the
+        # set of tensor attributes change only through here; in-place tensor edits are seen by their versions)
+        d = self.__dict__
+        d["_attr_gen"] = d.get("_attr_gen", 0) + 1
+        object.__setattr__(self, k, v)
+
     def __len__(self):
         return max(self.R.shape[0], self.T.shape[0], getattr(self, "_n_intr", 1))
 
@@ -132,29 +139,28 @@ class FoVPerspectiveCameras(CamerasBase):
 
 
 def _param_key(cameras):
-    """The caches' key: (name, storage, version) of the camera's tensor attributes and (name, value) of its
-    scalar ones (FoV cameras keep fov / aspect_ratio / znear as floats). The attribute names are listed
-    once per set of names (an eager loop calls this several times per render)."""
-    d = vars(cameras)
-    keys = tuple(k for k in d if not k.startswith("_") or k == "_in_ndc")
+    """The caches' key: the camera's attribute generation (CamerasBase.__setattr__ bumps it on every
+    assignment, so it covers the scalar attributes — FoV cameras keep fov / aspect_ratio / znear as floats —
+    and which tensors are attached) and (storage, version) of its tensor attributes (in-place edits). The
+    tensor attribute names are listed once per generation (an eager loop calls this on every render)."""
+    d = cameras.__dict__
+    gen = d.get("_attr_gen", 0)
     names = d.get("_pk_names")
-    if names is None or names[0] != keys:
-        names = (keys, tuple(sorted(keys)))
+    if names is None or names[0] != gen:
+        names = (gen, tuple(k for k in sorted(d) if (not k.startswith("_") or k == "_in_ndc") and torch.is_tensor(d[k])))
         d["_pk_names"] = names
-    out = []
+    out = [gen]
     for k in names[1]:
         v = d[k]
-        if torch.is_tensor(v):
-            out.append((k, v.data_ptr(), v._version))
-        elif isinstance(v, (bool, int, float, str)):
-            out.append((k, v))
+        out.append(v.data_ptr())
+        out.append(v._version)
     return tuple(out)
 
 
 def cached_ndc_affine(cameras: CamerasBase, image_size, device):
     """ndc_affine on `device`, recomputed only when the camera's tensors change (their
     storage or version) — the per-call double-precision conversions are host-side launches."""
-    key = (tuple(int(x) for x in image_size), str(device), _param_key(cameras))
+    key = (int(image_size[0]), int(image_size[1]), device, _param_key(cameras))
     c = cameras.__dict__.get("_ndc_cache")
     if c is None or c[0] != key:
         c = (key, cameras.ndc_affine(image_size).to(device).contiguous())
@@ -164,7 +170,7 @@ def cached_ndc_affine(cameras: CamerasBase, image_size, device):
 
 def cached_camera_center(cameras: CamerasBase, device):
     """get_camera_center() (camera's own R, T) on `device`, cached like cached_ndc_affine."""
-    key = (str(device), _param_key(cameras))
+    key = (device, _param_key(cameras))
     c = cameras.__dict__.get("_cc_cache")
     if c is None or c[0] != key:
         c = (key, cameras.get_camera_center().to(device).contiguous())

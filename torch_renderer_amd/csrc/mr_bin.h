@@ -898,6 +898,7 @@ struct ViewBinParams {
   ShadeRec* srec;
   int64_t Fs;
   int nsrec_wg;  // ShadeRec workgroups (N .. N + nsrec_wg - 1); the background ones follow (k_bin_view<MODE, CH>)
+  int srec_fpw;  // faces per ShadeRec workgroup (a multiple of 256: srec_wgs)
   int stage_cap;  // list entries of a view staged in LDS (after the histogram)
   // bands > 1: the records of each (view, band) listed by k_band_bucket (blist[(n B + b) bcap + e],
   // bcnt[n B + b] of them); NULL: every band reads all of the view's rectangles
@@ -967,6 +968,12 @@ MR_DEV void rect_tiles(uint32_t r, int TX, int by0, int by1, Fn&& fn) {
 // rectangles (4 B each, L2-resident after the first band) and bins the part of each inside its rows.
 // Bands share nothing, so a view's binning runs on `bands` CUs at once instead of one (a single
 // workgroup per view was the fragment pass's 26-us critical path with 64 views on 256 CUs).
+#ifdef MR_XP_BV_STAMP  // experiment builds only: phase ends of a binning workgroup (k_bin_view's stamps)
+__shared__ unsigned long long g_bv_ph[5];
+#define BV_PH(i) do { if (threadIdx.x == 0) g_bv_ph[i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define BV_PH(i) do { } while (0)
+#endif
 MR_DEV void bin_view_body(const ViewBinParams& P) {
   extern __shared__ __attribute__((aligned(16))) int hist[];  // Tb (+ Tb/64 pad): counts, then fill cursors
   __shared__ int part[16];
@@ -977,12 +984,9 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   const int blk = blockIdx.x, t = threadIdx.x;
   const int B = P.bands;
   if (blk >= P.nviews * B) {  // ShadeRec workgroups (they run on the CUs the views leave idle)
-    const int64_t f = (int64_t)(blk - P.nviews * B) * 1024 + t;
-    if (f < P.Fs) {
-      ShadeRec R;
-      make_shade_rec(P.S, (uint32_t)f, R);
-      P.srec[f] = R;
-    }
+    const int64_t fa = (int64_t)(blk - P.nviews * B) * P.srec_fpw;
+    const int64_t nf = P.Fs - fa < P.srec_fpw ? P.Fs - fa : P.srec_fpw;
+    if (nf > 0) pack_shade_recs(P.S, P.srec, fa, nf, (float*)hist);
     return;
   }
   const int n = blk / B, b = blk - n * B;
@@ -998,6 +1002,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
   for (int i = t; i < HS; i += 1024) hist[i] = 0;
   if (t == 0) nmulti = 0;
   lds_barrier();
+  BV_PH(0);
   const int nq = P.clipz ? 2 : 1;
   // the entries this workgroup bins: the view's records (both triangles of a split face per entry), or
   // with band lists the records k_band_bucket listed for this band (one per entry)
@@ -1040,6 +1045,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       for (int q = 0; q < 2; ++q) rect_tiles(rr[k][q], P.TX, by0, by1, [&](int tt) { atomicAdd(&hist[tt + (tt >> 6)], 1); });
   }
   lds_barrier();
+  BV_PH(1);
   // scan: each thread owns a run of C consecutive tiles (entries, units, slots in tile order)
   const int C = (Tb + 1023) / 1024;
   const int t0 = min(t * C, Tb), t1 = min(t0 + C, Tb);
@@ -1070,6 +1076,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     base[2] = (long long)atomicAdd((unsigned long long*)(P.ctr + CTR_ENTRIES64), (unsigned long long)te);
   }
   lds_barrier();
+  BV_PH(2);
   const long long vb = base[2];
   // tile list starts are absolute pool positions here (view base 0): a view's bands take separate
   // ranges of the pool. (Readers use vbase[n] + start[tile], as on the count -> scan path.)
@@ -1111,6 +1118,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
     ex += cc;
   }
   lds_barrier();
+  BV_PH(3);
   const int nm = min(nmulti, MR_SCAN_MULTI);
   for (int i = t; i < nm * 64; i += 1024) P.tkey[(int64_t)multi_slot[i >> 6] * 64 + (i & 63)] = MR_KEY_EMPTY;
   // fill: the band's entries occupy [vb, vb + te) of the pool; the first stage_cap of them are
@@ -1139,6 +1147,7 @@ MR_DEV void bin_view_body(const ViewBinParams& P) {
       }
   }
   lds_barrier();
+  BV_PH(4);
   for (int i = t; i < lst; i += 1024)
     if (vb + i < P.list_cap) P.list[vb + i] = stage[i];
 }

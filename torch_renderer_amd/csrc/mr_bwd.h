@@ -477,7 +477,9 @@ MR_DEV void seg_flush_fix(int nt, unsigned long long* __restrict__ gfix, float* 
       const int j = 64 * i + lane;
       if (j < tot) {
         const float x = lrow[j];
-        const uint32_t e = (uint32_t)lkey[r] * (uint32_t)STRIDE + (uint32_t)c;
+        // a geometry-only run (ACC = 9 position values) into an ACC-wide row: value 3 corner + k -> col_pos
+        const int cc = (ACC == 9 && STRIDE == 27) ? (c / 3) * 6 + (c - (c / 3) * 3) : c;
+        const uint32_t e = (uint32_t)lkey[r] * (uint32_t)STRIDE + (uint32_t)cc;
         if (fabsf(x) < MR_FIX_MAX) {
           if (x != 0.0f) atomicAdd(gfix + e, (unsigned long long)fix_of(x));
         } else {
@@ -795,11 +797,11 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
           if (GEO) {
-            row[3 * c + k] = gX[k];
+            row[3 * c + k] = gX[k];  // (positions only; seg_flush_fix places them in the ACC-wide row)
           } else {
-            row[3 * c + k] = b[c] * gP[k] + gX[k];
-            row[9 + 3 * c + k] = b[c] * gNn[k];
-            if (ACC == 27) row[18 + 3 * c + k] = b[c] * gt3[k];
+            row[col_pos<ACC>(c, k)] = b[c] * gP[k] + gX[k];
+            row[col_nrm<ACC>(c, k)] = b[c] * gNn[k];
+            if (ACC == 27) row[col_rgb<ACC>(c, k)] = b[c] * gt3[k];
           }
         }
       }
@@ -822,9 +824,12 @@ __global__ void __launch_bounds__(256) MR_BWD_ATTR k_bwd_fused(RenderBwdParams P
 // out (N,12) PyTorch3D-frame R/T grads, or (gRcv, gtcv) non-null: the same grads written
 // straight in the OpenCV frame (k_view_grads_to_opencv's chain rule, saving its launch).
 // vslot holds (first slot, count) of each (view, band) range: N * bands firsts, then the counts.
+// NT threads per workgroup (256, or 1024 inside k_rt_vgrad_a/b: four times the rows in flight).
+template <int NT = 256>
 MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict__ vslot, int N, int bands,
                            float* __restrict__ out, float* __restrict__ gRcv, float* __restrict__ gtcv, int n) {
-  __shared__ float sm[12][4];
+  constexpr int NW = NT / 64;
+  __shared__ float sm[12][NW];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   // each thread sums whole 48-B partial rows (three 16-B loads in flight together instead of 12
   // dependent passes over the rows); per component the order is the same as a per-component loop
@@ -832,7 +837,7 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
 #pragma unroll
   for (int i = 0; i < 12; ++i) acc[i] = 0.0f;
   // the view's slots in tile order: its bands' ranges concatenated (band b holds tile rows above band b+1's).
-  // Thread t sums the slots t, t + 256, ... of that sequence in that order, whatever the band split — the
+  // Thread t sums the slots t, t + NT, ... of that sequence in that order, whatever the band split — the
   // result does not depend on how many bands (i.e. on the batch size: a view's gradient is bitwise the same
   // in any batch). Four positions' rows are loaded together (a single-view batch has thousands of slots:
   // one dependent load per 256 slots made k_rt_reduce 24 us at C5), then added in sequence order.
@@ -852,17 +857,21 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
   }
   __syncthreads();
   const int total = bpre[bands];
-  int cb = 0;  // this thread's positions only increase: the band pointer advances with them
-  auto slot_at = [&](int p) {  // sequence position -> slot
-    while (cb + 1 < bands && bpre[cb + 1] <= p) ++cb;
-    return bfirst[cb] + (p - bpre[cb]);
+  auto slot_at = [&](int p) {  // sequence position -> slot: the last band starting at or before p (binary search:
+    int lo = 0, hi = bands - 1;  // a walk advanced ~15 of C5's 64 bands per 1024 positions, one LDS read each)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (bpre[mid] <= p) lo = mid;
+      else hi = mid - 1;
+    }
+    return bfirst[lo] + (p - bpre[lo]);
   };
 #pragma unroll 1
-  for (int p0 = threadIdx.x; p0 < total; p0 += 4 * 256) {
+  for (int p0 = threadIdx.x; p0 < total; p0 += 4 * NT) {
     float4 r[4][3];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int p = p0 + u * 256 < total ? p0 + u * 256 : total - 1;
+      const int p = p0 + u * NT < total ? p0 + u * NT : total - 1;
       const float4* q = (const float4*)(part + (int64_t)slot_at(p) * 12);
       r[u][0] = q[0];
       r[u][1] = q[1];
@@ -870,7 +879,7 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if (p0 + u * 256 >= total) break;
+      if (p0 + u * NT >= total) break;
       const float4 a = r[u][0], c4 = r[u][1], c = r[u][2];
       acc[0] += a.x; acc[1] += a.y; acc[2] += a.z; acc[3] += a.w;
       acc[4] += c4.x; acc[5] += c4.y; acc[6] += c4.z; acc[7] += c4.w;
@@ -885,7 +894,9 @@ MR_DEV void rt_reduce_view(const float* __restrict__ part, const int* __restrict
   __syncthreads();
   const int i = threadIdx.x;
   if (i >= 12) return;
-  const float v = ((sm[i][0] + sm[i][1]) + sm[i][2]) + sm[i][3];
+  float v = sm[i][0];
+#pragma unroll
+  for (int k = 1; k < NW; ++k) v += sm[i][k];  // ((w0 + w1) + w2) + ...
   if (!gRcv) {
     out[n * 12 + i] = v;
   } else if (i < 9) {  // dL/dR_cv[b][a] = dL/dR_p3d[a][b] * s[b]

@@ -48,6 +48,13 @@ MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)
 // Per-face total component i: the fixed-point sum plus the float-atomic remainder.
 // (rem false: the float remainder rows are all zero and not read — fix_to_f never returns -0, so the
 // sum with a zero remainder is the same bits)
+// Columns of a face's gradient-total row: ACC = 18 holds the three corners' position then normal columns
+// (3 c + k, 9 + 3 c + k); ACC = 27 (vertex colours) keeps each corner's position and colour columns adjacent
+// (6 c + k, 6 c + 3 + k; normals 18 + 3 c + k), so that a vertex gathers one 48-B piece of each incident face's
+// row instead of two 24-B pieces 144 B apart (the C5 gathers are HBM-bound: r6n_pmc_c5.json).
+template <int ACC> MR_DEV constexpr int col_pos(int c, int k) { return ACC == 27 ? 6 * c + k : 3 * c + k; }
+template <int ACC> MR_DEV constexpr int col_rgb(int c, int k) { return 6 * c + 3 + k; }
+template <int ACC> MR_DEV constexpr int col_nrm(int c, int k) { return ACC == 27 ? 18 + 3 * c + k : 9 + 3 * c + k; }
 MR_DEV float fix_total(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i,
                        bool rem = true) {
   return gfix ? (rem ? fix_to_f(gfix[i]) + gflt[i] : fix_to_f(gfix[i])) : gflt[i];

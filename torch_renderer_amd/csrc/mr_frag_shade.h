@@ -205,9 +205,9 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
         key = face;
         for (int c = 0; c < 3; ++c)
           for (int q = 0; q < 3; ++q) {
-            row[3 * c + q] = b[c] * gP[q];
-            row[9 + 3 * c + q] = b[c] * gNn[q];
-            if (ACC == 27) row[18 + 3 * c + q] = b[c] * gtex[q];
+            row[col_pos<ACC>(c, q)] = b[c] * gP[q];
+            row[col_nrm<ACC>(c, q)] = b[c] * gNn[q];
+            if (ACC == 27) row[col_rgb<ACC>(c, q)] = b[c] * gtex[q];
           }
         if (S.tex_kind == 2) {
           if (P.gmap) tex_map_bwd(S, C.tap, gtex, P.gmap);
@@ -255,9 +255,9 @@ __global__ void __launch_bounds__(256) k_frag_shade_bwd(FragShadeParams P) {
         key = face;
         for (int c = 0; c < 3; ++c)
           for (int q = 0; q < 3; ++q) {
-            row[3 * c + q] = b[c] * gP[q];
-            row[9 + 3 * c + q] = b[c] * gNn[q];
-            if (ACC == 27) row[18 + 3 * c + q] = b[c] * gtex[q];
+            row[col_pos<ACC>(c, q)] = b[c] * gP[q];
+            row[col_nrm<ACC>(c, q)] = b[c] * gNn[q];
+            if (ACC == 27) row[col_rgb<ACC>(c, q)] = b[c] * gtex[q];
           }
         if (S.tex_kind == 2) {
           if (P.gmap) tex_map_bwd(S, C.tap, gtex, P.gmap);

@@ -163,6 +163,19 @@ static size_t view_lds_bytes() {
 static int64_t bin_bg_wgs(int64_t nbin, int64_t sb, bool banded) {
   return (int64_t)num_cus() * (banded ? MR_BG_WG_PER_CU : 1) - nbin - sb;
 }
+// ShadeRec workgroups of the k_bin_view launch and their faces each (a multiple of 256, pack_shade_recs' pass).
+// 1024 faces per workgroup: smaller shares took workgroups from the background and slowed the headline's raster
+// (r6n: sb 6 -> 23, k_tile_raster +3 us), and with the corner-parallel packing 1024 faces take ~13 us, under the
+// binning's critical path at C5 (20 us) and at the headline (38 us).
+#ifndef MR_SREC_FPW
+#define MR_SREC_FPW 1024
+#endif
+static int64_t srec_wgs(int64_t F, int64_t nbin, int* fpw_out = nullptr) {
+  (void)nbin;
+  if (F <= 0) return 0;
+  if (fpw_out) *fpw_out = MR_SREC_FPW;
+  return ceil_div(F, MR_SREC_FPW);
+}
 // Background chunks the k_bin_view launch takes over (chunks of 64 lanes x 4 pixels when W % 4 == 0,
 // else 64 pixels); 0 when the binning leaves no workgroup slot free.
 static int64_t bg_chunks(int64_t N, int64_t nbin, int64_t sb, int H, int W, int mode) {
@@ -187,13 +200,13 @@ static int launch_bin_view(const SetupParams& SP, const RasterWS& w, const BinGe
     V.S = *S;
     V.srec = Pf ? (ShadeRec*)Pf->srec : w.srec;  // the call's ShadeRec slot
     V.Fs = F;
-    sb = ceil_div(F, 1024);
   }
-  V.nsrec_wg = (int)sb;
   V.T = g.T; V.TX = g.TX; V.TY = g.TY; V.mfpb = g.mfpb; V.clipz = SP.clipz;
   const int B = bin_bands(N, g);
   V.bands = B;
   const int64_t nbin = N * B;
+  if (S) sb = srec_wgs(F, nbin, &V.srec_fpw);
+  V.nsrec_wg = (int)sb;
   V.list_cap = g.list_cap; V.NF = SP.NF;
   V.rects = w.rects; V.first = first; V.view_count = view_count; V.F = F;
   V.cnt = w.cnt; V.start = w.start; V.vbase = w.vbase; V.tdone = w.tdone; V.vslot = w.vslot; V.stile = w.stile;
@@ -236,8 +249,9 @@ int64_t mr_binning_background_pixels(int64_t N, int64_t F, int32_t H, int32_t W,
   if (N <= 0 || H <= 0 || W <= 0) return 0;
   BinGeom g = bin_geom(H, W, N, N * (F > 0 ? F : 1), 0);
   if (!view_binning(g, N, N * (F > 0 ? F : 1))) return 0;
-  const int64_t sb = mode == 1 ? ceil_div(F, 1024) : 0;
-  const int64_t px = bg_chunks(N, N * bin_bands(N, g), sb, H, W, mode) * ((W & 3) == 0 ? 256 : 64);
+  const int64_t nbin = N * bin_bands(N, g);
+  const int64_t sb = mode == 1 ? srec_wgs(F, nbin) : 0;
+  const int64_t px = bg_chunks(N, nbin, sb, H, W, mode) * ((W & 3) == 0 ? 256 : 64);
   return std::min<int64_t>(px, N * (int64_t)H * W);
 }
 
@@ -1060,14 +1074,18 @@ static int32_t render_backward(const mr_mesh_t* m, const float* vraw, const mr_v
   const int vb = ceil_div(m->V * MR_VL, 256);
   // the forward's slot ranges: one per (view, band) on the per-view binning, one per view otherwise
   const int bands = view_binning(g, N, NF) ? bin_bands(N, g) : 1;
+  RtReduce RR;
+  RR.part = rt_part; RR.vslot = w.vslot; RR.N = (int)N; RR.bands = bands;
+  RR.gviews = gviews; RR.gRcv = gRcv; RR.gtcv = gtcv;
+  const int vbw = ceil_div(m->V * MR_VL, MR_VGRAD_NT);  // vertex-gather workgroups of k_rt_vgrad_a / _b
   if (!use_n) {  // no normal chain: the R/T reduction and the vertex gathers in one launch
-    if (vcol) MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
-    else MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
+    if (vcol) MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<27><<<(unsigned)(N + vbw), MR_VGRAD_NT, 0, st>>>(RR, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
+    else MR_TIMED(KID_RT_VGRAD_B, st, (k_rt_vgrad_b<18><<<(unsigned)(N + vbw), MR_VGRAD_NT, 0, st>>>(RR, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gverts, gcol)));
     MR_CHECK_LAUNCH("k_rt_vgrad_b");
     return MR_OK;
   }
-  if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
-  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vb), 256, 0, st>>>(rt_part, w.vslot, (int)N, bands, gviews, gRcv, gtcv, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
+  if (vcol) MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<27><<<(unsigned)(N + vbw), MR_VGRAD_NT, 0, st>>>(RR, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
+  else MR_TIMED(KID_RT_VGRAD_A, st, (k_rt_vgrad_a<18><<<(unsigned)(N + vbw), MR_VGRAD_NT, 0, st>>>(RR, m->V, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, vraw, gnu)));
   MR_CHECK_LAUNCH("k_rt_vgrad_a");
   if (vcol) {
     MR_TIMED(KID_VGRAD_B, st, (k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, gfix, gface, P.fflag, gnu, use_n, gverts, gcol)));
@@ -1180,8 +1198,12 @@ int32_t mr_shade_fragments_backward(const mr_mesh_t* m, const float* vraw, const
   const int use_n = sp->light_kind == 0 && !P.sil;
   const int vb = ceil_div(m->V * MR_VL, 256);
   if (use_n) {
-    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
-    else k_rt_vgrad_a<18><<<(unsigned)vb, 256, 0, st>>>(nullptr, nullptr, 0, 1, nullptr, nullptr, nullptr, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
+    RtReduce R0;
+    memset(&R0, 0, sizeof(R0));
+    R0.bands = 1;
+    const int vbw = ceil_div(m->V * MR_VL, MR_VGRAD_NT);
+    if (vcol) k_rt_vgrad_a<27><<<(unsigned)vbw, MR_VGRAD_NT, 0, st>>>(R0, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
+    else k_rt_vgrad_a<18><<<(unsigned)vbw, MR_VGRAD_NT, 0, st>>>(R0, m->V, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, vraw, gnu);
     MR_CHECK_LAUNCH("k_rt_vgrad_a");
   }
   if (vcol) k_vgrad_b<27><<<vb, 256, 0, st>>>(m->V, m->verts, m->faces, m->vadj_ptr, m->vadj, nullptr, gface, nullptr, gnu, use_n, g_verts, g_vcolors);
@@ -1286,6 +1308,14 @@ int32_t mr_timing_kernel_count(void) { return KID_COUNT; }
 int32_t mr_xp_bwd_stamps(unsigned long long* out, int32_t waves) {
   if (waves > MR_XP_WAVES) waves = MR_XP_WAVES;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bwd_stamp), sizeof(unsigned long long) * 8 * (size_t)waves, 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? MR_OK : MR_ELAUNCH;
+}
+#endif
+#ifdef MR_XP_BV_STAMP
+// experiment builds only: the last k_bin_view<MODE, CH> launch's per-workgroup stamps (8 u64 per workgroup)
+int32_t mr_xp_bv_stamps(unsigned long long* out, int32_t wgs) {
+  if (wgs > MR_XP_BV_WGS) wgs = MR_XP_BV_WGS;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bv_stamp), sizeof(unsigned long long) * 8 * (size_t)wgs, 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? MR_OK : MR_ELAUNCH;
 }
 #endif

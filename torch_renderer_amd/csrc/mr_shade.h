@@ -277,6 +277,7 @@ struct PixGeom {
 struct __attribute__((aligned(16))) ShadeRec {
   float X[9], N[9], A[9], pad[3];
 };
+static_assert(sizeof(ShadeRec) == 128, "ShadeRec is 8 float4 (pack_shade_recs, load_geom)");
 
 MR_DEV void gather_geom(const ShadeParams& S, uint32_t face, PixGeom& G) {
   // Every field is written on every path and every loop is unrolled: a conditionally
@@ -310,6 +311,52 @@ MR_DEV void make_shade_rec(const ShadeParams& S, uint32_t face, ShadeRec& R) {
       R.A[3 * c + k] = S.tex_kind == 1 ? G.col[c][k] : k < 2 ? G.uv[c][k] : 0.0f;
     }
   R.pad[0] = R.pad[1] = R.pad[2] = 0.0f;
+}
+
+// The ShadeRecs of faces [fa, fa + nf) packed by one 1024-thread workgroup, 256 faces per pass, bitwise
+// make_shade_rec's records. Four lanes per face: lane c < 3 gathers corner c's vertex (one 12-B load per
+// attribute instead of three 4-B ones), lane 3 the padding; the records are staged in LDS (`stage`, 32 KB) and
+// stored as consecutive 16-B pieces. One lane per face writing its whole 128-B record made every store
+// instruction touch ~64 cache lines, and the C5 render's 81,920 records took 13-19 us on 80 workgroups
+// (profiles/r6n_binview_stamps.txt); the L1's address processing, not HBM, bounded it. Uniform call.
+struct __attribute__((packed, aligned(4))) F3u {
+  float x, y, z;
+};
+MR_DEV void pack_shade_recs(const ShadeParams& S, ShadeRec* __restrict__ out, int64_t fa, int64_t nf,
+                            float* __restrict__ stage) {
+  const int t = (int)threadIdx.x, lf = t >> 2, c = t & 3;
+#pragma unroll 1
+  for (int64_t p = 0; p < nf; p += 256) {
+    const int np = (int)(nf - p < 256 ? nf - p : 256);
+    float* r = stage + lf * 32;
+    if (lf < np) {
+      const int64_t f = fa + p + lf;
+      if (c < 3) {
+        const int64_t v = S.faces[3 * f + c];
+        const F3u X = *(const F3u*)(S.verts + 3 * v);
+        F3u Nn = {0.0f, 0.0f, 0.0f}, A = {0.0f, 0.0f, 0.0f};
+        if (S.light_kind == 0) Nn = *(const F3u*)(S.vnormals + 3 * v);
+        if (S.tex_kind == 1) {
+          A = *(const F3u*)(S.vcolors + 3 * v);
+        } else if (S.tex_kind == 2) {
+          const int64_t tu = S.faces_uvs[3 * f + c];
+          A.x = S.verts_uvs[2 * tu];
+          A.y = S.verts_uvs[2 * tu + 1];
+        }
+        r[3 * c] = X.x; r[3 * c + 1] = X.y; r[3 * c + 2] = X.z;
+        r[9 + 3 * c] = Nn.x; r[9 + 3 * c + 1] = Nn.y; r[9 + 3 * c + 2] = Nn.z;
+        r[18 + 3 * c] = A.x; r[18 + 3 * c + 1] = A.y; r[18 + 3 * c + 2] = A.z;
+      } else {
+#pragma unroll
+        for (int k = 27; k < 32; ++k) r[k] = 0.0f;
+      }
+    }
+    __syncthreads();
+    float4* o = (float4*)(out + fa + p);
+    const float4* s4 = (const float4*)stage;
+    for (int i = t; i < np * 8; i += 1024) o[i] = s4[i];
+    __syncthreads();
+  }
 }
 
 MR_DEV void load_geom(const ShadeRec* __restrict__ recs, uint32_t face, PixGeom& G) {

@@ -513,8 +513,31 @@ __global__ void __launch_bounds__(256) k_fill(FwdParams P) {
 // most CUs idle, so workgroups past the views (and the ShadeRec ones) stream the background of
 // the first F.fill_first chunks (view-major) while the views bin; k_tile_raster writes the rest.
 // The background does not depend on the raster (k_shade overwrites the covered pixels later).
+// Experiment builds only (-DMR_XP_BV_STAMP, tools/binview_stamps.py): per workgroup of the last launch, the
+// global clock when its first wave starts and when its last wave ends, its role (0 binning, 1 ShadeRec,
+// 2 background) and a binning workgroup's phase ends (BV_PH). Reads of the clock counters only; vector stores.
+#ifdef MR_XP_BV_STAMP
+#define MR_XP_BV_WGS 4096
+__device__ unsigned long long g_bv_stamp[MR_XP_BV_WGS * 8];
+#endif
 template <int MODE, int CH>
 __global__ void __launch_bounds__(1024) k_bin_view(ViewBinParams P, FwdParams F) {
+#ifdef MR_XP_BV_STAMP
+  const unsigned long long xp_t0 = __builtin_amdgcn_s_memrealtime();
+  const int xp_role = (int)blockIdx.x < P.nviews * P.bands ? 0 : (int)blockIdx.x < P.nviews * P.bands + P.nsrec_wg ? 1 : 2;
+  struct XpEnd {
+    unsigned long long t0;
+    int role;
+    __device__ ~XpEnd() {
+      __syncthreads();
+      const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+      const int i = (int)threadIdx.x;
+      if (blockIdx.x < MR_XP_BV_WGS && i < 8)
+        g_bv_stamp[(size_t)blockIdx.x * 8 + i] = i == 0 ? t0 : i == 1 ? t1 : i == 2 ? (unsigned long long)role
+                                               : role == 0 ? g_bv_ph[i - 3] : 0ull;
+    }
+  } xp_end{xp_t0, xp_role};
+#endif
   const int b = (int)blockIdx.x - P.nviews * P.bands - P.nsrec_wg;
   if (b < 0) {
     bin_view_body(P);

@@ -63,7 +63,7 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
   if (act) {
     for (int e = ptr[v] + j; e < ptr[v + 1]; e += MR_VL) {
       const int f = adj[e] >> 2, c = adj[e] & 3;
-      for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 9 + 3 * c + k, rem);
+      for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_nrm<ACC>(c, k), rem);
     }
   }
 #pragma unroll
@@ -81,16 +81,35 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
 // The per-view R/T reduction and the vertex-normal gradient read disjoint inputs written by
 // k_bwd_fused, so one launch does both: blocks [0, N) reduce views, the rest run k_vgrad_a
 // (saves a dependent launch of two tiny kernels per step).
+// The vertex gathers' blocks in XCD-contiguous order: the hardware deals a launch's workgroups round-robin over
+// the 8 XCDs (each with its own L2), so block j of nb is remapped to vertex range x * nb / 8 + j / 8 of its XCD x
+// (= j mod 8 up to a fixed rotation) — neighbouring vertices, which gather the same face rows, share an L2
+// instead of fetching each row from HBM once per XCD. A bijection on [0, nb).
+MR_DEV int64_t xcd_block(int64_t j, int64_t nb) {
+  const int64_t x = j & 7, q = nb >> 3, r = nb & 7;
+  return x * q + (x < r ? x : r) + (j >> 3);
+}
+// (blocks [0, N): rt_reduce_view, one workgroup per view)
+struct RtReduce {
+  const float* part;
+  const int* vslot;
+  int N, bands;
+  float *gviews, *gRcv, *gtcv;
+};
+// threads per workgroup of k_rt_vgrad_a / _b: the view reduction's rows in flight (C5's single view: k_rt_vgrad_b
+// 22.3 us at 256, 18.9-19.2 at 512; 1024 slowed the headline's k_rt_vgrad_a 7.6 -> 8.7 us; r6n_vgrad_nt_ab.txt)
+#ifndef MR_VGRAD_NT
+#define MR_VGRAD_NT 512
+#endif
 template <int ACC>
-__global__ void __launch_bounds__(256) k_rt_vgrad_a(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                    int N, int bands, float* __restrict__ gviews, float* __restrict__ gRcv,
-                                                    float* __restrict__ gtcv, int64_t V,
-                                                    const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
-                                                    const unsigned long long* __restrict__ gfix,
-                                                    const float* __restrict__ gface, const int* __restrict__ fflag,
-                                                    const float* __restrict__ vraw, float* __restrict__ gnu) {
-  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, bands, gviews, gRcv, gtcv, blockIdx.x);
-  else vgrad_a_block<ACC>(V, ptr, adj, gfix, gface, fflag, vraw, gnu, (int64_t)blockIdx.x - N);
+__global__ void __launch_bounds__(MR_VGRAD_NT) k_rt_vgrad_a(RtReduce R, int64_t V,
+                                                            const int32_t* __restrict__ ptr, const int32_t* __restrict__ adj,
+                                                            const unsigned long long* __restrict__ gfix,
+                                                            const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                            const float* __restrict__ vraw, float* __restrict__ gnu) {
+  if ((int)blockIdx.x < R.N) rt_reduce_view<MR_VGRAD_NT>(R.part, R.vslot, R.N, R.bands, R.gviews, R.gRcv, R.gtcv, blockIdx.x);
+  else vgrad_a_block<ACC>(V, ptr, adj, gfix, gface, fflag, vraw, gnu,
+                          xcd_block((int64_t)blockIdx.x - R.N, (int64_t)gridDim.x - R.N));
 }
 
 // B: grad_verts[v] = sum over incident (f, c) of position rows + cross-product backward of the face normal.
@@ -109,9 +128,9 @@ MR_DEV void vgrad_b_block(int64_t V, const float* __restrict__ verts, const int3
   const int e0 = act ? ptr[v] + j : 0, e1 = act ? ptr[v + 1] : 0;
   for (int e = e0; e < e1; e += MR_VL) {
     const int f = adj[e] >> 2, c = adj[e] & 3;
-    for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + 3 * c + k, rem);
+    for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_pos<ACC>(c, k), rem);
     if (ACC == 27)
-      for (int k = 0; k < 3; ++k) gc[k] += fix_total(gfix, gface, (int64_t)f * ACC + 18 + 3 * c + k, rem);
+      for (int k = 0; k < 3; ++k) gc[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_rgb<ACC>(c, k), rem);
     if (use_normals) {
       const int32_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
       float gn[3], a[3], b[3];
@@ -148,22 +167,21 @@ __global__ void __launch_bounds__(256) k_vgrad_b(int64_t V, const float* __restr
                                                  const float* __restrict__ gface, const int* __restrict__ fflag,
                                                  const float* __restrict__ gnu, int use_normals, float* __restrict__ gverts,
                                                  float* __restrict__ gcol) {
-  vgrad_b_block<ACC>(V, verts, faces, ptr, adj, gfix, gface, fflag, gnu, use_normals, gverts, gcol, blockIdx.x);
+  vgrad_b_block<ACC>(V, verts, faces, ptr, adj, gfix, gface, fflag, gnu, use_normals, gverts, gcol,
+                     xcd_block(blockIdx.x, gridDim.x));
 }
 // Without vertex normals in the shading (no k_vgrad_a step): the per-view R/T reduction (blocks [0, N)) and
 // the vertex gradients (the rest) read disjoint inputs, so one launch runs both side by side (C5: a single
 // view's reduction is one long-running workgroup that the gathers now overlap).
 template <int ACC>
-__global__ void __launch_bounds__(256) k_rt_vgrad_b(const float* __restrict__ part, const int* __restrict__ vslot,
-                                                    int N, int bands, float* __restrict__ gviews, float* __restrict__ gRcv,
-                                                    float* __restrict__ gtcv, int64_t V, const int32_t* __restrict__ ptr,
-                                                    const int32_t* __restrict__ adj,
-                                                    const unsigned long long* __restrict__ gfix,
-                                                    const float* __restrict__ gface, const int* __restrict__ fflag,
-                                                    float* __restrict__ gverts, float* __restrict__ gcol) {
-  if ((int)blockIdx.x < N) rt_reduce_view(part, vslot, N, bands, gviews, gRcv, gtcv, blockIdx.x);
+__global__ void __launch_bounds__(MR_VGRAD_NT) k_rt_vgrad_b(RtReduce R, int64_t V, const int32_t* __restrict__ ptr,
+                                                            const int32_t* __restrict__ adj,
+                                                            const unsigned long long* __restrict__ gfix,
+                                                            const float* __restrict__ gface, const int* __restrict__ fflag,
+                                                            float* __restrict__ gverts, float* __restrict__ gcol) {
+  if ((int)blockIdx.x < R.N) rt_reduce_view<MR_VGRAD_NT>(R.part, R.vslot, R.N, R.bands, R.gviews, R.gRcv, R.gtcv, blockIdx.x);
   else vgrad_b_block<ACC>(V, nullptr, nullptr, ptr, adj, gfix, gface, fflag, nullptr, 0, gverts, gcol,
-                          (int64_t)blockIdx.x - N);
+                          xcd_block((int64_t)blockIdx.x - R.N, (int64_t)gridDim.x - R.N));
 }
 
 // projection: face_verts[n*F+f][c] = ndc(view n, X); distinct meshes (ff = first union face of

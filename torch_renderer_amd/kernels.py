@@ -516,9 +516,10 @@ def _geom_sig(v, f, R, T, intr, cfg, pose_cv, ranges, stream):
             cfg.max_faces_per_bin, cfg.z_clip, bool(pose_cv), ranges is None, stream)
 
 
-def _blob(kind, cfg, make):
-    """The bytes of one of cfg's ctypes structs (cached by the configuration's values)."""
-    k = (kind, cfg.key())
+def _blob(kind, cfg, make, ckey=None):
+    """The bytes of one of cfg's ctypes structs (cached by the configuration's values; ckey: cfg.key()
+    when the caller already has it)."""
+    k = (kind, cfg.key() if ckey is None else ckey)
     hit = _STRUCT_CACHE.get(k)
     if hit is None:
         if len(_STRUCT_CACHE) > 256:
@@ -547,12 +548,12 @@ def render_views(verts, R, T, faces, intr, cam_centers, cfg: ShadeConfig, tex: T
         cfg = ShadeConfig(**{**cfg.__dict__, "light_kind": 1})
     dev = verts.device
     f, vptr, vadj = mesh_topology(faces, verts.shape[0])
-    rsb = _blob("rb", cfg, cfg.raster_struct)
-    spb = _blob("sb", cfg, cfg.shade_struct)
+    ssig = cfg.key()  # the shading signature (_shade_sig) and the struct caches' key
+    rsb = _blob("rb", cfg, cfg.raster_struct, ssig)
+    spb = _blob("sb", cfg, cfg.shade_struct, ssig)
     stream = _lib.stream_handle(dev).value
     geom = _geom_sig(verts, f, R, T, intr, cfg, pose_cv, ranges, stream)
     ent = _RESHADE["entry"]
-    ssig = _shade_sig(cfg)
     ws = views = None
     slot = 0
     if (_RESHADE["enabled"] and ent is not None and ent["geom"] == geom and ssig not in ent["served"] and

@@ -75,6 +75,8 @@ def _bg_triple(bp):
     work)."""
     bc = bp.background_color
     if not torch.is_tensor(bc):
+        if type(bc) in (tuple, list) and len(bc) == 3 and all(type(x) in (float, int) for x in bc):
+            return (float(bc[0]), float(bc[1]), float(bc[2]))  # the common case: three numbers, no tensor work
         return _triple(bc, None, "BlendParams.background_color")
     key = (bc.data_ptr(), bc._version, tuple(bc.shape), str(bc.device))
     c = bp.__dict__.get("_bg_cache")

@@ -1,7 +1,7 @@
 """Per-workgroup timeline of k_bin_view on the C5 render (mesh_deformer.py:197: one view of the F=81,920 sphere at
 1024x1024, AmbientLights, TexturesVertex), from an experiment build with workgroup stamps:
 python tools/build_variant.py bvstamp -DMR_XP_BV_STAMP, then (GPU)
-MI355R_LIB=exp/bvstamp.so python tools/binview_stamps.py
+MI355R_LIB=exp/bvstamp.so python tools/binview_stamps.py [--fragments]   (--fragments: the fragment pass's launch)
 Roles: binning (one workgroup per band of tile rows), ShadeRec packing, background fill. The launch's span is
 the last end minus the first start; each role's start / end spread says which one is the critical path."""
 import ctypes
@@ -21,8 +21,23 @@ from torch_renderer_amd.transforms import look_at_view_transform  # noqa: E402
 from torch_renderer_amd.utils import subdivided_sphere  # noqa: E402
 
 
+def run_fragments(dev):
+    """The fragment pass of bench.py --mode fragments (cow, 512x512, 64 views: k_bin_view<0, 3>)."""
+    import argparse
+
+    import bench
+    a = argparse.Namespace(gpus=1, steps=3, warmup=1, views=64, size=512, mesh="cow", no_cpu_baseline=True,
+                           no_fragment_pass=False, cpu_views=2, no_secondary=True, eager=True, texture="uv",
+                           mode="fragments")
+    bench.measure_fragments(a, dev, 1, 0)
+    torch.cuda.synchronize()
+
+
 def main():
     dev = torch.device("cuda:0")
+    if "--fragments" in sys.argv:
+        run_fragments(dev)
+        return report()
     sph = subdivided_sphere(2)
     v0, faces = sph.verts_list()[0].to(dev), sph.faces_list()[0].to(dev)
     R, T = look_at_view_transform(dist=2.0, elev=torch.tensor([40.0]), azim=torch.tensor([-140.0]))
@@ -37,6 +52,10 @@ def main():
         img = ren(mesh, cameras=cams, lights=lights)
         img[..., :3].sum().backward()
     torch.cuda.synchronize()
+    report()
+
+
+def report():
     fn = _lib.load().mr_xp_bv_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_int32]
     nw = 4096

@@ -37,7 +37,7 @@ run bench 400 && prof render --no-fragment-pass --no-secondary --steps 20 --warm
 run frag 300 --mode fragments --steps 50 --warmup 10 && prof frag --mode fragments --steps 20 --warmup 5 && \
 run soft 400 --mode soft --size 128 && prof soft --mode soft --size 128 --steps 10 --warmup 3 && \
 run pose 400 --mode pose --steps 20 --warmup 5 && prof pose --mode pose --steps 20 --warmup 5 && \
-run c5 400 --mode c5 --steps 10 --warmup 3 && prof c5 --mode c5 --steps 10 --warmup 3 && \
+run c5 400 --mode c5 --steps 60 --warmup 10 && prof c5 --mode c5 --steps 10 --warmup 3 && \
 run c4 300 --mode gather --mesh dolphin --size 1024 --views 64 --no-cpu-baseline --steps 20 --warmup 5 && \
 MR_BENCH_REHEARSE=1 run rehearse 300 --gpus 2 --no-cpu-baseline --no-fragment-pass --steps 10 --warmup 3 && \
 python -c "import json; d=json.loads(open('gpurun_out/rehearse_${TAG}.json').read().strip().splitlines()[-1]); print('rehearse', d.get('n_gpus'), d.get('allreduce_us'), d.get('allreduce_overlapped_with_forward'), d.get('allreduce_check'))"

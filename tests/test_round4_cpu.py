@@ -36,6 +36,9 @@ def test_camera_key_tracks_edits_replacements_and_new_attributes():
     assert _param_key(c0) == kc
     c0.T[0, 0] = 1.0
     assert _param_key(c0) != kc
+    k4 = _param_key(cams)
+    del cams.extra  # a removed attribute leaves the key (and is not looked up again)
+    assert _param_key(cams) != k4 and len(_param_key(cams)) == len(k4) - 2
 
 
 def test_cached_ndc_affine_follows_the_focal_length():

@@ -34,6 +34,11 @@ class CamerasBase:
         d["_attr_gen"] = d.get("_attr_gen", 0) + 1
         object.__setattr__(self, k, v)
 
+    def __delattr__(self, k):
+        d = self.__dict__
+        d["_attr_gen"] = d.get("_attr_gen", 0) + 1
+        object.__delattr__(self, k)
+
     def __len__(self):
         return max(self.R.shape[0], self.T.shape[0], getattr(self, "_n_intr", 1))
 

@@ -1129,6 +1129,9 @@ static FwdParams make_fwd(const mr_raster_settings_t* s, const BinGeom& g, const
 #ifndef MR_UNIT_ORDER
 #define MR_UNIT_ORDER 1
 #endif
+#ifndef MR_UNIT_ORDER_MIN_VIEWS
+#define MR_UNIT_ORDER_MIN_VIEWS 16
+#endif
 MR_DEV int unit_key(const int4& U) { return U.y < 0 ? 0 : MR_UE + 1 - min(max(U.z, 1), MR_UE); }
 __global__ void __launch_bounds__(1024) k_unit_order(const int4* __restrict__ units, const int* __restrict__ ctr,
                                                      int4* __restrict__ out) {
@@ -1182,8 +1185,10 @@ static int launch_raster_and_shade(FwdParams P, const BinGeom& g, int64_t N, hip
   if (!rgrid_c) rgrid_c = resident_grid(k_tile_raster<MODE, CH, true>, 256, 7);
   if (!sgrid) sgrid = resident_grid(k_shade<MODE, CH>, 256, 6);
   // (the fused render only: in the fragment pass the raster's time is its background stores, and the order's
-  // launch cost more than it saved — fragments 421k -> 405-416k, render 300k -> 301-302k, profiles/r5_unit_order_ab.txt)
-  if (MR_UNIT_ORDER && MODE == 1 && P.units_ws2) {
+  // launch cost more than it saved — fragments 421k -> 405-416k, render 300k -> 301-302k, profiles/r5_unit_order_ab.txt;
+  // and only for batches of MR_UNIT_ORDER_MIN_VIEWS views or more: C5's single view rasters 0.3 us slower without it
+  // and saves the 4.4-us launch, profiles/r6n_c5_ab.txt)
+  if (MR_UNIT_ORDER && MODE == 1 && P.units_ws2 && N >= MR_UNIT_ORDER_MIN_VIEWS) {
     MR_TIMED(KID_UNIT_ORDER, st, (k_unit_order<<<8, 1024, 0, st>>>(P.units, P.ctr, P.units_ws2)));
     MR_CHECK_LAUNCH("k_unit_order");
     P.units = P.units_ws2;

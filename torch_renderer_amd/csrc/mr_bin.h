@@ -920,7 +920,7 @@ MR_DEV int rect_size(uint32_t r) {
 // Band lists for the banded per-view binning of one shared mesh: every record of view n (one thread per
 // face, both triangles of a split face) is appended to the list of each band its tile rectangle meets,
 // one global atomic per (band, workgroup) — so a band's workgroup in k_bin_view reads its ~F / B records
-// instead of all F rectangles of the view (C5: 81,920 faces, one view, 32 bands). The order inside a list
+// instead of all F rectangles of the view (C5: 81,920 faces, one view, 64 bands). The order inside a list
 // is arbitrary; nothing downstream depends on it (the raster's keys are order-free, the backward groups a
 // tile's pixels by record, slots stay in tile order).
 __global__ void __launch_bounds__(1024) k_band_bucket(const uint32_t* __restrict__ rects, int64_t F, int64_t NF, int nq,

@@ -125,7 +125,7 @@ static int num_cus() {
   return cus;
 }
 // Workgroups (bands of tile rows) per view of the per-view binning: enough for the views to cover
-// 1 / MR_BAND_CU_DIV of the CUs (1 view -> 32 bands, 16 views -> 4, 64 views -> 1 on 256 CUs), at
+// 1 / MR_BAND_CU_DIV of the CUs (1 view -> 64 bands, 16 views -> 4, 64 views -> 1 on 256 CUs), at
 // most MR_BANDS_MAX and one tile row per band. The CUs left over stream the background beside the
 // binning: banding 64 views 4 ways starved that share (fragment pass 421k -> 363k frames/s, render
 // 240k -> 223k, profiles/r4f_bands_ab.txt). A pure function of the batch geometry: the backward's

@@ -820,8 +820,12 @@ def secondary_steps(args, dev, world, rank):
     plans = (("pose_step", bench_pose, dict(size=512, views=64, steps=30, warmup=10)),
              ("c5_step", bench_c5, dict(size=1024, views=5, steps=60, warmup=10)),
              ("soft_step", bench_soft, dict(size=128, views=64, steps=10, warmup=3, mesh="cow")))
+    import gc
+
     for name, fn, over in plans:
         torch.cuda.empty_cache()  # (the headline's graph pool and fragment buffers are gone: start each clean)
+        gc.collect()  # the previous workload's garbage collected here, not by a gen-2 pass inside this one's timed
+        # steps (r6n_c5_embed_probe.txt: one such pass in C5's window after C3 cost 8 %)
         sub = argparse.Namespace(**{**vars(args), **over, "no_cpu_baseline": True})
         try:
             out[name] = fn(sub, dev, world, rank, embed=True)

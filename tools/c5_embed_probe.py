@@ -1,6 +1,7 @@
 """Why the C5 step embedded in the default bench run (secondary_steps, after the headline, the fragment pass and
 C3) is slower than bench.py --mode c5 alone: C5 alone twice, then after C3, then after C3 with Python's cyclic
-GC frozen. Experiments only (GPU): python tools/c5_embed_probe.py"""
+GC frozen; or (--after-headline) alone, after the headline line, after the headline and C3. Experiments only (GPU):
+python tools/c5_embed_probe.py [--after-headline]"""
 import argparse
 import gc
 import json
@@ -30,6 +31,20 @@ def main():
                     "gc_objects": len(gc.get_objects())}
         print(tag, json.dumps(res[tag]), flush=True)
 
+    if "--after-headline" in sys.argv:  # the default line's order: headline (HIP graph), fragment pass, C3, C5
+        run("alone")
+        argv = sys.argv
+        sys.argv = ["bench.py", "--no-secondary", "--no-cpu-baseline", "--steps", "20", "--warmup", "5"]
+        bench.main()
+        sys.argv = argv
+        gc.collect()
+        run("after_headline")
+        torch.cuda.empty_cache()
+        bench.bench_pose(pose, dev, 1, 0, embed=True)
+        gc.collect()
+        run("after_headline_pose")
+        print(json.dumps(res))
+        return
     run("alone_1")
     run("alone_2")
     torch.cuda.empty_cache()

@@ -9,6 +9,7 @@
   clears all 27 face-total columns, whatever the first call's texture.
 * Run totals beyond the fixed-point cutoff (upstream gradients scaled so that per-(view, tile) runs reach ~2^28)
   take the float rows: the scaled gradients equal the unscaled ones times the scale.
+* With vertex colours (corner-major 27-column face rows) the geometry-only backward equals the full kernel's.
 """
 import warnings
 
@@ -177,3 +178,42 @@ def test_large_run_totals_take_the_float_rows():
         tol = 1e-5 * b.abs().max().item()
         print(f"[parity] scaled x2^24 grad {nm}: max |g/2^24 - g| = {err:.3e} (tol {tol:.3e})")
         assert torch.isfinite(a).all() and err <= tol, nm
+
+
+@pytest.mark.parametrize("clip", [False, True])
+def test_geometry_only_backward_equals_full_vertex_colours(clip):
+    """With vertex colours (27-column face rows, corner-major since round 6: col_pos / col_rgb / col_nrm) the
+    geometry-only backward places its 9 position values at the full kernel's position columns: vertex and pose
+    gradients equal, bitwise, those of the full kernel given an all-zero RGB gradient, and no colour gradient
+    arrives from either (as test_gpu_round5's untextured case)."""
+    from tests.test_gpu_round5 import _cow_views
+
+    N, H = 4, 160
+    v0, f0, R, T = _cow_views(N, dist=0.4 if clip else 0.7)
+    intr = torch.tensor([[2.0, 0.0, 2.0, 0.0]], device=DEV).expand(N, 4).contiguous()
+    cfg = Kn.ShadeConfig(H=H, W=H, clip=False, z_clip=0.3 if clip else None)
+    cc = torch.zeros(1, 3, device=DEV)
+    g = torch.Generator().manual_seed(5)
+    gD = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)
+    gS = (torch.rand(N, H, H, generator=g) - 0.5).to(DEV)
+    col0 = torch.rand(v0.shape[0], 3, generator=g).to(DEV)
+
+    def run(zero_rgb):
+        v = v0.clone().requires_grad_(True)
+        col = col0.clone().requires_grad_(True)
+        Rg, Tg = R.clone().requires_grad_(True), T.clone().requires_grad_(True)
+        Kn._RESHADE["entry"] = None
+        out = Kn.render_views(v, Rg, Tg, f0, intr, cc, cfg, Kn.TextureArgs(1), vcolors=col)
+        loss = (out["depth"] * gD).sum() + (out["sil"] * gS).sum()
+        if zero_rgb:
+            loss = loss + (out["rgb"] * 0.0).sum()
+        loss.backward()
+        torch.cuda.synchronize()
+        return v.grad, Rg.grad, Tg.grad, col.grad
+
+    geo, full = run(False), run(True)
+    assert geo[0].abs().max() > 0
+    for a, b, nm in zip(geo[:3], full[:3], ("verts", "R", "T")):
+        assert torch.equal(a, b), f"{nm}: geometry-only backward differs from the full kernel's"
+    assert geo[3] is None or geo[3].abs().max() == 0
+    assert full[3] is None or full[3].abs().max() == 0

@@ -45,9 +45,6 @@ MR_DEV float fpow(float a, float b) { return a > 0.0f ? __builtin_amdgcn_exp2f(b
 #define MR_FIX_MAX 16777216.0f  // 2^24
 MR_DEV long long fix_of(float x) { return __float2ll_rn(x * 4294967296.0f); }
 MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)v * (1.0 / 4294967296.0)); }
-// Per-face total component i: the fixed-point sum plus the float-atomic remainder.
-// (rem false: the float remainder rows are all zero and not read — fix_to_f never returns -0, so the
-// sum with a zero remainder is the same bits)
 // Columns of a face's gradient-total row: ACC = 18 holds the three corners' position then normal columns
 // (3 c + k, 9 + 3 c + k); ACC = 27 (vertex colours) keeps each corner's position and colour columns adjacent
 // (6 c + k, 6 c + 3 + k; normals 18 + 3 c + k), so that a vertex gathers one 48-B piece of each incident face's
@@ -55,9 +52,36 @@ MR_DEV float fix_to_f(unsigned long long v) { return (float)((double)(long long)
 template <int ACC> MR_DEV constexpr int col_pos(int c, int k) { return ACC == 27 ? 6 * c + k : 3 * c + k; }
 template <int ACC> MR_DEV constexpr int col_rgb(int c, int k) { return 6 * c + 3 + k; }
 template <int ACC> MR_DEV constexpr int col_nrm(int c, int k) { return ACC == 27 ? 18 + 3 * c + k : 9 + 3 * c + k; }
+// Per-face total component i: the fixed-point sum plus the float-atomic remainder.
+// (rem false: the float remainder rows are all zero and not read — fix_to_f never returns -0, so the
+// sum with a zero remainder is the same bits)
 MR_DEV float fix_total(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i,
                        bool rem = true) {
   return gfix ? (rem ? fix_to_f(gfix[i]) + gflt[i] : fix_to_f(gfix[i])) : gflt[i];
+}
+// NC consecutive totals (components i .. i + NC - 1, NC even or 3), the fixed-point words read 16 B at a time: the
+// vertex gathers' lanes each read a different face row, so every load instruction is ~64 cache-line requests and
+// the C5 gathers were bound by those requests, not by bytes (r6n_pmc_c5.json: 49 MB over ~16 us). Bitwise
+// fix_total's values. (Rows are 8-B aligned: 16-B loads at 8-B alignment, which gfx950's global loads take.)
+typedef unsigned long long mr_u64x2 __attribute__((ext_vector_type(2), aligned(8)));
+template <int NC>
+MR_DEV void fix_totals(const unsigned long long* __restrict__ gfix, const float* __restrict__ gflt, int64_t i, bool rem,
+                       float (&out)[NC]) {
+  if (!gfix) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) out[k] = gflt[i + k];
+    return;
+  }
+  unsigned long long w[NC];
+#pragma unroll
+  for (int k = 0; k + 1 < NC; k += 2) {
+    const mr_u64x2 q = *(const mr_u64x2*)(gfix + i + k);
+    w[k] = q.x;
+    w[k + 1] = q.y;
+  }
+  if (NC & 1) w[NC - 1] = gfix[i + NC - 1];
+#pragma unroll
+  for (int k = 0; k < NC; ++k) out[k] = rem ? fix_to_f(w[k]) + gflt[i + k] : fix_to_f(w[k]);
 }
 
 // std::max/std::min semantics (a < b ? b : a) — NaN handling follows the CPU code.

@@ -63,7 +63,9 @@ MR_DEV void vgrad_a_block(int64_t V, const int32_t* __restrict__ ptr, const int3
   if (act) {
     for (int e = ptr[v] + j; e < ptr[v + 1]; e += MR_VL) {
       const int f = adj[e] >> 2, c = adj[e] & 3;
-      for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_nrm<ACC>(c, k), rem);
+      float t[3];
+      fix_totals<3>(gfix, gface, (int64_t)f * ACC + col_nrm<ACC>(c, 0), rem, t);
+      for (int k = 0; k < 3; ++k) g[k] += t[k];
     }
   }
 #pragma unroll
@@ -128,9 +130,18 @@ MR_DEV void vgrad_b_block(int64_t V, const float* __restrict__ verts, const int3
   const int e0 = act ? ptr[v] + j : 0, e1 = act ? ptr[v + 1] : 0;
   for (int e = e0; e < e1; e += MR_VL) {
     const int f = adj[e] >> 2, c = adj[e] & 3;
-    for (int k = 0; k < 3; ++k) g[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_pos<ACC>(c, k), rem);
-    if (ACC == 27)
-      for (int k = 0; k < 3; ++k) gc[k] += fix_total(gfix, gface, (int64_t)f * ACC + col_rgb<ACC>(c, k), rem);
+    if (ACC == 27) {  // a corner's position and colour columns are adjacent: 48 B in three 16-B loads
+      float t[6];
+      fix_totals<6>(gfix, gface, (int64_t)f * ACC + col_pos<ACC>(c, 0), rem, t);
+      for (int k = 0; k < 3; ++k) {
+        g[k] += t[k];
+        gc[k] += t[3 + k];
+      }
+    } else {
+      float t[3];
+      fix_totals<3>(gfix, gface, (int64_t)f * ACC + col_pos<ACC>(c, 0), rem, t);
+      for (int k = 0; k < 3; ++k) g[k] += t[k];
+    }
     if (use_normals) {
       const int32_t i0 = faces[3 * f], i1 = faces[3 * f + 1], i2 = faces[3 * f + 2];
       float gn[3], a[3], b[3];

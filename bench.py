@@ -1198,7 +1198,18 @@ def bench_c5(args, dev, world, rank, embed=False):
         opt.step()
         it[0] += 1
 
-    elapsed = _time_steps(step, args, dev, world)
+    windows = None
+    if embed:
+        # the default line's C5: the eager caller loop is host-bound on a loaded box, and one host hiccup inside a
+        # single window moved the recorded value by up to 40 % between boxes (r6n-r6r): three windows of
+        # args.steps / 3 steps after the warm-up, the median one reported (all three listed in the line)
+        sub = argparse.Namespace(**{**vars(args), "steps": max(1, args.steps // 3)})
+        again = argparse.Namespace(**{**vars(sub), "warmup": 0})
+        ws = [_time_steps(step, sub if k == 0 else again, dev, world) for k in range(3)]
+        windows = [round(w / sub.steps * 1e3, 4) for w in ws]
+        elapsed = sorted(ws)[1] * args.steps / sub.steps
+    else:
+        elapsed = _time_steps(step, args, dev, world)
     kt = _kernel_times(step, min(args.steps, 10))
     _host_profile(step, dev)
     # host cost of one single-view renderer(...) call as the caller makes it (:197), no synchronisation inside
@@ -1242,6 +1253,7 @@ def bench_c5(args, dev, world, rank, embed=False):
                       f"ico-sphere (F={Fn}, V={Vn}), {H}x{W}, {nper} single-view renders per step, "
                       "mesh_deformer.py:196-215 colour step (backward to colours and positions, SGD)")
         e["host_us_per_render_call"] = round(host_us, 1)
+        e["windows_ms_per_step"] = windows
         return e
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
